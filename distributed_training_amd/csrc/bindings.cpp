@@ -1,0 +1,398 @@
+// Python bindings of the native runtime (_C extension).
+//
+// Every entry point validates device / dtype / contiguity / alignment / shape
+// on the host BEFORE enqueueing a kernel, so a bad call raises in Python
+// instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mlp_fused.h"
+#include "rccl_comm.h"
+
+// ---- launchers implemented in the .hip translation units ----
+hipError_t dta_flat_sgd(const float*, float*, const float*, float*, void*, int64_t, float, float, float, float, float,
+                        int, int, int, hipStream_t);
+hipError_t dta_flat_adam(float*, const float*, float*, float*, float*, void*, int64_t, float*, float, float, float,
+                         float, float, float, int, int, int, int, hipStream_t);
+hipError_t dta_step_inc(float*, hipStream_t);
+hipError_t dta_mt_scale_copy(const void* const*, void* const*, const int64_t*, int, int, int, float, hipStream_t);
+hipError_t dta_flat_sumsq(const float*, int64_t, float*, hipStream_t);
+hipError_t dta_flat_clip(float*, int64_t, const float*, float, hipStream_t);
+hipError_t dta_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
+hipError_t dta_mlp2_fused_step(const dta::MlpArgs*, hipStream_t);
+size_t dta_mlp2_lds_bytes(int64_t, int);
+
+namespace {
+
+hipStream_t pick_stream(int64_t s) {
+  if (s == -1) return c10::hip::getCurrentHIPStream().stream();
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+void hip_ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+void check_gpu(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_f32(const torch::Tensor& t, const char* name, bool aligned16 = true) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+  if (aligned16) TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+float* fptr(const c10::optional<torch::Tensor>& t) {
+  return (t && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+void flat_sgd(torch::Tensor p_in, torch::Tensor p_out, torch::Tensor g, c10::optional<torch::Tensor> mom,
+              c10::optional<torch::Tensor> p_bf16, double lr, double momentum, double dampening, double wd,
+              double grad_scale, bool nesterov, bool maximize, bool first_step, int64_t stream) {
+  check_f32(p_in, "p_in");
+  check_f32(p_out, "p_out");
+  check_f32(g, "grad");
+  const int64_t n = p_in.numel();
+  TORCH_CHECK(p_out.numel() == n && g.numel() == n, "flat_sgd: size mismatch");
+  if (mom && mom->defined()) {
+    check_f32(*mom, "momentum_buffer");
+    TORCH_CHECK(mom->numel() == n, "flat_sgd: momentum size mismatch");
+  }
+  void* pb = nullptr;
+  if (p_bf16 && p_bf16->defined()) {
+    check_gpu(*p_bf16, "p_bf16");
+    TORCH_CHECK(p_bf16->scalar_type() == torch::kBFloat16 && p_bf16->numel() == n, "p_bf16: bf16 of same size");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p_bf16->data_ptr()) % 8 == 0, "p_bf16 must be 8-byte aligned");
+    pb = p_bf16->data_ptr();
+  }
+  hip_ok(dta_flat_sgd(p_in.data_ptr<float>(), p_out.data_ptr<float>(), g.data_ptr<float>(), fptr(mom), pb, n,
+                      (float)lr, (float)momentum, (float)dampening, (float)wd, (float)grad_scale, nesterov, maximize,
+                      first_step, pick_stream(stream)),
+         "flat_sgd");
+}
+
+void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> vmax,
+               c10::optional<torch::Tensor> p_bf16, torch::Tensor step, double lr, double beta1, double beta2,
+               double eps, double wd, double grad_scale, bool adamw, bool maximize, bool amsgrad, bool bump_step,
+               int64_t stream) {
+  check_f32(p, "param");
+  check_f32(g, "grad");
+  check_f32(m, "exp_avg");
+  check_f32(v, "exp_avg_sq");
+  check_f32(step, "step", false);
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "flat_adam: size mismatch");
+  TORCH_CHECK(step.numel() == 1, "step must have one element");
+  if (vmax && vmax->defined()) {
+    check_f32(*vmax, "max_exp_avg_sq");
+    TORCH_CHECK(vmax->numel() == n, "flat_adam: max_exp_avg_sq size mismatch");
+  }
+  TORCH_CHECK(!amsgrad || (vmax && vmax->defined()), "amsgrad needs max_exp_avg_sq");
+  void* pb = nullptr;
+  if (p_bf16 && p_bf16->defined()) {
+    check_gpu(*p_bf16, "p_bf16");
+    TORCH_CHECK(p_bf16->scalar_type() == torch::kBFloat16 && p_bf16->numel() == n, "p_bf16: bf16 of same size");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p_bf16->data_ptr()) % 8 == 0, "p_bf16 must be 8-byte aligned");
+    pb = p_bf16->data_ptr();
+  }
+  hip_ok(dta_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), fptr(vmax),
+                       pb, n, step.data_ptr<float>(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
+                       (float)grad_scale, adamw, maximize, amsgrad, bump_step, pick_stream(stream)),
+         "flat_adam");
+}
+
+void step_inc(torch::Tensor step, int64_t stream) {
+  check_f32(step, "step", false);
+  hip_ok(dta_step_inc(step.data_ptr<float>(), pick_stream(stream)), "step_inc");
+}
+
+int dtype_code(const torch::Tensor& t) {
+  if (t.scalar_type() == torch::kFloat32) return 0;
+  if (t.scalar_type() == torch::kBFloat16) return 1;
+  TORCH_CHECK(false, "multi-tensor ops support float32 / bfloat16 only");
+  return -1;
+}
+
+void mt_scale_copy(std::vector<torch::Tensor> src, std::vector<torch::Tensor> dst, double scale, int64_t stream) {
+  TORCH_CHECK(src.size() == dst.size(), "mt_scale_copy: list length mismatch");
+  if (src.empty()) return;
+  const int sdt = dtype_code(src[0]), ddt = dtype_code(dst[0]);
+  std::vector<const void*> s(src.size());
+  std::vector<void*> d(dst.size());
+  std::vector<int64_t> n(src.size());
+  for (size_t i = 0; i < src.size(); ++i) {
+    check_gpu(src[i], "src");
+    check_gpu(dst[i], "dst");
+    TORCH_CHECK(dtype_code(src[i]) == sdt && dtype_code(dst[i]) == ddt, "mt_scale_copy: mixed dtypes in a list");
+    TORCH_CHECK(src[i].numel() == dst[i].numel(), "mt_scale_copy: size mismatch at ", i);
+    s[i] = src[i].data_ptr();
+    d[i] = dst[i].data_ptr();
+    n[i] = src[i].numel();
+  }
+  hip_ok(dta_mt_scale_copy(s.data(), d.data(), n.data(), (int)src.size(), sdt, ddt, (float)scale,
+                           pick_stream(stream)),
+         "mt_scale_copy");
+}
+
+void flat_sumsq(torch::Tensor x, torch::Tensor out, int64_t stream) {
+  check_f32(x, "x");
+  check_f32(out, "out", false);
+  TORCH_CHECK(out.numel() >= 1, "out must have >= 1 element");
+  hip_ok(dta_flat_sumsq(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), pick_stream(stream)), "flat_sumsq");
+}
+
+void flat_clip(torch::Tensor x, torch::Tensor sumsq, double max_norm, int64_t stream) {
+  check_f32(x, "x", false);
+  check_f32(sumsq, "sumsq", false);
+  hip_ok(dta_flat_clip(x.data_ptr<float>(), x.numel(), sumsq.data_ptr<float>(), (float)max_norm,
+                       pick_stream(stream)),
+         "flat_clip");
+}
+
+void cast_f32_bf16(torch::Tensor src, torch::Tensor dst, int64_t stream) {
+  check_f32(src, "src");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(dst.scalar_type() == torch::kBFloat16 && dst.numel() == src.numel(), "dst must be bf16, same size");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dst.data_ptr()) % 8 == 0, "dst must be 8-byte aligned");
+  hip_ok(dta_cast_f32_bf16(src.data_ptr<float>(), dst.data_ptr(), src.numel(), pick_stream(stream)), "cast");
+}
+
+// ----------------------------- fused MLP step -----------------------------
+void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
+                     torch::Tensor ticket, torch::Tensor loss_ring, torch::Tensor p_in, torch::Tensor p_out,
+                     torch::Tensor g_prev, torch::Tensor g_out, c10::optional<torch::Tensor> mom_in,
+                     c10::optional<torch::Tensor> mom_out, std::vector<int64_t> offsets, int64_t in_dim,
+                     int64_t hidden, int64_t out_dim, int64_t B, int64_t own_tiles, int64_t act, int64_t loss_type,
+                     bool apply_update, double grad_scale, double lr, double momentum, double dampening, double wd,
+                     double prev_grad_scale, bool nesterov, bool maximize, bool first_step, int64_t stream,
+                     c10::optional<torch::Tensor> dbg_stamps) {
+  check_f32(X, "X", false);
+  check_f32(T, "T", false);
+  check_gpu(idx_ring, "idx_ring");
+  TORCH_CHECK(idx_ring.scalar_type() == torch::kInt32 && idx_ring.dim() == 2, "idx_ring: int32 [steps, stride]");
+  check_gpu(cursor, "cursor");
+  TORCH_CHECK(cursor.scalar_type() == torch::kInt32 && cursor.numel() >= 1, "cursor: int32[1]");
+  check_gpu(ticket, "ticket");
+  TORCH_CHECK(ticket.scalar_type() == torch::kInt32 && ticket.numel() >= 1, "ticket: int32[1]");
+  check_f32(loss_ring, "loss_ring", false);
+  for (auto* t : {&p_in, &p_out, &g_prev, &g_out}) check_f32(*t, "flat buffer", false);
+  TORCH_CHECK(offsets.size() == 4, "offsets = [w1, b1, w2, b2]");
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == in_dim, "X must be [N, in_dim]");
+  TORCH_CHECK(T.dim() == 2 && T.size(1) == out_dim && T.size(0) == X.size(0), "T must be [N, out_dim]");
+  TORCH_CHECK(in_dim >= 1 && in_dim <= 31, "fused MLP: in_dim must be in [1, 31]");
+  TORCH_CHECK(out_dim >= 1 && out_dim <= 8, "fused MLP: out_dim must be in [1, 8]");
+  TORCH_CHECK(hidden % 32 == 0 && hidden >= 32, "fused MLP: hidden must be a multiple of 32");
+  TORCH_CHECK(B >= 1 && B <= 128 && B <= idx_ring.size(1), "fused MLP: batch must be in [1, 128] and <= idx stride");
+  TORCH_CHECK(own_tiles >= 1 && own_tiles <= 8, "own_tiles in [1, 8]");
+  const int64_t need = offsets[3] + out_dim;
+  TORCH_CHECK(offsets[0] + hidden * in_dim <= need && offsets[1] + hidden <= need && offsets[2] + out_dim * hidden <= need,
+              "bad flat offsets");
+  const int64_t total = p_in.numel();
+  TORCH_CHECK(offsets[0] == 0 && offsets[1] % 4 == 0 && offsets[2] % 4 == 0 && offsets[3] % 4 == 0 && total % 4 == 0,
+              "fused MLP: flat layout must start W1 at 0 with 16-byte aligned regions");
+  TORCH_CHECK(offsets[0] + hidden * in_dim <= offsets[1] && offsets[1] + hidden <= offsets[2] &&
+                  offsets[2] + out_dim * hidden <= offsets[3] && total >= need && total < (int64_t)1 << 31,
+              "fused MLP: overlapping or oversize flat regions");
+  const int bpad = ((B + 31) / 32 <= 1) ? 32 : (((B + 31) / 32 <= 2) ? 64 : 128);
+  TORCH_CHECK(dta_mlp2_lds_bytes(total, bpad) <= 160 * 1024, "fused MLP: parameters too large for the LDS image");
+  TORCH_CHECK(act >= 0 && act <= 3, "fused MLP: unknown activation code");
+  for (auto* t : {&p_in, &p_out, &g_prev, &g_out}) {
+    TORCH_CHECK(t->numel() == total, "flat buffers must all have the same length");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "flat buffers must be 16-byte aligned");
+  }
+  const bool has_mom = mom_in && mom_in->defined();
+  TORCH_CHECK(has_mom == (mom_out && mom_out->defined()), "mom_in / mom_out must both be given or both None");
+  if (has_mom) {
+    check_f32(*mom_in, "mom_in", false);
+    check_f32(*mom_out, "mom_out", false);
+    TORCH_CHECK(mom_in->numel() == total && mom_out->numel() == total, "momentum buffers: same length as params");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(mom_in->data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(mom_out->data_ptr()) % 16 == 0,
+                "momentum buffers must be 16-byte aligned");
+  }
+  TORCH_CHECK(momentum == 0.0 || has_mom, "momentum > 0 needs momentum buffers");
+  dta::MlpArgs a;
+  a.X = X.data_ptr<float>();
+  a.T = T.data_ptr<float>();
+  a.idx_ring = idx_ring.data_ptr<int>();
+  a.cursor = cursor.data_ptr<int>();
+  a.ticket = reinterpret_cast<unsigned*>(ticket.data_ptr<int>());
+  a.loss_ring = loss_ring.data_ptr<float>();
+  a.p_in = p_in.data_ptr<float>();
+  a.p_out = p_out.data_ptr<float>();
+  a.g_prev = g_prev.data_ptr<float>();
+  a.g_out = g_out.data_ptr<float>();
+  a.mom_in = has_mom ? mom_in->data_ptr<float>() : nullptr;
+  a.mom_out = has_mom ? mom_out->data_ptr<float>() : nullptr;
+  a.o_w1 = offsets[0];
+  a.o_b1 = offsets[1];
+  a.o_w2 = offsets[2];
+  a.o_b2 = offsets[3];
+  a.total = total;
+  a.in_dim = (int)in_dim;
+  a.hidden = (int)hidden;
+  a.out_dim = (int)out_dim;
+  a.B = (int)B;
+  a.ring_steps = (int)idx_ring.size(0);
+  a.idx_stride = (int)idx_ring.size(1);
+  a.loss_len = (int)loss_ring.numel();
+  a.own_tiles = (int)own_tiles;
+  a.act = (int)act;
+  a.loss_type = (int)loss_type;
+  a.apply_update = apply_update ? 1 : 0;
+  a.grad_scale = (float)grad_scale;
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.weight_decay = (float)wd;
+  a.prev_grad_scale = (float)prev_grad_scale;
+  a.nesterov = nesterov;
+  a.maximize = maximize;
+  a.first_step = first_step;
+  a.dbg_stamps = nullptr;
+  if (dbg_stamps && dbg_stamps->defined()) {
+    check_gpu(*dbg_stamps, "dbg_stamps");
+    TORCH_CHECK(dbg_stamps->scalar_type() == torch::kInt64 && dbg_stamps->numel() >= 8 * 64, "dbg_stamps: int64[>=512]");
+    a.dbg_stamps = reinterpret_cast<unsigned long long*>(dbg_stamps->data_ptr<int64_t>());
+  }
+  hip_ok(dta_mlp2_fused_step(&a, pick_stream(stream)), "mlp2_fused_step");
+}
+
+// ----------------------------- RCCL -----------------------------
+ncclDataType_t nccl_dtype(const torch::Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kFloat32: return ncclFloat32;
+    case torch::kBFloat16: return ncclBfloat16;
+    case torch::kFloat16: return ncclFloat16;
+    case torch::kFloat64: return ncclFloat64;
+    case torch::kInt32: return ncclInt32;
+    case torch::kInt64: return ncclInt64;
+    case torch::kUInt8: return ncclUint8;
+    case torch::kInt8: return ncclInt8;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL");
+  }
+  return ncclFloat32;
+}
+
+ncclRedOp_t nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  TORCH_CHECK(false, "unknown reduce op ", op);
+  return ncclSum;
+}
+
+class PyRcclComm {
+ public:
+  PyRcclComm(py::bytes uid, int nranks, int rank, int device)
+      : comm_(std::make_unique<dta::RcclComm>(std::string(uid), nranks, rank, device)) {}
+  void all_reduce(torch::Tensor t, const std::string& op, int64_t stream) {
+    check_gpu(t, "tensor");
+    comm_->all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), pick_stream(stream));
+  }
+  void all_gather(torch::Tensor out, torch::Tensor in, int64_t stream) {
+    check_gpu(out, "out");
+    check_gpu(in, "in");
+    TORCH_CHECK(out.numel() == in.numel() * comm_->size(), "all_gather: out must be world_size x in");
+    TORCH_CHECK(out.scalar_type() == in.scalar_type(), "all_gather: dtype mismatch");
+    comm_->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), pick_stream(stream));
+  }
+  void reduce_scatter(torch::Tensor out, torch::Tensor in, const std::string& op, int64_t stream) {
+    check_gpu(out, "out");
+    check_gpu(in, "in");
+    TORCH_CHECK(in.numel() == out.numel() * comm_->size(), "reduce_scatter: in must be world_size x out");
+    TORCH_CHECK(out.scalar_type() == in.scalar_type(), "reduce_scatter: dtype mismatch");
+    comm_->reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in), nccl_op(op),
+                          pick_stream(stream));
+  }
+  void broadcast(torch::Tensor t, int root, int64_t stream) {
+    check_gpu(t, "tensor");
+    comm_->broadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, pick_stream(stream));
+  }
+  void send(torch::Tensor t, int peer, int64_t stream) {
+    check_gpu(t, "tensor");
+    comm_->send(t.data_ptr(), t.numel(), nccl_dtype(t), peer, pick_stream(stream));
+  }
+  void recv(torch::Tensor t, int peer, int64_t stream) {
+    check_gpu(t, "tensor");
+    comm_->recv(t.data_ptr(), t.numel(), nccl_dtype(t), peer, pick_stream(stream));
+  }
+  // all-to-all of equal chunks: in/out are [world_size * chunk]
+  void all_to_all(torch::Tensor out, torch::Tensor in, int64_t stream) {
+    check_gpu(out, "out");
+    check_gpu(in, "in");
+    const int ws = comm_->size();
+    TORCH_CHECK(in.numel() == out.numel() && in.numel() % ws == 0, "all_to_all: equal, divisible sizes");
+    const int64_t chunk = in.numel() / ws;
+    const size_t esz = in.element_size();
+    hipStream_t st = pick_stream(stream);
+    comm_->group_start();
+    for (int p = 0; p < ws; ++p) {
+      comm_->send(static_cast<char*>(in.data_ptr()) + p * chunk * esz, chunk, nccl_dtype(in), p, st);
+      comm_->recv(static_cast<char*>(out.data_ptr()) + p * chunk * esz, chunk, nccl_dtype(out), p, st);
+    }
+    comm_->group_end();
+  }
+  void group_start() { comm_->group_start(); }
+  void group_end() { comm_->group_end(); }
+  void abort() { comm_->abort(); }
+  void destroy() { comm_.reset(); }
+  int rank() const { return comm_->rank(); }
+  int size() const { return comm_->size(); }
+
+ private:
+  std::unique_ptr<dta::RcclComm> comm_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "distributed_training_amd native runtime (gfx950 HIP kernels + RCCL communicator)";
+  m.def("flat_sgd", &flat_sgd);
+  m.def("flat_adam", &flat_adam);
+  m.def("step_inc", &step_inc);
+  m.def("mt_scale_copy", &mt_scale_copy);
+  m.def("flat_sumsq", &flat_sumsq);
+  m.def("flat_clip", &flat_clip);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("mlp2_fused_step", &mlp2_fused_step, py::arg("X"), py::arg("T"), py::arg("idx_ring"), py::arg("cursor"),
+        py::arg("ticket"), py::arg("loss_ring"), py::arg("p_in"), py::arg("p_out"), py::arg("g_prev"), py::arg("g_out"),
+        py::arg("mom_in"), py::arg("mom_out"), py::arg("offsets"), py::arg("in_dim"), py::arg("hidden"),
+        py::arg("out_dim"), py::arg("B"), py::arg("own_tiles"), py::arg("act"), py::arg("loss_type"),
+        py::arg("apply_update"), py::arg("grad_scale"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"),
+        py::arg("wd"), py::arg("prev_grad_scale"), py::arg("nesterov"), py::arg("maximize"), py::arg("first_step"),
+        py::arg("stream") = -1, py::arg("dbg_stamps") = py::none());
+  m.def("mlp2_lds_bytes", &dta_mlp2_lds_bytes);
+  m.def("rccl_load", &dta::rccl_load);
+  m.def("rccl_loaded", &dta::rccl_loaded);
+  m.def("rccl_unique_id", []() { return py::bytes(dta::rccl_unique_id()); });
+  m.def("rccl_version", []() {
+    int v = 0;
+    if (dta::rccl_loaded()) dta::rccl_api().GetVersion(&v);
+    return v;
+  });
+  py::class_<PyRcclComm>(m, "RcclComm")
+      .def(py::init<py::bytes, int, int, int>())
+      .def("all_reduce", &PyRcclComm::all_reduce)
+      .def("all_gather", &PyRcclComm::all_gather)
+      .def("reduce_scatter", &PyRcclComm::reduce_scatter)
+      .def("broadcast", &PyRcclComm::broadcast)
+      .def("send", &PyRcclComm::send)
+      .def("recv", &PyRcclComm::recv)
+      .def("all_to_all", &PyRcclComm::all_to_all)
+      .def("group_start", &PyRcclComm::group_start)
+      .def("group_end", &PyRcclComm::group_end)
+      .def("abort", &PyRcclComm::abort)
+      .def("destroy", &PyRcclComm::destroy)
+      .def_property_readonly("rank", &PyRcclComm::rank)
+      .def_property_readonly("size", &PyRcclComm::size);
+}

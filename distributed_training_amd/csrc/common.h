@@ -1,0 +1,110 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels.
+//
+// Everything in csrc/ is written directly for gfx950: 64-lane wavefronts,
+// MFMA matrix cores (v_mfma_f32_32x32x16_bf16 / 16x16x32_bf16), 160 KiB LDS.
+// There is no CUDA path and no platform #ifdef: this is CDNA4 code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dta {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+// Plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) at -O3.
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Sum over the 32 lanes that share one half of the wave (lanes 0-31 or 32-63).
+__device__ __forceinline__ float half_wave_sum(float v) {
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Row index of accumulator register `reg` for v_mfma_f32_32x32x16_bf16
+// (column = lane & 31).  cdna_hip_programming.md §3.
+__device__ __forceinline__ int mfma32_row(int reg, int lane) {
+  return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5,
+// "XCD swizzle must be bijective"): blocks that land on one XCD (b % 8 equal)
+// get a contiguous chunk of the logical tile space so they share L2 panels.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nxcd = 8;
+  if (nwg <= nxcd) return orig;
+  const int q = nwg / nxcd, r = nwg % nxcd;
+  const int xcd = orig % nxcd;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / nxcd;
+}
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU_TANH = 2, ACT_SILU = 3 };
+
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_GELU_TANH: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      float t = tanhf(k0 * (x + k1 * x * x * x));
+      return 0.5f * x * (1.f + t);
+    }
+    case ACT_SILU: return x / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+
+// d act(x) / dx
+__device__ __forceinline__ float act_bwd(int act, float x) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_GELU_TANH: {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      float u = k0 * (x + k1 * x * x * x);
+      float t = tanhf(u);
+      float du = k0 * (1.f + 3.f * k1 * x * x);
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+    }
+    case ACT_SILU: {
+      float s = 1.f / (1.f + __expf(-x));
+      return s * (1.f + x * (1.f - s));
+    }
+    default: return 1.f;
+  }
+}
+
+}  // namespace dta
+
+#define DTA_HIP_CHECK(expr)                                                   \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) return _e;                                          \
+  } while (0)

@@ -1,0 +1,162 @@
+"""Thin Python wrapper of the fused 2-layer-MLP train-step kernel
+(``csrc/mlp_fused.hip``) plus its fp32 PyTorch reference.
+
+Flat parameter layout (fp32, each region 64-byte aligned)::
+
+    [ W1 (hidden x in) | b1 (hidden) | W2 (out x hidden) | b2 (out) ]
+
+Names match ``nn.Linear`` state-dict order of the MLP model
+(``models/mlp.py``: ``fc1.weight, fc1.bias, fc2.weight, fc2.bias``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+ACTIVATIONS = {"none": 0, "identity": 0, "relu": 1, "gelu": 2, "gelu_tanh": 2, "silu": 3}
+LOSSES = {"mse": 0, "cross_entropy": 1}
+ALIGN = 16  # floats (64 bytes)
+
+LDS_LIMIT = 160 * 1024
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass(frozen=True)
+class MlpLayout:
+    in_dim: int
+    hidden: int
+    out_dim: int
+    o_w1: int
+    o_b1: int
+    o_w2: int
+    o_b2: int
+    total: int
+
+    @property
+    def offsets(self):
+        return [self.o_w1, self.o_b1, self.o_w2, self.o_b2]
+
+    def views(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        H, I, O = self.hidden, self.in_dim, self.out_dim
+        return {
+            "fc1.weight": flat[self.o_w1:self.o_w1 + H * I].view(H, I),
+            "fc1.bias": flat[self.o_b1:self.o_b1 + H],
+            "fc2.weight": flat[self.o_w2:self.o_w2 + O * H].view(O, H),
+            "fc2.bias": flat[self.o_b2:self.o_b2 + O],
+        }
+
+
+def make_layout(in_dim: int, hidden: int, out_dim: int) -> MlpLayout:
+    o_w1 = 0
+    o_b1 = _align(o_w1 + hidden * in_dim)
+    o_w2 = _align(o_b1 + hidden)
+    o_b2 = _align(o_w2 + out_dim * hidden)
+    total = _align(o_b2 + out_dim)
+    return MlpLayout(in_dim, hidden, out_dim, o_w1, o_b1, o_w2, o_b2, total)
+
+
+def lds_bytes(in_dim: int, hidden: int, out_dim: int, batch: int) -> int:
+    """LDS footprint: fp32 image of the flat params + bf16 X tile + small buffers."""
+    rt = (batch + 31) // 32
+    bpad = 32 if rt <= 1 else (64 if rt <= 2 else 128)
+    total = make_layout(in_dim, hidden, out_dim).total
+    return total * 4 + bpad * 80 + 32 * (bpad + 8) * 2 + 8 * 2 * 32 * 40 * 2 + 3 * bpad * 32 + 32
+
+
+def supported(in_dim: int, hidden: int, out_dim: int, batch: int) -> bool:
+    """Shapes covered by the fused kernel (host mirror of the kernel's limits)."""
+    return (
+        1 <= in_dim <= 31
+        and 1 <= out_dim <= 8
+        and hidden >= 32
+        and hidden % 32 == 0
+        and 1 <= batch <= 128
+        and lds_bytes(in_dim, hidden, out_dim, batch) <= LDS_LIMIT
+    )
+
+
+def fused_step(
+    X, T, idx_ring, cursor, ticket, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+    layout: MlpLayout, batch: int, own_tiles: int, act: str, loss: str, apply_update: bool,
+    grad_scale: float, sgd: Dict[str, float], prev_grad_scale: float, first_step: bool, stream=None,
+    dbg_stamps=None,
+) -> None:
+    C = native()
+    C.mlp2_fused_step(
+        X, T, idx_ring, cursor, ticket, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+        layout.offsets, layout.in_dim, layout.hidden, layout.out_dim, int(batch), int(own_tiles),
+        ACTIVATIONS[act], LOSSES[loss], bool(apply_update), float(grad_scale),
+        float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)), float(sgd.get("dampening", 0.0)),
+        float(sgd.get("weight_decay", 0.0)), float(prev_grad_scale), bool(sgd.get("nesterov", False)),
+        bool(sgd.get("maximize", False)), bool(first_step), -1 if stream is None else int(stream.cuda_stream),
+        dbg_stamps,
+    )
+
+
+def _act(x: torch.Tensor, act: str) -> torch.Tensor:
+    if act == "relu":
+        return F.relu(x)
+    if act in ("gelu", "gelu_tanh"):
+        return F.gelu(x, approximate="tanh")
+    if act == "silu":
+        return F.silu(x)
+    return x
+
+
+def loss_fn(y: torch.Tensor, t: torch.Tensor, loss: str) -> torch.Tensor:
+    if loss == "mse":
+        return F.mse_loss(y, t)
+    return F.cross_entropy(y, t)
+
+
+def reference_step(
+    X: torch.Tensor, T: torch.Tensor, idx: torch.Tensor, params: Dict[str, torch.Tensor], act: str, loss: str,
+    emulate_bf16: bool = False,
+) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """fp32 autograd reference of one step on the gathered batch.
+
+    With ``emulate_bf16`` the forward MFMA operands are rounded to bf16 exactly
+    as the kernel does (X, W1 for layer 1; act(H), W2 for layer 2)."""
+    p = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
+    x = X[idx.long()].float()
+    t = T[idx.long()].float()
+    w1 = p["fc1.weight"]
+    if emulate_bf16:
+        h = x.bfloat16().float() @ w1.bfloat16().float().t() + p["fc1.bias"]
+    else:
+        h = x @ w1.t() + p["fc1.bias"]
+    a = _act(h, act)
+    if emulate_bf16:
+        y = a.bfloat16().float() @ p["fc2.weight"].bfloat16().float().t() + p["fc2.bias"]
+    else:
+        y = a @ p["fc2.weight"].t() + p["fc2.bias"]
+    lv = loss_fn(y, t, loss)
+    lv.backward()
+    return lv.detach(), {k: v.grad.detach() for k, v in p.items()}
+
+
+def apply_sgd_reference(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], sgd: Dict[str, float],
+                        first_step: bool) -> torch.Tensor:
+    """torch.optim.SGD single-tensor math (for tests)."""
+    lr = sgd.get("lr", 1e-3)
+    mom = sgd.get("momentum", 0.0)
+    damp = sgd.get("dampening", 0.0)
+    wd = sgd.get("weight_decay", 0.0)
+    d = -g if sgd.get("maximize", False) else g.clone()
+    if wd:
+        d = d + wd * p
+    if mom:
+        if first_step:
+            buf.copy_(d)
+        else:
+            buf.mul_(mom).add_(d, alpha=1 - damp)
+        d = d + mom * buf if sgd.get("nesterov", False) else buf
+    return p - lr * d
