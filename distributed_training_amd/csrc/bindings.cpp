@@ -56,20 +56,19 @@ float* fptr(const c10::optional<torch::Tensor>& t) {
 void flat_sgd(torch::Tensor p_in, torch::Tensor p_out, torch::Tensor g, c10::optional<torch::Tensor> mom,
               c10::optional<torch::Tensor> p_bf16, double lr, double momentum, double dampening, double wd,
               double grad_scale, bool nesterov, bool maximize, bool first_step, int64_t stream) {
-  check_f32(p_in, "p_in");
-  check_f32(p_out, "p_out");
-  check_f32(g, "grad");
+  check_f32(p_in, "p_in", false);
+  check_f32(p_out, "p_out", false);
+  check_f32(g, "grad", false);
   const int64_t n = p_in.numel();
   TORCH_CHECK(p_out.numel() == n && g.numel() == n, "flat_sgd: size mismatch");
   if (mom && mom->defined()) {
-    check_f32(*mom, "momentum_buffer");
+    check_f32(*mom, "momentum_buffer", false);
     TORCH_CHECK(mom->numel() == n, "flat_sgd: momentum size mismatch");
   }
   void* pb = nullptr;
   if (p_bf16 && p_bf16->defined()) {
     check_gpu(*p_bf16, "p_bf16");
     TORCH_CHECK(p_bf16->scalar_type() == torch::kBFloat16 && p_bf16->numel() == n, "p_bf16: bf16 of same size");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(p_bf16->data_ptr()) % 8 == 0, "p_bf16 must be 8-byte aligned");
     pb = p_bf16->data_ptr();
   }
   hip_ok(dta_flat_sgd(p_in.data_ptr<float>(), p_out.data_ptr<float>(), g.data_ptr<float>(), fptr(mom), pb, n,
@@ -82,16 +81,16 @@ void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
                c10::optional<torch::Tensor> p_bf16, torch::Tensor step, double lr, double beta1, double beta2,
                double eps, double wd, double grad_scale, bool adamw, bool maximize, bool amsgrad, bool bump_step,
                int64_t stream) {
-  check_f32(p, "param");
-  check_f32(g, "grad");
-  check_f32(m, "exp_avg");
-  check_f32(v, "exp_avg_sq");
+  check_f32(p, "param", false);
+  check_f32(g, "grad", false);
+  check_f32(m, "exp_avg", false);
+  check_f32(v, "exp_avg_sq", false);
   check_f32(step, "step", false);
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "flat_adam: size mismatch");
   TORCH_CHECK(step.numel() == 1, "step must have one element");
   if (vmax && vmax->defined()) {
-    check_f32(*vmax, "max_exp_avg_sq");
+    check_f32(*vmax, "max_exp_avg_sq", false);
     TORCH_CHECK(vmax->numel() == n, "flat_adam: max_exp_avg_sq size mismatch");
   }
   TORCH_CHECK(!amsgrad || (vmax && vmax->defined()), "amsgrad needs max_exp_avg_sq");
@@ -99,7 +98,6 @@ void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
   if (p_bf16 && p_bf16->defined()) {
     check_gpu(*p_bf16, "p_bf16");
     TORCH_CHECK(p_bf16->scalar_type() == torch::kBFloat16 && p_bf16->numel() == n, "p_bf16: bf16 of same size");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(p_bf16->data_ptr()) % 8 == 0, "p_bf16 must be 8-byte aligned");
     pb = p_bf16->data_ptr();
   }
   hip_ok(dta_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), fptr(vmax),

@@ -16,7 +16,7 @@ namespace dta {
 
 struct SgdHyper {
   float lr, momentum, dampening, weight_decay, grad_scale;
-  int nesterov, maximize, first_step;
+  int nesterov, maximize, first_step, vec;
 };
 
 __device__ __forceinline__ float sgd_one(float p, float g, float* mbuf, const SgdHyper& h) {
@@ -35,7 +35,7 @@ __device__ __forceinline__ float sgd_one(float p, float g, float* mbuf, const Sg
 __global__ void __launch_bounds__(256) flat_sgd_kernel(const float* __restrict__ p_in, float* p_out,
                                                        const float* __restrict__ g, float* mom,
                                                        bf16* __restrict__ p_bf16, int64_t n, SgdHyper h) {
-  const int64_t n4 = n >> 2;
+  const int64_t n4 = h.vec ? (n >> 2) : 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 p = reinterpret_cast<const float4*>(p_in)[i];
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) flat_sgd_kernel(const float* __restrict__
 
 struct AdamHyper {
   float lr, beta1, beta2, eps, weight_decay, grad_scale;
-  int adamw, maximize, amsgrad;
+  int adamw, maximize, amsgrad, vec;
 };
 
 __device__ __forceinline__ float adam_one(float p, float g, float* m, float* v, float* vmax, float bc1,
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, c
   const float bc1 = 1.f - powf(h.beta1, t);
   const float bc2_sqrt = sqrtf(1.f - powf(h.beta2, t));
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n4 = n >> 2;
+  const int64_t n4 = h.vec ? (n >> 2) : 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
     float4 gg = reinterpret_cast<const float4*>(g)[i];
@@ -224,7 +224,9 @@ hipError_t dta_flat_sgd(const float* p_in, float* p_out, const float* g, float* 
                         float lr, float momentum, float dampening, float wd, float grad_scale, int nesterov,
                         int maximize, int first_step, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  SgdHyper h{lr, momentum, dampening, wd, grad_scale, nesterov, maximize, first_step};
+  auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) % a) == 0; };
+  const int vec = al(p_in, 16) && al(p_out, 16) && al(g, 16) && al(mom, 16) && al(p_bf16, 8);
+  SgdHyper h{lr, momentum, dampening, wd, grad_scale, nesterov, maximize, first_step, vec};
   hipLaunchKernelGGL(flat_sgd_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p_in, p_out, g, mom,
                      reinterpret_cast<bf16*>(p_bf16), n, h);
   return hipGetLastError();
@@ -235,7 +237,9 @@ hipError_t dta_flat_adam(float* p, const float* g, float* m, float* v, float* vm
                          int adamw, int maximize, int amsgrad, int bump_step, hipStream_t st) {
   if (bump_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   if (n <= 0) return hipGetLastError();
-  AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad};
+  auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) % a) == 0; };
+  const int vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
+  AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad, vec};
   hipLaunchKernelGGL(flat_adam_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, m, v, vmax,
                      reinterpret_cast<bf16*>(p_bf16), n, step, h);
   return hipGetLastError();

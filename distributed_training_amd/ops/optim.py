@@ -1,0 +1,266 @@
+"""Fused optimizers (drop-in ``torch.optim.SGD`` / ``AdamW`` / ``Adam``).
+
+GPU parameters are updated by the hand-written HIP kernels of
+``csrc/optim.hip``.  When the parameters belong to a :class:`FlatParamGroup`
+(DDP/FSDP engines) the whole group is updated by ONE launch over the flat
+buffer, including the fp32-master -> bf16 compute copy under mixed precision.
+CPU parameters (gloo plumbing path) use the same math in plain PyTorch.
+
+Semantics follow torch.optim exactly (tested against it), so the reference's
+``torch.optim.SGD(model.parameters(), lr=cfg.train.learning_rate)``
+(src/distributed_trainer.py:200) maps 1:1 onto :class:`FusedSGD`.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from . import native
+
+
+def cast_into(src: torch.Tensor, dst: torch.Tensor) -> None:
+    if src.is_cuda and src.dtype == torch.float32 and dst.dtype == torch.bfloat16:
+        native().cast_f32_bf16(src, dst, -1)
+    else:
+        dst.copy_(src)
+
+
+def _grad32(fg_grad: torch.Tensor) -> torch.Tensor:
+    return fg_grad if fg_grad.dtype == torch.float32 else fg_grad.float()
+
+
+def _split_params(group_params):
+    flats: Dict[int, list] = {}
+    flat_objs = {}
+    singles = []
+    for p in group_params:
+        tag = getattr(p, "_dta_flat", None)
+        if tag is not None and p.is_cuda:
+            fg = tag[0]
+            flats.setdefault(id(fg), []).append(p)
+            flat_objs[id(fg)] = fg
+        else:
+            singles.append(p)
+    return [(flat_objs[k], v) for k, v in flats.items()], singles
+
+
+def _sgd_ref(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], lr, momentum, dampening, wd,
+             nesterov, maximize, first) -> None:
+    d = -g if maximize else g
+    if wd:
+        d = d.add(p, alpha=wd)
+    if momentum:
+        if first:
+            buf.copy_(d)
+        else:
+            buf.mul_(momentum).add_(d, alpha=1 - dampening)
+        d = d.add(buf, alpha=momentum) if nesterov else buf
+    p.add_(d, alpha=-lr)
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov, maximize=maximize)
+        super().__init__(params, defaults)
+        self._flat_state: Dict[int, dict] = {}
+
+    def hyper(self, group=None) -> dict:
+        g = group or self.param_groups[0]
+        return {k: g[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov", "maximize")}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            lr, mom, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]
+            nest, maxi = group["nesterov"], group["maximize"]
+            flats, singles = _split_params(group["params"])
+            for fg, ps in flats:
+                if len(ps) == len(fg.params):
+                    st = self._flat_state.setdefault(id(fg), {"first": True})
+                    if mom and "mom" not in st:
+                        st["mom"] = torch.zeros_like(fg.master)
+                        for i, p in enumerate(fg.params):
+                            self.state[p]["momentum_buffer"] = fg._view(st["mom"], i)
+                    pb = fg.compute if fg.mixed else None
+                    native().flat_sgd(fg.master, fg.master, _grad32(fg.grad), st.get("mom"), pb, lr, mom, damp, wd,
+                                      1.0, nest, maxi, st["first"], -1)
+                    st["first"] = False
+                else:
+                    for p in ps:
+                        self._single_gpu(fg, p, lr, mom, damp, wd, nest, maxi)
+            for p in singles:
+                if p.grad is None:
+                    continue
+                state = self.state[p]
+                first = "momentum_buffer" not in state or state["momentum_buffer"] is None
+                if mom and first:
+                    state["momentum_buffer"] = torch.zeros_like(p, dtype=torch.float32)
+                buf = state.get("momentum_buffer") if mom else None
+                if p.is_cuda:
+                    if p.dtype != torch.float32:
+                        raise TypeError("FusedSGD on GPU needs fp32 parameters (or a FlatParamGroup with a master)")
+                    native().flat_sgd(p.view(-1), p.view(-1), p.grad.float().contiguous().view(-1),
+                                      None if buf is None else buf.view(-1), None, lr, mom, damp, wd, 1.0, nest,
+                                      maxi, first, -1)
+                else:
+                    _sgd_ref(p, p.grad, buf, lr, mom, damp, wd, nest, maxi, first)
+        return loss
+
+    def _single_gpu(self, fg, p, lr, mom, damp, wd, nest, maxi):
+        i = fg.index_of(p)
+        state = self.state[p]
+        first = "momentum_buffer" not in state or state["momentum_buffer"] is None
+        if mom and first:
+            state["momentum_buffer"] = torch.zeros(fg.numels[i], device=p.device)
+        buf = state.get("momentum_buffer") if mom else None
+        m = fg.master_view(i).view(-1)
+        g = fg.grad_view(i).view(-1).float()
+        pb = fg.param_view(i).view(-1) if fg.mixed else None
+        native().flat_sgd(m, m, g, None if buf is None else buf.view(-1), pb, lr, mom, damp, wd, 1.0, nest, maxi,
+                          first, -1)
+
+    def zero_grad(self, set_to_none: bool = True):
+        flats_done = set()
+        for group in self.param_groups:
+            flats, singles = _split_params(group["params"])
+            for fg, _ in flats:
+                if id(fg) not in flats_done:
+                    fg.zero_grad()  # keep the grads as flat views
+                    flats_done.add(id(fg))
+            for p in singles:
+                tag = getattr(p, "_dta_flat", None)
+                if tag is not None:
+                    tag[0].zero_grad()
+                elif p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()
+
+
+def _adam_ref(p, g, m, v, vmax, step, lr, b1, b2, eps, wd, adamw, maximize, amsgrad):
+    g = -g if maximize else g
+    if wd:
+        if adamw:
+            p.mul_(1 - lr * wd)
+        else:
+            g = g.add(p, alpha=wd)
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    vv = v
+    if amsgrad:
+        torch.maximum(vmax, v, out=vmax)
+        vv = vmax
+    denom = (vv.sqrt() / (bc2 ** 0.5)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """AdamW (``adamw=True``, default) or Adam with L2 (``adamw=False``)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 amsgrad: bool = False, maximize: bool = False, adamw: bool = True):
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
+                        maximize=maximize, adamw=adamw)
+        super().__init__(params, defaults)
+        self._flat_state: Dict[int, dict] = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+            ams, maxi, adamw = group["amsgrad"], group["maximize"], group["adamw"]
+            flats, singles = _split_params(group["params"])
+            for fg, ps in flats:
+                if len(ps) != len(fg.params):
+                    raise ValueError("FusedAdamW: a FlatParamGroup must be optimised as a whole by one param group")
+                st = self._flat_state.get(id(fg))
+                if st is None:
+                    st = {"m": torch.zeros_like(fg.master), "v": torch.zeros_like(fg.master),
+                          "vmax": torch.zeros_like(fg.master) if ams else None,
+                          "step": torch.zeros(1, device=fg.master.device)}
+                    self._flat_state[id(fg)] = st
+                    for i, p in enumerate(fg.params):
+                        self.state[p]["exp_avg"] = fg._view(st["m"], i)
+                        self.state[p]["exp_avg_sq"] = fg._view(st["v"], i)
+                        self.state[p]["step"] = st["step"]
+                        if ams:
+                            self.state[p]["max_exp_avg_sq"] = fg._view(st["vmax"], i)
+                pb = fg.compute if fg.mixed else None
+                native().flat_adam(fg.master, _grad32(fg.grad), st["m"], st["v"], st["vmax"], pb, st["step"], lr, b1,
+                                   b2, eps, wd, 1.0, adamw, maxi, ams, True, -1)
+            for p in singles:
+                if p.grad is None:
+                    continue
+                state = self.state[p]
+                if not state:
+                    state["exp_avg"] = torch.zeros_like(p, dtype=torch.float32)
+                    state["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
+                    state["step"] = torch.zeros(1, device=p.device) if p.is_cuda else torch.zeros(())
+                    if ams:
+                        state["max_exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32)
+                if p.is_cuda:
+                    if p.dtype != torch.float32:
+                        raise TypeError("FusedAdamW on GPU needs fp32 parameters (or a FlatParamGroup with a master)")
+                    native().flat_adam(p.view(-1), p.grad.float().contiguous().view(-1), state["exp_avg"].view(-1),
+                                       state["exp_avg_sq"].view(-1),
+                                       state["max_exp_avg_sq"].view(-1) if ams else None, None, state["step"], lr,
+                                       b1, b2, eps, wd, 1.0, adamw, maxi, ams, True, -1)
+                else:
+                    state["step"] += 1
+                    _adam_ref(p, p.grad, state["exp_avg"], state["exp_avg_sq"], state.get("max_exp_avg_sq"),
+                              float(state["step"]), lr, b1, b2, eps, wd, adamw, maxi, ams)
+        return loss
+
+    zero_grad = FusedSGD.zero_grad
+
+
+def build_optimizer(name: str, params, **kw) -> torch.optim.Optimizer:
+    name = name.lower()
+    if name == "sgd":
+        return FusedSGD(params, **kw)
+    if name == "adamw":
+        return FusedAdamW(params, adamw=True, **kw)
+    if name == "adam":
+        return FusedAdamW(params, adamw=False, **{"weight_decay": 0.0, **kw})
+    raise ValueError(f"unknown optimizer {name!r}")
+
+
+def optimizer_hparams(opt: torch.optim.Optimizer) -> Dict[str, object]:
+    """Hyper-parameters of param group 0 (works for torch and fused optimizers)."""
+    g = opt.param_groups[0]
+    return {k: v for k, v in g.items() if k != "params"}
+
+
+def same_kind_optimizer(opt: torch.optim.Optimizer, params: List[torch.nn.Parameter]) -> torch.optim.Optimizer:
+    """Rebuild ``opt`` (same class / hyper-parameters) over ``params``."""
+    hp = optimizer_hparams(opt)
+    cls = type(opt)
+    if cls is torch.optim.SGD:
+        keep = {k: hp[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov", "maximize") if k in hp}
+        return FusedSGD(params, **keep)
+    if cls in (torch.optim.AdamW, torch.optim.Adam):
+        keep = {k: hp[k] for k in ("lr", "betas", "eps", "weight_decay", "amsgrad", "maximize") if k in hp}
+        return FusedAdamW(params, adamw=cls is torch.optim.AdamW, **keep)
+    if cls is FusedSGD:
+        keep = {k: hp[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov", "maximize")}
+        return FusedSGD(params, **keep)
+    if cls is FusedAdamW:
+        keep = {k: hp[k] for k in ("lr", "betas", "eps", "weight_decay", "amsgrad", "maximize", "adamw")}
+        return FusedAdamW(params, **keep)
+    return cls(params, **hp)

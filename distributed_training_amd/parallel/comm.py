@@ -1,0 +1,230 @@
+"""Collective communication layer.
+
+Two implementations behind one small interface:
+
+* :class:`RcclComm` -- the GPU hot path.  A native RCCL communicator
+  (``csrc/rccl_comm.cpp``) bootstrapped through torchrun's TCPStore, with its
+  own high-priority HIP stream.  Collectives are enqueued on that stream after
+  an event wait on the producing (compute) stream, so they overlap with the
+  rest of backward; :class:`CommWork.wait` makes the consumer stream wait on
+  the comm stream (no host synchronisation) and the whole thing can be
+  captured into a hipGraph.
+* :class:`TorchComm` -- ``torch.distributed`` (gloo on CPU, or any backend);
+  used for the CPU plumbing path and as the control plane.
+
+Reference parity: replaces the implicit c10d NCCL/Gloo process group of
+``src/distributed_trainer.py:61-62`` and the explicit ``dist.broadcast`` /
+``dist.all_reduce`` of ``src/playground/ddp_script.py:120-121,149-153``
+(SURVEY.md §2.4, §2.7).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+        "prod": dist.ReduceOp.PRODUCT}
+
+
+class CommWork:
+    """Handle of an asynchronous collective."""
+
+    def __init__(self, torch_work=None, event=None, post=None):
+        self._work = torch_work
+        self._event = event
+        self._post = post
+        self._done = False
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        if self._done:
+            return
+        if self._work is not None:
+            self._work.wait()
+        if self._event is not None:
+            (stream or torch.cuda.current_stream()).wait_event(self._event)
+        if self._post is not None:
+            self._post()
+        self._done = True
+
+
+class Communicator:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+    name = "base"
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
+        raise NotImplementedError
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Optional[CommWork]:
+        raise NotImplementedError
+
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum",
+                            async_op: bool = False) -> Optional[CommWork]:
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False) -> Optional[CommWork]:
+        raise NotImplementedError
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    def supports_avg(self) -> bool:
+        return False
+
+
+class TorchComm(Communicator):
+    """torch.distributed-backed communicator (gloo on CPU)."""
+
+    name = "torch"
+
+    def __init__(self, group=None, device: Optional[torch.device] = None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.device = device or torch.device("cpu")
+        self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
+
+    def _w(self, work, async_op):
+        if async_op:
+            return CommWork(torch_work=work)
+        return None
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        if self.world_size == 1:
+            return CommWork() if async_op else None
+        if op == "avg":
+            t.div_(self.world_size)
+            op = "sum"
+        work = dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=async_op)
+        return self._w(work, async_op)
+
+    def all_gather_into(self, out, inp, async_op=False):
+        if self.world_size == 1:
+            if out.data_ptr() != inp.data_ptr():
+                out.view(-1).copy_(inp.view(-1))
+            return CommWork() if async_op else None
+        work = dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+        return self._w(work, async_op)
+
+    def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
+        if self.world_size == 1:
+            if out.data_ptr() != inp.data_ptr():
+                out.view(-1).copy_(inp.view(-1))
+            return CommWork() if async_op else None
+        post = None
+        if op == "avg":
+            op = "sum"
+            ws = self.world_size
+            post = lambda: out.div_(ws)  # noqa: E731
+        work = dist.reduce_scatter_tensor(out, inp, op=_OPS[op], group=self.group, async_op=async_op)
+        if async_op:
+            return CommWork(torch_work=work, post=post)
+        if post:
+            post()
+        return None
+
+    def broadcast(self, t, src=0, async_op=False):
+        if self.world_size == 1:
+            return CommWork() if async_op else None
+        work = dist.broadcast(t, src=src, group=self.group, async_op=async_op)
+        return self._w(work, async_op)
+
+    def all_to_all_single(self, out, inp):
+        if self.world_size == 1:
+            out.copy_(inp)
+            return
+        dist.all_to_all_single(out, inp, group=self.group)
+
+    def barrier(self):
+        if self.world_size > 1:
+            dist.barrier(group=self.group)
+
+
+class RcclComm(Communicator):
+    """Native RCCL communicator on a dedicated HIP stream (GPU hot path)."""
+
+    name = "rccl"
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
+                 stream_priority: int = -1):
+        from ..ops import ensure_rccl
+
+        C = ensure_rccl()
+        self.rank, self.world_size, self.device = rank, world_size, device
+        key = f"dta_rccl_uid/{tag}"
+        if store is None and dist.is_initialized():
+            store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            uid = C.rccl_unique_id()
+            if store is not None:
+                store.set(key, uid)
+        else:
+            if store is None:
+                raise RuntimeError("RcclComm needs a store (torch.distributed initialised) for world_size > 1")
+            uid = store.get(key)
+        self._comm = C.RcclComm(uid, world_size, rank, device.index if device.index is not None else 0)
+        # dedicated high-priority stream for collectives (lower number = higher priority)
+        self.stream = torch.cuda.Stream(device=device, priority=stream_priority)
+
+    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor]) -> Optional[CommWork]:
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        fn(int(self.stream.cuda_stream))
+        for t in tensors:  # keep the caching allocator from recycling the memory early
+            t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        work = CommWork(event=ev)
+        if async_op:
+            return work
+        work.wait(cur)
+        return None
+
+    def supports_avg(self) -> bool:
+        return True
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t])
+
+    def all_gather_into(self, out, inp, async_op=False):
+        return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp])
+
+    def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
+        return self._enqueue(lambda s: self._comm.reduce_scatter(out, inp, op, s), async_op, [out, inp])
+
+    def broadcast(self, t, src=0, async_op=False):
+        return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t])
+
+    def all_to_all_single(self, out, inp):
+        self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp])
+
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
+        """Enqueue on ``stream`` (default: current) with no stream hop: used
+        inside hipGraph-captured step programs."""
+        s = stream or torch.cuda.current_stream(self.device)
+        self._comm.all_reduce(t, op, int(s.cuda_stream))
+
+    def barrier(self):
+        x = torch.zeros(1, device=self.device)
+        self.all_reduce(x)
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def destroy(self):
+        self._comm.destroy()
+
+
+def make_comm(device: torch.device, prefer: str = "auto", group=None) -> Communicator:
+    """Pick the communicator for ``device``: native RCCL for GPU tensors
+    (``prefer`` = auto|rccl), torch.distributed otherwise."""
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    ws = dist.get_world_size() if dist.is_initialized() else 1
+    if device.type == "cuda" and prefer in ("auto", "rccl") and os.environ.get("DTA_COMM", "") != "torch":
+        return RcclComm(rank, ws, device)
+    return TorchComm(group=group, device=device)

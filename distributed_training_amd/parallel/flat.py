@@ -1,0 +1,164 @@
+"""Flat, HBM-resident parameter / gradient storage.
+
+MI355X-first layout: every trainable parameter of a module lives as a view
+into ONE contiguous fp32 master buffer (and, under bf16 mixed precision, one
+bf16 compute buffer), and every gradient is a view into ONE contiguous
+gradient buffer.  Consequences:
+
+* DDP buckets are plain slices of the gradient buffer ("grads as bucket
+  views"): no flatten/unflatten copies (the reference's DDP Reducer copies
+  grad x 1/ws into the bucket and back);
+* the fused optimizer updates the whole model with ONE kernel over the flat
+  buffer (fp32 master -> bf16 compute copy in the same pass);
+* every region starts on a 64-byte boundary so kernels use 16-byte accesses.
+
+Parameters keep their identity (``nn.Parameter`` objects are not replaced:
+only ``.data`` is re-pointed), so an optimizer created before wrapping -- as
+the reference does (src/distributed_trainer.py:195-201 creates SGD before
+Trainer wraps the model) -- keeps working.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+ALIGN_ELEMS = 16
+
+
+def _align(n: int, a: int = ALIGN_ELEMS) -> int:
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class Bucket:
+    index: int
+    start: int            # element offset in the flat buffers
+    end: int
+    param_ids: List[int]  # indices into FlatParamGroup.params
+
+
+class FlatParamGroup:
+    def __init__(self, params: Sequence[torch.nn.Parameter], device: torch.device,
+                 param_dtype: torch.dtype = torch.float32, grad_dtype: Optional[torch.dtype] = None,
+                 names: Optional[Sequence[str]] = None):
+        self.params: List[torch.nn.Parameter] = list(params)
+        self.names = list(names) if names is not None else [f"p{i}" for i in range(len(self.params))]
+        self.device = device
+        self.param_dtype = param_dtype
+        self.grad_dtype = grad_dtype or param_dtype
+        self.shapes = [tuple(p.shape) for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        self.offsets: List[int] = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off = _align(off + n)
+        self.total = max(off, ALIGN_ELEMS)
+        self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                self.master[o:o + n].copy_(p.detach().reshape(-1).to(torch.float32))
+        self.mixed = param_dtype != torch.float32
+        self.compute = self.master if not self.mixed else self.master.to(param_dtype)
+        self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=device)
+        for i, p in enumerate(self.params):
+            p.data = self.param_view(i)
+            p.grad = self.grad_view(i)
+            p._dta_flat = (self, i)  # noqa: SLF001 - tag read by the fused optimizers
+
+    # -------------------------------------------------------------- views
+    def _view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
+        o, n = self.offsets[i], self.numels[i]
+        return buf[o:o + n].view(self.shapes[i])
+
+    def param_view(self, i: int) -> torch.Tensor:
+        return self._view(self.compute, i)
+
+    def master_view(self, i: int) -> torch.Tensor:
+        return self._view(self.master, i)
+
+    def grad_view(self, i: int) -> torch.Tensor:
+        return self._view(self.grad, i)
+
+    def index_of(self, p: torch.nn.Parameter) -> int:
+        tag = getattr(p, "_dta_flat", None)
+        if tag is None or tag[0] is not self:
+            raise KeyError("parameter does not belong to this flat group")
+        return tag[1]
+
+    # ------------------------------------------------------------ helpers
+    def rebind_grad(self, i: int) -> None:
+        """Make ``params[i].grad`` the flat view again (after a torch optimizer
+        set it to None or autograd stole a fresh tensor)."""
+        p = self.params[i]
+        view = self.grad_view(i)
+        g = p.grad
+        if g is None:
+            view.zero_()
+        elif g.data_ptr() != view.data_ptr():
+            view.copy_(g)
+        p.grad = view
+
+    def grad_is_view(self, i: int) -> bool:
+        g = self.params[i].grad
+        return g is not None and g.data_ptr() == self.grad_view(i).data_ptr()
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+        for i, p in enumerate(self.params):
+            if p.grad is None or p.grad.data_ptr() != self.grad_view(i).data_ptr():
+                p.grad = self.grad_view(i)
+
+    def sync_compute_from_master(self) -> None:
+        if self.mixed:
+            from ..ops.optim import cast_into
+
+            cast_into(self.master, self.compute)
+
+    def sync_master_from_compute(self) -> None:
+        if self.mixed:
+            self.master.copy_(self.compute.float())
+
+    def make_buckets(self, order: Sequence[int], cap_bytes: int, first_cap_bytes: int) -> List[Bucket]:
+        """Contiguous buckets over the flat buffer (params are laid out in
+        ``order``, which callers choose as reverse registration order so the
+        first bucket fills first during backward)."""
+        esize = torch.empty((), dtype=self.grad_dtype).element_size()
+        buckets: List[Bucket] = []
+        cur: List[int] = []
+        start = None
+        cap = first_cap_bytes
+        for i in order:
+            o, n = self.offsets[i], self.numels[i]
+            if start is None:
+                start = o
+            cur.append(i)
+            end = _align(o + n)
+            if (end - start) * esize >= cap:
+                buckets.append(Bucket(len(buckets), start, end, cur))
+                cur, start, cap = [], None, cap_bytes
+        if cur:
+            end = _align(self.offsets[cur[-1]] + self.numels[cur[-1]])
+            buckets.append(Bucket(len(buckets), start, end, cur))
+        return buckets
+
+
+def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]], device: torch.device,
+                     param_dtype=torch.float32, grad_dtype=None, reverse: bool = True) -> FlatParamGroup:
+    items = list(params_with_names)
+    if reverse:
+        items = items[::-1]
+    names = [n for n, _ in items]
+    params = [p for _, p in items]
+    return FlatParamGroup(params, device, param_dtype=param_dtype, grad_dtype=grad_dtype, names=names)
+
+
+def param_flat_tags(params) -> Dict[int, Tuple[FlatParamGroup, int]]:
+    out = {}
+    for p in params:
+        tag = getattr(p, "_dta_flat", None)
+        if tag is not None:
+            out[id(p)] = tag
+    return out
