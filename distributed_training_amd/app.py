@@ -1,0 +1,136 @@
+"""Application layer: config -> objects -> training (the Hydra ``main``).
+
+Reference: ``load_train_objs`` (src/distributed_trainer.py:195-201),
+``prepare_dataloader`` (:204-211) and ``main`` (:243-276).  ``main`` keeps the
+reference flow and log lines (``"Training failed: ..."`` then re-raise;
+``destroy_process_group`` in ``finally``).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Tuple
+
+import torch
+from torch.utils.data import Dataset
+
+from .data.datasets import DeviceDataLoader, MyTrainDataset, SyntheticTokens
+from .engine.trainer import Trainer, TrainingConfig
+from .parallel.env import DistributedEnvironment
+from .parallel.sampler import DistributedSampler
+from .utils.logging_utils import setup_logging
+
+logger = logging.getLogger("distributed_training_amd.trainer")
+
+
+def _get(node, key, default=None):
+    if node is None:
+        return default
+    if hasattr(node, "get"):
+        return node.get(key, default)
+    return getattr(node, key, default)
+
+
+def build_model(cfg_model) -> torch.nn.Module:
+    name = str(_get(cfg_model, "name", "") or "")
+    if name in ("gpt2", "gpt2_small"):
+        from .models.gpt2 import GPT2, GPT2Config
+
+        return GPT2(GPT2Config.from_cfg(cfg_model))
+    if name in ("llama", "llama3", "llama3_8b"):
+        from .models.llama import Llama, LlamaConfig
+
+        return Llama(LlamaConfig.from_cfg(cfg_model))
+    from .models.mlp import build_mlp
+
+    return build_mlp(cfg_model)
+
+
+def build_optimizer(cfg_train, params):
+    from .ops.optim import build_optimizer as _b
+
+    name = str(_get(cfg_train, "optimizer", "sgd"))
+    lr = float(_get(cfg_train, "learning_rate", 1e-3))
+    wd = float(_get(cfg_train, "weight_decay", 0.0) or 0.0)
+    if name == "sgd":
+        return _b("sgd", params, lr=lr, momentum=float(_get(cfg_train, "momentum", 0.0) or 0.0), weight_decay=wd)
+    betas = tuple(_get(cfg_train, "betas", (0.9, 0.95)))
+    return _b(name, params, lr=lr, betas=betas, weight_decay=wd)
+
+
+def load_train_objs(cfg) -> Tuple[Dataset, torch.nn.Module, torch.optim.Optimizer]:
+    seed = _get(cfg.train, "seed", None)
+    if seed is not None:
+        torch.manual_seed(int(seed))
+    model = build_model(cfg.model)
+    if hasattr(model, "vocab_size"):
+        train_set = SyntheticTokens(int(cfg.train.dataset_size), int(_get(cfg.train, "seq_len", 1024)),
+                                    model.vocab_size, seed=int(seed or 0))
+    else:
+        train_set = MyTrainDataset(cfg.train.dataset_size, int(_get(cfg.model, "input_size", 20)),
+                                   int(_get(cfg.model, "output_size", 1)))
+    optimizer = build_optimizer(cfg.train, model.parameters())
+    return train_set, model, optimizer
+
+
+def prepare_dataloader(dataset: Dataset, batch_size: int) -> DeviceDataLoader:
+    return DeviceDataLoader(dataset, batch_size=batch_size, sampler=DistributedSampler(dataset))
+
+
+def _wrap_policy(name, model):
+    if not name:
+        return None
+    if name == "block":
+        return getattr(model, "block_class", None) and {model.block_class}
+    return None
+
+
+def training_config_from(cfg, model=None) -> TrainingConfig:
+    t = cfg.train
+    return TrainingConfig(
+        max_epochs=t.total_epochs,
+        save_every=t.save_every,
+        batch_size=t.batch_size,
+        learning_rate=t.learning_rate,
+        snapshot_path=t.snapshot_path,
+        device=_get(t, "device", "auto"),
+        parallel_strategy=_get(t, "parallel_strategy", "ddp"),
+        loss=_get(t, "loss", "cross_entropy"),
+        fused_step=bool(_get(t, "fused_step", True)),
+        graph_steps=int(_get(t, "graph_steps", 32)),
+        bucket_cap_mb=float(_get(t, "bucket_cap_mb", 25)),
+        first_bucket_mb=float(_get(t, "first_bucket_mb", 1)),
+        mixed_precision=_get(t, "mixed_precision", None),
+        fsdp_wrap=_wrap_policy(_get(t, "fsdp_wrap", None), model),
+        log_throughput=bool(_get(t, "log_throughput", False)),
+        grad_clip=_get(t, "grad_clip", None),
+        save_optimizer=bool(_get(t, "save_optimizer", False)),
+        desync_check_every=int(_get(t, "desync_check_every", 0) or 0),
+        fault_injection=_get(t, "fault_injection", None),
+    )
+
+
+def run(cfg) -> Trainer:
+    """Main training entry point (reference ``main`` body)."""
+    env = None
+    try:
+        setup_logging(cfg)
+        env = DistributedEnvironment(_get(cfg.train, "device", "auto"),
+                                     timeout_s=_get(cfg.train, "timeout_s", None))
+        env.setup()
+        dataset, model, optimizer = load_train_objs(cfg)
+        if _get(cfg.train, "activation_checkpointing", False) and hasattr(model, "enable_activation_checkpointing"):
+            model.enable_activation_checkpointing()
+        train_config = training_config_from(cfg, model)
+        train_data = prepare_dataloader(dataset, train_config.batch_size)
+        trainer = Trainer(model, train_data, optimizer, train_config, env)
+        trainer.train(train_config.max_epochs)
+        return trainer
+    except Exception as e:
+        logger.error(f"Training failed: {str(e)}")
+        raise
+    finally:
+        if torch.distributed.is_initialized():
+            if env is not None:
+                env.teardown()
+            else:
+                torch.distributed.destroy_process_group()

@@ -164,11 +164,11 @@ void cast_f32_bf16(torch::Tensor src, torch::Tensor dst, int64_t stream) {
 
 // ----------------------------- fused MLP step -----------------------------
 void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
-                     torch::Tensor ticket, torch::Tensor loss_ring, torch::Tensor p_in, torch::Tensor p_out,
+                     torch::Tensor x_stage, torch::Tensor t_stage, torch::Tensor loss_ring, torch::Tensor p_in, torch::Tensor p_out,
                      torch::Tensor g_prev, torch::Tensor g_out, c10::optional<torch::Tensor> mom_in,
                      c10::optional<torch::Tensor> mom_out, std::vector<int64_t> offsets, int64_t in_dim,
                      int64_t hidden, int64_t out_dim, int64_t B, int64_t own_tiles, int64_t act, int64_t loss_type,
-                     bool apply_update, double grad_scale, double lr, double momentum, double dampening, double wd,
+                     bool apply_update, int64_t parity, bool gather_self, double grad_scale, double lr, double momentum, double dampening, double wd,
                      double prev_grad_scale, bool nesterov, bool maximize, bool first_step, int64_t stream,
                      c10::optional<torch::Tensor> dbg_stamps) {
   check_f32(X, "X", false);
@@ -177,8 +177,13 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
   TORCH_CHECK(idx_ring.scalar_type() == torch::kInt32 && idx_ring.dim() == 2, "idx_ring: int32 [steps, stride]");
   check_gpu(cursor, "cursor");
   TORCH_CHECK(cursor.scalar_type() == torch::kInt32 && cursor.numel() >= 1, "cursor: int32[1]");
-  check_gpu(ticket, "ticket");
-  TORCH_CHECK(ticket.scalar_type() == torch::kInt32 && ticket.numel() >= 1, "ticket: int32[1]");
+  check_gpu(x_stage, "x_stage");
+  TORCH_CHECK(x_stage.scalar_type() == torch::kBFloat16 && x_stage.numel() == 2 * dta::kMlpStageRows * dta::kMlpStageCols,
+              "x_stage: bf16 [2, 128, 32]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x_stage.data_ptr()) % 16 == 0, "x_stage must be 16-byte aligned");
+  check_f32(t_stage, "t_stage");
+  TORCH_CHECK(t_stage.numel() == 2 * dta::kMlpStageRows * 8, "t_stage: f32 [2, 128, 8]");
+  TORCH_CHECK(idx_ring.size(1) <= dta::kMlpStageRows, "idx_ring stride must be <= 128");
   check_f32(loss_ring, "loss_ring", false);
   for (auto* t : {&p_in, &p_out, &g_prev, &g_out}) check_f32(*t, "flat buffer", false);
   TORCH_CHECK(offsets.size() == 4, "offsets = [w1, b1, w2, b2]");
@@ -221,7 +226,10 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
   a.T = T.data_ptr<float>();
   a.idx_ring = idx_ring.data_ptr<int>();
   a.cursor = cursor.data_ptr<int>();
-  a.ticket = reinterpret_cast<unsigned*>(ticket.data_ptr<int>());
+  a.x_stage = reinterpret_cast<unsigned short*>(x_stage.data_ptr());
+  a.t_stage = t_stage.data_ptr<float>();
+  a.parity = (int)(parity & 1);
+  a.gather_self = gather_self ? 1 : 0;
   a.loss_ring = loss_ring.data_ptr<float>();
   a.p_in = p_in.data_ptr<float>();
   a.p_out = p_out.data_ptr<float>();
@@ -363,10 +371,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("flat_clip", &flat_clip);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("mlp2_fused_step", &mlp2_fused_step, py::arg("X"), py::arg("T"), py::arg("idx_ring"), py::arg("cursor"),
-        py::arg("ticket"), py::arg("loss_ring"), py::arg("p_in"), py::arg("p_out"), py::arg("g_prev"), py::arg("g_out"),
+        py::arg("x_stage"), py::arg("t_stage"), py::arg("loss_ring"), py::arg("p_in"), py::arg("p_out"), py::arg("g_prev"), py::arg("g_out"),
         py::arg("mom_in"), py::arg("mom_out"), py::arg("offsets"), py::arg("in_dim"), py::arg("hidden"),
         py::arg("out_dim"), py::arg("B"), py::arg("own_tiles"), py::arg("act"), py::arg("loss_type"),
-        py::arg("apply_update"), py::arg("grad_scale"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"),
+        py::arg("apply_update"), py::arg("parity"), py::arg("gather_self"), py::arg("grad_scale"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"),
         py::arg("wd"), py::arg("prev_grad_scale"), py::arg("nesterov"), py::arg("maximize"), py::arg("first_step"),
         py::arg("stream") = -1, py::arg("dbg_stamps") = py::none());
   m.def("mlp2_lds_bytes", &dta_mlp2_lds_bytes);

@@ -6,12 +6,16 @@ namespace dta {
 
 enum LossType : int { LOSS_MSE = 0, LOSS_CE = 1 };
 
+constexpr int kMlpStageRows = 128;  // max micro-batch rows of the staged gather
+constexpr int kMlpStageCols = 32;   // bf16 columns per staged row (in_dim <= 31, zero padded)
+
 struct MlpArgs {
   const float* X;        // [N, in_dim]   device-resident dataset features
   const float* T;        // [N, out_dim]  targets
   const int* idx_ring;   // [ring_steps, idx_stride] sampler indices
-  int* cursor;           // global step counter (device)
-  unsigned* ticket;      // arrival ticket (zeroed once at setup)
+  int* cursor;           // global step counter (device; read/advanced by ONE wave)
+  unsigned short* x_stage;  // [2][kMlpStageRows][kMlpStageCols] bf16 bits: gathered batch
+  float* t_stage;        // [2][kMlpStageRows][8]
   float* loss_ring;      // [loss_len]
   const float* p_in;     // flat master weights (read)
   float* p_out;          // flat master weights (owner write)
@@ -24,6 +28,8 @@ struct MlpArgs {
   int in_dim, hidden, out_dim, B;
   int ring_steps, idx_stride, loss_len, own_tiles;
   int act, loss_type, apply_update;
+  int parity;       // staged batch of THIS step is slot `parity`; next step's goes to 1-parity
+  int gather_self;  // 1: gather this step's batch from the ring (first step); cursor not advanced
   float grad_scale;
   // SGD hyper-parameters of the pending update
   float lr, momentum, dampening, weight_decay, prev_grad_scale;

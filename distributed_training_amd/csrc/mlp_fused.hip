@@ -31,9 +31,14 @@
 // (p_in != p_out, g_prev != g_out); the host alternates them every step, so an
 // even number of steps captured in one hipGraph replays cleanly.
 //
-// The sampler cursor lives on the device: every workgroup reads it at entry and
-// the last workgroup to finish (arrival ticket) advances it, so a captured
-// multi-step graph walks through the index ring without host involvement.
+// The sampler gather is software-pipelined across steps: while the owner waves
+// run the backward, one spare wave of workgroup 0 reads the device cursor c,
+// gathers the micro-batch of step c+1 (indices from the device index ring) into
+// a staging slot and advances the cursor -- it is the ONLY reader/writer of the
+// cursor, so no cross-workgroup ticket is needed.  Every workgroup of the next
+// step then loads its batch from the staging slot in one round trip, in
+// parallel with the parameter loads.  A captured multi-step graph therefore
+// walks the index ring without host involvement.
 #include "common.h"
 #include "mlp_fused.h"
 
@@ -90,65 +95,90 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   bf16* Tw = XsT + 32 * BPS;                               // [NWAVE][2][32][TS] wave-private transposes
   float* Tg = reinterpret_cast<float*>(Tw + NWAVE * 2 * 32 * TS);  // [BP][8] targets
   float* Ys = Tg + BP * 8;                                 // [BP][8]
-  float* dYs = Ys + BP * 8;                                // [BP][8]
-  float* red = dYs + BP * 8;                               // [8]
+  float* dYw = Ys + BP * 8;                                // [NWAVE][BP][8] wave-private dY
 
 #define DTA_STAMP(k) \
   if (a.dbg_stamps && tid == 0) a.dbg_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   DTA_STAMP(0);
-  const int cur = *a.cursor;
-  const int* idx = a.idx_ring + (int64_t)(cur % a.ring_steps) * a.idx_stride;
 
   const int NT = H >> 5;
   const int ct0 = blockIdx.x * a.own_tiles;
   const int ct1 = min(ct0 + a.own_tiles, NT);
   const int h0 = ct0 * 32, h1 = ct1 * 32;
+  const bool stager = blockIdx.x == 0 && wave == NWAVE - 1;
 
-  // ---------------- phase 0a: gather the micro-batch ----------------
-  for (int e = tid; e < BP * 8; e += NTHR) Ys[e] = 0.f;
-  if (tid < 8) red[tid] = 0.f;
-  for (int e = tid; e < BP * 32; e += NTHR) {
-    const int r = e >> 5, k = e & 31;
-    float v = 0.f;
-    if (r < B) {
-      if (k < IN) v = a.X[(int64_t)idx[r] * IN + k];
-      else if (k == IN) v = 1.f;  // ones column: dW1's extra output column is db1
+  // ---------------- phase 0: loads (params first, then the staged batch) ----------------
+  constexpr int U = 4;
+  const int n4 = (int)(a.total >> 2);
+  const bool has_mom = a.mom_in != nullptr;
+  float4 pv[U], gv[U], mv[U];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e4 = base + u * NTHR + tid;
+      pv[u] = gv[u] = mv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e4 < n4) {
+        pv[u] = reinterpret_cast<const float4*>(a.p_in)[e4];
+        if (a.apply_update) gv[u] = reinterpret_cast<const float4*>(a.g_prev)[e4];
+        if (has_mom) mv[u] = reinterpret_cast<const float4*>(a.mom_in)[e4];
+      }
     }
-    const bf16 bv = f2bf(v);
-    Xs[r * XS + k] = bv;
-    XsT[k * BPS + r] = bv;
-  }
-  for (int e = tid; e < BP * 8; e += NTHR) {
-    const int r = e >> 3, o = e & 7;
-    float v = 0.f;
-    if (r < B && o < OUT) v = a.T[(int64_t)idx[r] * OUT + o];
-    Tg[e] = v;
+  };
+  issue(0);
+
+  // the micro-batch: staged by the previous step (one 16-byte load per thread)
+  for (int e = tid; e < BP * 8; e += NTHR) Ys[e] = 0.f;
+  if (a.gather_self) {
+    const int cur = *a.cursor;
+    const int* idx = a.idx_ring + (int64_t)(cur % a.ring_steps) * a.idx_stride;
+    for (int e = tid; e < BP * 32; e += NTHR) {
+      const int r = e >> 5, k = e & 31;
+      float v = 0.f;
+      if (r < B) {
+        if (k < IN) v = a.X[(int64_t)idx[r] * IN + k];
+        else if (k == IN) v = 1.f;  // ones column: dW1's extra output column is db1
+      }
+      const bf16 bv = f2bf(v);
+      Xs[r * XS + k] = bv;
+      XsT[k * BPS + r] = bv;
+    }
+    for (int e = tid; e < BP * 8; e += NTHR) {
+      const int r = e >> 3, o = e & 7;
+      float v = 0.f;
+      if (r < B && o < OUT) v = a.T[(int64_t)idx[r] * OUT + o];
+      Tg[e] = v;
+    }
+  } else {
+    const unsigned short* xs = a.x_stage + (size_t)a.parity * kMlpStageRows * kMlpStageCols;
+    const float* ts = a.t_stage + (size_t)a.parity * kMlpStageRows * 8;
+    for (int e = tid; e < BP * 4; e += NTHR) {  // 8 bf16 per thread
+      const int r = e >> 2, c8 = (e & 3) * 8;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(xs + r * kMlpStageCols + c8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = c8 + j;
+        if (r >= B || k > IN) v[j] = f2bf(0.f);
+        else if (k == IN) v[j] = f2bf(1.f);
+      }
+      *reinterpret_cast<bf16x8*>(Xs + r * XS + c8) = v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) XsT[(c8 + j) * BPS + r] = v[j];
+    }
+    for (int e = tid; e < BP * 2; e += NTHR) {  // 4 floats per thread
+      const int r = e >> 1, c4 = (e & 1) * 4;
+      float4 v = *reinterpret_cast<const float4*>(ts + r * 8 + c4);
+      if (r >= B) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(Tg + r * 8 + c4) = v;
+    }
   }
 
-  // ---------------- phase 0b: pending optimizer update -> LDS image ----------------
-  // Batched 16-byte loads (U float4 per thread in flight before any use).  Every
-  // workgroup computes the same updated values; only the owner of a slice writes
-  // it back (p_out / mom_out).  Regions are 16-float aligned, so a float4 never
-  // straddles two regions.
+  // pending optimizer update -> LDS image (+ owner write-back)
   {
-    constexpr int U = 4;
-    const int n4 = (int)(a.total >> 2);
-    const bool has_mom = a.mom_in != nullptr;
     const int w1_lo = h0 * IN, w1_hi = h1 * IN;
     const int b1_lo = o_b1 + h0, b1_hi = o_b1 + h1;
 #pragma unroll 1
     for (int base = 0; base < n4; base += NTHR * U) {
-      float4 pv[U], gv[U], mv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e4 = base + u * NTHR + tid;
-        pv[u] = gv[u] = mv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (e4 < n4) {
-          pv[u] = reinterpret_cast<const float4*>(a.p_in)[e4];
-          if (a.apply_update) gv[u] = reinterpret_cast<const float4*>(a.g_prev)[e4];
-          if (has_mom) mv[u] = reinterpret_cast<const float4*>(a.mom_in)[e4];
-        }
-      }
+      if (base > 0) issue(base);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e4 = base + u * NTHR + tid;
@@ -295,64 +325,64 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   __syncthreads();
   DTA_STAMP(2);
 
-  // ---------------- phase 2: loss + dY ----------------
-  if (tid < BP) {
-    const int r = tid;
-    float lossr = 0.f;
-    float dy[8];
+  // ---------------- phase 2: loss + dY (per wave, no further barrier) ----------------
+  float* dYme = dYw + wave * BP * 8;
+  float lossr = 0.f;
+  float db2p[8];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) dy[o] = 0.f;
-    if (r < B) {
-      float y[8];
+  for (int o = 0; o < 8; ++o) db2p[o] = 0.f;
+  if (owner_wave || stager) {
 #pragma unroll
-      for (int o = 0; o < 8; ++o) y[o] = (o < OUT) ? Ys[r * 8 + o] + Pf[o_b2 + o] : 0.f;
-      if (a.loss_type == LOSS_MSE) {
-        const float inv = 1.f / (float)(B * OUT);
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r = rt * 32 + r32;
+      float dy[8];
 #pragma unroll
-        for (int o = 0; o < 8; ++o)
-          if (o < OUT) {
-            const float d = y[o] - Tg[r * 8 + o];
-            lossr += d * d;
-            dy[o] = 2.f * d * inv;
-          }
-      } else {
-        float m = -INFINITY;
+      for (int o = 0; o < 8; ++o) dy[o] = 0.f;
+      if (r < B && hh == 0) {
+        float y[8];
 #pragma unroll
-        for (int o = 0; o < 8; ++o)
-          if (o < OUT) m = fmaxf(m, y[o]);
-        float s = 0.f, tsum = 0.f;
+        for (int o = 0; o < 8; ++o) y[o] = (o < OUT) ? Ys[r * 8 + o] + Pf[o_b2 + o] : 0.f;
+        if (a.loss_type == LOSS_MSE) {
+          const float inv = 1.f / (float)(B * OUT);
 #pragma unroll
-        for (int o = 0; o < 8; ++o)
-          if (o < OUT) {
-            s += __expf(y[o] - m);
-            tsum += Tg[r * 8 + o];
-          }
-        const float lse = m + __logf(s);
-        const float inv = 1.f / (float)B;
+          for (int o = 0; o < 8; ++o)
+            if (o < OUT) {
+              const float d = y[o] - Tg[r * 8 + o];
+              lossr += d * d;
+              dy[o] = 2.f * d * inv;
+            }
+        } else {
+          float m = -INFINITY;
 #pragma unroll
-        for (int o = 0; o < 8; ++o)
-          if (o < OUT) {
-            const float t = Tg[r * 8 + o];
-            lossr -= t * (y[o] - lse);
-            dy[o] = (__expf(y[o] - lse) * tsum - t) * inv;
-          }
+          for (int o = 0; o < 8; ++o)
+            if (o < OUT) m = fmaxf(m, y[o]);
+          float sx = 0.f, tsum = 0.f;
+#pragma unroll
+          for (int o = 0; o < 8; ++o)
+            if (o < OUT) {
+              sx += __expf(y[o] - m);
+              tsum += Tg[r * 8 + o];
+            }
+          const float lse = m + __logf(sx);
+          const float inv = 1.f / (float)B;
+#pragma unroll
+          for (int o = 0; o < 8; ++o)
+            if (o < OUT) {
+              const float t = Tg[r * 8 + o];
+              lossr -= t * (y[o] - lse);
+              dy[o] = (__expf(y[o] - lse) * tsum - t) * inv;
+            }
+        }
+      }
+      if (hh == 0) {
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          dYme[r * 8 + o] = dy[o];
+          db2p[o] += dy[o];
+        }
       }
     }
-#pragma unroll
-    for (int o = 0; o < 8; ++o) dYs[r * 8 + o] = dy[o];
-    atomicAdd(&red[0], lossr);
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    if (tid == 0) {
-      const float scale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
-      a.loss_ring[cur % a.loss_len] = red[0] * scale;
-    }
-    if (tid < OUT) {
-      float s = 0.f;
-      for (int r = 0; r < B; ++r) s += dYs[r * 8 + tid];
-      a.g_out[o_b2 + tid] = s * a.grad_scale;
-    }
+    wave_lds_fence();
   }
   DTA_STAMP(3);
 
@@ -375,7 +405,7 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int o = 8 * hh + j;
-        bdy[j] = f2bf(o < 8 ? dYs[(rt * 32 + r32) * 8 + (o & 7)] : 0.f);
+        bdy[j] = f2bf(o < 8 ? dYme[(rt * 32 + r32) * 8 + (o & 7)] : 0.f);
       }
       const f32x16 dat = mfma32x32x16(aw2, bdy, zero16);  // rows h, cols b (= kept H^T layout)
       const f32x16 hp = keep[rt];
@@ -396,7 +426,7 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
         bf16x8 bdy2;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          bdy2[j] = f2bf(r32 < OUT ? dYs[(rt * 32 + kb + j) * 8 + (r32 & 7)] : 0.f);
+          bdy2[j] = f2bf(r32 < OUT ? dYme[(rt * 32 + kb + j) * 8 + (r32 & 7)] : 0.f);
         dw2 = mfma32x32x16(aat, bdy2, dw2);  // rows h, cols o
       }
       wave_lds_fence();
@@ -411,16 +441,51 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
     }
   }
 
-  // ---------------- phase 4: advance the sampler cursor ----------------
-  __syncthreads();
-  DTA_STAMP(4);
-  if (tid == 0) {
-    const unsigned t = atomicAdd(a.ticket, 1u);
-    if (t == gridDim.x - 1) {
-      *a.ticket = 0u;
-      *a.cursor = cur + 1;
+  // ------- the stager: loss, db2, and the NEXT step's gathered batch -------
+  if (stager) {
+    const float lsum = wave_sum(lossr);
+#pragma unroll
+    for (int o = 0; o < 8; ++o) db2p[o] = wave_sum(db2p[o]);
+    const int cur = *a.cursor;
+    if (lane == 0) {
+      const float scale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
+      a.loss_ring[cur % a.loss_len] = lsum * scale;
     }
+    if (lane < OUT) {
+      float v = 0.f;
+#pragma unroll
+      for (int o = 0; o < 8; ++o)
+        if (o == lane) v = db2p[o];
+      a.g_out[o_b2 + lane] = v * a.grad_scale;
+    }
+    // gather step cur+1 into the other staging slot (rows beyond the batch read
+    // valid zero-padded ring entries and are masked by the consumer)
+    // (with gather_self nobody else touches the cursor in this launch; the host advances it)
+    const int* idx = a.idx_ring + (int64_t)((cur + 1) % a.ring_steps) * a.idx_stride;
+    unsigned short* xs = a.x_stage + (size_t)(1 - a.parity) * kMlpStageRows * kMlpStageCols;
+    float* ts = a.t_stage + (size_t)(1 - a.parity) * kMlpStageRows * 8;
+    const int rows = min(a.idx_stride, kMlpStageRows);
+    for (int r = lane; r < rows; r += 64) {
+      const int64_t src = idx[r];
+      bf16x8 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = c * 8 + j;
+          v[c][j] = f2bf(k < IN ? a.X[src * IN + k] : 0.f);
+        }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(xs + r * kMlpStageCols + c * 8) = v[c];
+      float t[8];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) t[o] = o < OUT ? a.T[src * OUT + o] : 0.f;
+      *reinterpret_cast<float4*>(ts + r * 8) = make_float4(t[0], t[1], t[2], t[3]);
+      *reinterpret_cast<float4*>(ts + r * 8 + 4) = make_float4(t[4], t[5], t[6], t[7]);
+    }
+    if (!a.gather_self && lane == 0) *a.cursor = cur + 1;
   }
+  DTA_STAMP(4);
 #undef DTA_STAMP
 }
 
@@ -453,7 +518,7 @@ using namespace dta;
 
 size_t dta_mlp2_lds_bytes(int64_t total, int bpad) {
   return (size_t)total * 4 + (size_t)bpad * XS * 2 + 32 * (size_t)(bpad + 8) * 2 + NWAVE * 2 * 32 * TS * 2 +
-         3 * (size_t)bpad * 32 + 32;
+         2 * (size_t)bpad * 32 + (size_t)NWAVE * bpad * 32;
 }
 
 // Returns hipErrorInvalidValue for shapes the fused kernel does not cover;

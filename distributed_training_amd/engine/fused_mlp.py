@@ -1,0 +1,265 @@
+"""Fused DDP step program for the 2-layer MLP (the headline benchmark model).
+
+One training step on one rank = ONE hand-written gfx950 kernel
+(``csrc/mlp_fused.hip``: pending SGD update + sampler gather + forward + loss +
+backward, gradients pre-scaled by 1/world_size) followed by ONE RCCL
+all-reduce of the flat gradient buffer (sum).  ``graph_steps`` consecutive
+steps (kernel + all-reduce each) are captured into a single hipGraph and
+replayed, so the host launches one graph per ``graph_steps`` steps.
+
+Equivalence to the reference step (src/distributed_trainer.py:160-165,
+zero_grad -> forward -> loss -> backward (DDP all-reduce) -> SGD step) is
+exact up to bf16 MFMA operand rounding: the SGD update of step t is applied
+at the start of step t+1 (or by :meth:`flush` before any read of the
+weights), which is mathematically the same update order.
+
+Batches follow ``DistributedSampler`` order exactly (per-epoch permutation,
+padding and rank striding); each epoch's indices are uploaded once into a
+device ring and a device-side cursor walks it.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..ops import mlp_fused as mf
+from ..ops import native
+
+logger = logging.getLogger(__name__)
+
+
+def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torch.device) -> Optional[str]:
+    """Return None when the fused program applies, else the reason it does not."""
+    from ..data.datasets import DeviceDataLoader
+    from ..models.mlp import MLP
+
+    if device.type != "cuda":
+        return "not a GPU run"
+    if not isinstance(module, MLP) or module.num_layers != 2:
+        return "model is not a 2-layer MLP"
+    if module.activation not in mf.ACTIVATIONS:
+        return f"activation {module.activation} not fused"
+    if loss not in mf.LOSSES:
+        return f"loss {loss} not fused"
+    if not isinstance(loader, DeviceDataLoader) or not hasattr(loader.dataset, "X"):
+        return "loader is not a device-resident feature loader"
+    if len(optimizer.param_groups) != 1:
+        return "optimizer has several param groups"
+    g = optimizer.param_groups[0]
+    if "momentum" not in g or "betas" in g:
+        return "optimizer is not SGD"
+    if g.get("momentum", 0) and g.get("dampening", 0):
+        return "SGD dampening not fused"
+    if not mf.supported(module.input_size, module.hidden[0], module.output_size, loader.batch_size):
+        return "shape outside the fused kernel's limits"
+    return None
+
+
+class FusedMLPProgram:
+    def __init__(self, module, optimizer, loader, comm, loss: str = "mse", graph_steps: int = 32,
+                 own_tiles: Optional[int] = None, allreduce_world1: bool = True, loss_len: int = 4096):
+        self.module = module
+        self.opt = optimizer
+        self.loader = loader
+        self.comm = comm
+        self.loss = loss
+        self.act = module.activation
+        self.ws = comm.world_size
+        self.device = loader.device
+        self.B = loader.batch_size
+        H = module.hidden[0]
+        self.layout = mf.make_layout(module.input_size, H, module.output_size)
+        nt = H // 32
+        self.own_tiles = own_tiles or max(1, min(8, nt // 8 if nt >= 64 else (nt + 15) // 16 if nt > 8 else 1))
+        if self.own_tiles > 8:
+            self.own_tiles = 8
+        self.graph_steps = max(2, graph_steps + (graph_steps % 2))  # even: ping-pong parity preserved
+        self.allreduce_world1 = allreduce_world1
+        dev = self.device
+        T = self.layout.total
+        self.P = [torch.zeros(T, device=dev) for _ in range(2)]
+        self.G = [torch.zeros(T, device=dev) for _ in range(2)]
+        hp = self.hyper()
+        self.use_mom = bool(hp["momentum"])
+        self.M = [torch.zeros(T, device=dev) for _ in range(2)] if self.use_mom else [None, None]
+        self.X, self.Y = loader.tensors()
+        self.X = self.X.float().contiguous()
+        self.Y = self.Y.float().contiguous()
+        self.steps_per_epoch = S = max(1, len(loader))
+        # index ring: whole epochs, at least one graph beyond an epoch, so uploads
+        # for epoch e+1 can be enqueued while epoch e's steps are still queued
+        k = max(2, -(-2 * self.graph_steps // S) + 1)
+        self.R = S * k
+        self.ring = torch.zeros(self.R, self.B, dtype=torch.int32, device=dev)
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.stage = mf.make_stage(dev)
+        self.staged = False        # staging slot `parity` holds the batch of step `launched`
+        self.loss_ring = torch.zeros(loss_len, device=dev)
+        self.parity = 0
+        self.pending = False
+        self.mom_started = False
+        self.launched = 0          # global steps enqueued (== device cursor when drained)
+        self.host_step = 0         # global steps whose indices are uploaded
+        self.next_epoch = 0        # next epoch to upload
+        self._batch_of: Dict[int, int] = {}
+        self._staging: List = []   # (pinned tensor, event) kept alive until the copy ran
+        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.load_from_module()
+
+    # ------------------------------------------------------------ state sync
+    def hyper(self) -> Dict[str, float]:
+        g = self.opt.param_groups[0]
+        return {"lr": g["lr"], "momentum": g.get("momentum", 0.0), "dampening": g.get("dampening", 0.0),
+                "weight_decay": g.get("weight_decay", 0.0), "nesterov": g.get("nesterov", False),
+                "maximize": g.get("maximize", False)}
+
+    @torch.no_grad()
+    def load_from_module(self) -> None:
+        """Copy the module's weights in (fp32 master copy when the DDP engine
+        keeps one, so bf16 compute copies never round the master)."""
+        v = self.layout.views(self.P[self.parity])
+        for name, p in self.module.named_parameters():
+            tag = getattr(p, "_dta_flat", None)
+            src = tag[0].master_view(tag[1]) if tag is not None else p.detach()
+            v[name].copy_(src.float())
+
+    @torch.no_grad()
+    def flush(self) -> None:
+        """Apply the pending SGD update (so P[parity] holds the current weights)."""
+        if not self.pending:
+            return
+        hp = self.hyper()
+        c = self.parity
+        native().flat_sgd(self.P[c], self.P[c], self.G[1 - c], self.M[c], None, hp["lr"], hp["momentum"],
+                          hp["dampening"], hp["weight_decay"], 1.0, hp["nesterov"], hp["maximize"],
+                          not self.mom_started, -1)
+        self.mom_started = True
+        self.pending = False
+
+    @torch.no_grad()
+    def store_to_module(self) -> None:
+        self.flush()
+        v = self.layout.views(self.P[self.parity])
+        for name, p in self.module.named_parameters():
+            tag = getattr(p, "_dta_flat", None)
+            if tag is not None:
+                tag[0].master_view(tag[1]).copy_(v[name])
+            p.copy_(v[name].to(p.dtype))
+
+    # ------------------------------------------------------------ stepping
+    def _launch(self, batch: int, apply_update: bool, first_mom: bool, parity: int, gather_self: bool) -> None:
+        hp = self.hyper()
+        c = parity
+        mf.fused_step(self.X, self.Y, self.ring, self.cursor, self.stage, self.loss_ring, self.P[c],
+                      self.P[1 - c], self.G[1 - c], self.G[c], self.M[c], self.M[1 - c], self.layout, batch,
+                      self.own_tiles, self.act, self.loss, apply_update, 1.0 / self.ws, hp, 1.0, first_mom,
+                      parity=c, gather_self=gather_self)
+        if gather_self:
+            self.cursor.add_(1)
+        if self.ws > 1 or self.allreduce_world1:
+            self._allreduce(self.G[c])
+
+    def _allreduce(self, t: torch.Tensor) -> None:
+        if hasattr(self.comm, "all_reduce_inline"):
+            self.comm.all_reduce_inline(t, "sum")
+        else:
+            self.comm.all_reduce(t, op="sum")
+
+    def _eager_step(self, batch: int) -> None:
+        first_mom = self.use_mom and self.pending and not self.mom_started
+        self._launch(batch, self.pending, first_mom, self.parity, gather_self=not self.staged)
+        if self.pending and self.use_mom:
+            self.mom_started = True
+        self.pending = True
+        self.staged = True
+        self.parity ^= 1
+
+    def _graph(self, parity: int) -> torch.cuda.CUDAGraph:
+        g = self._graphs.get(parity)
+        if g is not None:
+            return g
+        # steady state only: pending update present, momentum already started
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                p = parity
+                for _ in range(self.graph_steps):
+                    self._launch(self.B, True, False, p, gather_self=False)
+                    p ^= 1
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._graphs[parity] = g
+        return g
+
+    # ------------------------------------------------------------ indices
+    def seek_epoch(self, epoch: int) -> None:
+        """Position the index stream at ``epoch`` (only between epochs)."""
+        if self.host_step != self.launched:
+            raise RuntimeError("seek_epoch with uploaded-but-unrun steps")
+        self.next_epoch = epoch
+        self.staged = False
+
+    def _upload_epoch(self) -> None:
+        e = self.next_epoch
+        S, B, R = self.steps_per_epoch, self.B, self.R
+        assert self.host_step + S - R <= self.launched, "index ring overrun"
+        self.loader.sampler.set_epoch(e)
+        idx = self.loader.epoch_indices().to(torch.int32)
+        host = torch.zeros(S, B, dtype=torch.int32).pin_memory()
+        host.view(-1)[: idx.numel()] = idx
+        last = idx.numel() - (S - 1) * B
+        r0 = self.host_step % R
+        n1 = min(S, R - r0)
+        self.ring[r0:r0 + n1].copy_(host[:n1], non_blocking=True)
+        if n1 < S:
+            self.ring[0:S - n1].copy_(host[n1:], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._staging.append((host, ev))
+        if len(self._staging) > 8:
+            self._staging = [(h, e2) for h, e2 in self._staging if not e2.query()]
+        for j in range(S):
+            self._batch_of[self.host_step + j] = B if j < S - 1 else last
+        self.host_step += S
+        self.next_epoch += 1
+
+    def _ensure(self, upto: int) -> None:
+        while self.host_step < upto:
+            self._upload_epoch()
+
+    # ------------------------------------------------------------ stepping API
+    @torch.no_grad()
+    def run_steps(self, n: int) -> None:
+        """Enqueue ``n`` training steps (crossing epochs as needed)."""
+        end = self.launched + n
+        while self.launched < end:
+            U = self.graph_steps
+            steady = self.pending and self.staged and (self.mom_started or not self.use_mom)
+            if steady and end - self.launched >= U:
+                self._ensure(self.launched + U + 1)  # +1: the last step stages its successor
+                if all(self._batch_of[self.launched + j] == self.B for j in range(U)):
+                    self._graph(self.parity).replay()
+                    for j in range(U):
+                        self._batch_of.pop(self.launched + j, None)
+                    self.launched += U  # parity unchanged (even number of steps)
+                    continue
+            self._ensure(self.launched + 2)
+            self._eager_step(self._batch_of.pop(self.launched))
+            self.launched += 1
+
+    def run_epoch(self, epoch: int) -> int:
+        if self.host_step == self.launched and self.next_epoch != epoch:
+            self.seek_epoch(epoch)
+        S = self.steps_per_epoch
+        self.run_steps(S)
+        return S
+
+    def last_losses(self, n: int) -> torch.Tensor:
+        """Losses of the last ``n`` launched steps (oldest first)."""
+        L = self.loss_ring.numel()
+        idx = [(self.launched - 1 - k) % L for k in range(min(n, self.launched, L))]
+        return self.loss_ring[idx].flip(0) if idx else torch.zeros(0)

@@ -68,7 +68,7 @@ def lds_bytes(in_dim: int, hidden: int, out_dim: int, batch: int) -> int:
     rt = (batch + 31) // 32
     bpad = 32 if rt <= 1 else (64 if rt <= 2 else 128)
     total = make_layout(in_dim, hidden, out_dim).total
-    return total * 4 + bpad * 80 + 32 * (bpad + 8) * 2 + 8 * 2 * 32 * 40 * 2 + 3 * bpad * 32 + 32
+    return total * 4 + bpad * 80 + 32 * (bpad + 8) * 2 + 8 * 2 * 32 * 40 * 2 + 2 * bpad * 32 + 8 * bpad * 32
 
 
 def supported(in_dim: int, hidden: int, out_dim: int, batch: int) -> bool:
@@ -83,17 +83,31 @@ def supported(in_dim: int, hidden: int, out_dim: int, batch: int) -> bool:
     )
 
 
+STAGE_ROWS, STAGE_COLS = 128, 32
+
+
+def make_stage(device):
+    """Double-buffered staging slots for the pipelined batch gather."""
+    return (torch.zeros(2, STAGE_ROWS, STAGE_COLS, dtype=torch.bfloat16, device=device),
+            torch.zeros(2, STAGE_ROWS, 8, dtype=torch.float32, device=device))
+
+
 def fused_step(
-    X, T, idx_ring, cursor, ticket, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+    X, T, idx_ring, cursor, stage, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
     layout: MlpLayout, batch: int, own_tiles: int, act: str, loss: str, apply_update: bool,
     grad_scale: float, sgd: Dict[str, float], prev_grad_scale: float, first_step: bool, stream=None,
-    dbg_stamps=None,
+    dbg_stamps=None, parity: int = 0, gather_self: bool = True,
 ) -> None:
+    """One fused step.  ``gather_self`` reads this step's batch straight from the
+    index ring at ``cursor`` (and leaves the cursor for the caller to advance);
+    otherwise the batch comes from staging slot ``parity``, which the previous
+    step filled, and the kernel advances the cursor itself.  Either way the next
+    step's batch is staged into slot ``1 - parity``."""
     C = native()
     C.mlp2_fused_step(
-        X, T, idx_ring, cursor, ticket, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+        X, T, idx_ring, cursor, stage[0], stage[1], loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
         layout.offsets, layout.in_dim, layout.hidden, layout.out_dim, int(batch), int(own_tiles),
-        ACTIVATIONS[act], LOSSES[loss], bool(apply_update), float(grad_scale),
+        ACTIVATIONS[act], LOSSES[loss], bool(apply_update), int(parity), bool(gather_self), float(grad_scale),
         float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)), float(sgd.get("dampening", 0.0)),
         float(sgd.get("weight_decay", 0.0)), float(prev_grad_scale), bool(sgd.get("nesterov", False)),
         bool(sgd.get("maximize", False)), bool(first_step), -1 if stream is None else int(stream.cuda_stream),

@@ -19,7 +19,9 @@ Reference parity: replaces the implicit c10d NCCL/Gloo process group of
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 from typing import List, Optional
 
 import torch
@@ -27,6 +29,20 @@ import torch.distributed as dist
 
 _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
         "prod": dist.ReduceOp.PRODUCT}
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Redirect the C-level stdout (fd 1) to stderr for the duration."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 class CommWork:
@@ -169,7 +185,8 @@ class RcclComm(Communicator):
             if store is None:
                 raise RuntimeError("RcclComm needs a store (torch.distributed initialised) for world_size > 1")
             uid = store.get(key)
-        self._comm = C.RcclComm(uid, world_size, rank, device.index if device.index is not None else 0)
+        with _stdout_to_stderr():  # RCCL prints its version banner on stdout at init
+            self._comm = C.RcclComm(uid, world_size, rank, device.index if device.index is not None else 0)
         # dedicated high-priority stream for collectives (lower number = higher priority)
         self.stream = torch.cuda.Stream(device=device, priority=stream_priority)
 

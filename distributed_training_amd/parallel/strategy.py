@@ -1,0 +1,124 @@
+"""Parallel strategies (Strategy pattern, same API as the reference).
+
+Reference: ``DistributedStrategy`` ABC (src/dist_strategy/dist_strategy.py:8-26),
+``DDPStrategy(local_rank, is_gpu)`` (ddp_strategy.py:10-32),
+``FSDPStrategy(is_gpu)`` (fsdp_strategy.py:13-46).  The strategies here wrap
+the NATIVE engines (:mod:`.ddp`, :mod:`.fsdp`) instead of torch DDP / FSDP1;
+extra keyword options (bucket size, wrap policy, mixed precision) default to
+the reference behaviour.  ``model_state`` is new: it is called on every rank
+by the checkpoint manager (FSDP's full-state gather is a collective).
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+from torch.nn import Module
+
+from .comm import Communicator, TorchComm, make_comm
+
+_COMMS: Dict[str, Communicator] = {}
+
+
+def default_comm(device: torch.device) -> Communicator:
+    """One communicator per process and device (RCCL on GPU, gloo on CPU)."""
+    key = str(device)
+    if key not in _COMMS:
+        _COMMS[key] = make_comm(device) if device.type == "cuda" else TorchComm(device=device)
+    return _COMMS[key]
+
+
+def set_default_comm(device: torch.device, comm: Communicator) -> None:
+    _COMMS[str(device)] = comm
+
+
+def _as_device(device: Any) -> torch.device:
+    if isinstance(device, torch.device):
+        return device
+    if isinstance(device, int):
+        return torch.device("cuda", device)
+    return torch.device(device)
+
+
+_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+class DistributedStrategy(ABC):
+    @abstractmethod
+    def prepare_model(self, model: Module, device: Any) -> Module:
+        """Wrap the model with the appropriate parallel strategy."""
+
+    @abstractmethod
+    def save_checkpoint(self, model: Module, state_dict: dict, path: str) -> None:
+        """Save model checkpoint (rank 0)."""
+
+    @abstractmethod
+    def load_checkpoint(self, model: Module, checkpoint: dict, device: Any) -> Tuple[Module, int]:
+        """Load model checkpoint."""
+
+    def model_state(self, model: Module) -> Dict[str, torch.Tensor]:
+        """State dict to checkpoint; called on ALL ranks."""
+        return model.state_dict()
+
+
+class DDPStrategy(DistributedStrategy):
+    def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
+                 mixed_precision: Optional[str] = None, comm: Optional[Communicator] = None):
+        self.local_rank = local_rank
+        self.is_gpu = is_gpu
+        self.bucket_cap_mb = bucket_cap_mb
+        self.first_bucket_mb = first_bucket_mb
+        self.param_dtype = _DTYPES[mixed_precision] if mixed_precision else torch.float32
+        self.comm = comm
+
+    def prepare_model(self, model: Module, device: Any) -> Module:
+        from .ddp import DistributedDataParallel
+
+        dev = _as_device(device)
+        comm = self.comm or default_comm(dev)
+        return DistributedDataParallel(model, comm=comm, device=dev, bucket_cap_mb=self.bucket_cap_mb,
+                                       first_bucket_mb=self.first_bucket_mb, param_dtype=self.param_dtype)
+
+    def save_checkpoint(self, model: Module, state_dict: dict, path: str) -> None:
+        from ..engine.checkpoint import atomic_torch_save
+
+        atomic_torch_save(state_dict, path)
+
+    def load_checkpoint(self, model: Module, checkpoint: dict, device: Any) -> Tuple[Module, int]:
+        model.load_state_dict(checkpoint["MODEL_STATE"])
+        return model, checkpoint["EPOCHS_RUN"]
+
+
+class FSDPStrategy(DistributedStrategy):
+    def __init__(self, is_gpu: bool, wrap_policy=None, mixed_precision: Optional[str] = None,
+                 reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None):
+        self.is_gpu = is_gpu
+        self.wrap_policy = wrap_policy
+        self.param_dtype = _DTYPES[mixed_precision] if mixed_precision else torch.float32
+        self.reshard_after_forward = reshard_after_forward
+        self.prefetch = prefetch
+        self.comm = comm
+
+    def prepare_model(self, model: Module, device: Any) -> Module:
+        from .fsdp import FullyShardedDataParallel
+
+        dev = _as_device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if self.is_gpu else torch.device("cpu"))
+        comm = self.comm or default_comm(dev)
+        return FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=self.wrap_policy,
+                                        param_dtype=self.param_dtype,
+                                        reshard_after_forward=self.reshard_after_forward, prefetch=self.prefetch)
+
+    def model_state(self, model: Module) -> Dict[str, torch.Tensor]:
+        # FULL_STATE_DICT, offload_to_cpu=True, rank0_only=True (fsdp_strategy.py:31-35) -- on all ranks
+        return model.full_state_dict(rank0_only=True, offload_to_cpu=True)
+
+    def save_checkpoint(self, model: Module, state_dict: dict, path: str) -> None:
+        from ..engine.checkpoint import atomic_torch_save
+
+        atomic_torch_save(state_dict, path)
+
+    def load_checkpoint(self, model: Module, checkpoint: dict, device: Any) -> Tuple[Module, int]:
+        model.load_state_dict(checkpoint["MODEL_STATE"])
+        return model, checkpoint["EPOCHS_RUN"]

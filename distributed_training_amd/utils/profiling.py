@@ -1,0 +1,88 @@
+"""Tracing helpers: roctx ranges + HIP-event step timer.
+
+``roctx`` ranges (``libroctx64``, resolved at run time with ctypes) mark step
+phases so ``rocprofv3 --marker-trace`` timelines show forward / backward /
+all-reduce / optimizer; without the library the ranges are no-ops.  The
+reference has no tracing at all.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import os
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+_roctx = None
+
+
+def _load_roctx():
+    global _roctx
+    if _roctx is not None:
+        return _roctx if _roctx else None
+    for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+        try:
+            lib = ctypes.CDLL(name)
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            lib.roctxRangePushA.restype = ctypes.c_int
+            lib.roctxRangePop.restype = ctypes.c_int
+            lib.roctxMarkA.argtypes = [ctypes.c_char_p]
+            _roctx = lib
+            return lib
+        except OSError:
+            continue
+    _roctx = False
+    return None
+
+
+def enabled() -> bool:
+    return os.environ.get("DTA_ROCTX", "0") == "1" and _load_roctx() is not None
+
+
+@contextlib.contextmanager
+def range_(name: str):
+    lib = _load_roctx() if os.environ.get("DTA_ROCTX", "0") == "1" else None
+    if lib is not None:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib is not None:
+            lib.roctxRangePop()
+
+
+def mark(name: str) -> None:
+    lib = _load_roctx() if os.environ.get("DTA_ROCTX", "0") == "1" else None
+    if lib is not None:
+        lib.roctxMarkA(name.encode())
+
+
+class StepTimer:
+    """Wall-clock step timer with device synchronisation at the boundaries."""
+
+    def __init__(self, device: Optional[torch.device] = None):
+        self.device = device
+        self.times: List[float] = []
+        self._t0 = None
+
+    def _sync(self):
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def start(self):
+        self._sync()
+        self._t0 = time.perf_counter()
+
+    def stop(self, n_steps: int = 1) -> float:
+        self._sync()
+        dt = time.perf_counter() - self._t0
+        self.times.append(dt / max(1, n_steps))
+        return dt
+
+    def summary(self) -> Dict[str, float]:
+        if not self.times:
+            return {}
+        ts = sorted(self.times)
+        return {"mean_s": sum(ts) / len(ts), "median_s": ts[len(ts) // 2], "min_s": ts[0]}

@@ -26,7 +26,7 @@ def main():
     T = torch.rand(N, args.out_dim, device=dev)
     ring = torch.randint(0, N, (64, args.batch), dtype=torch.int32, device=dev)
     cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-    ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    stage = mf.make_stage(dev)
     loss = torch.zeros(64, device=dev)
     P = [torch.randn(lay.total, device=dev) * 0.05 for _ in range(2)]
     G = [torch.zeros(lay.total, device=dev) for _ in range(2)]
@@ -34,8 +34,8 @@ def main():
 
     def step(i):
         a, b = i % 2, (i + 1) % 2
-        mf.fused_step(X, T, ring, cursor, ticket, loss, P[a], P[b], G[b], G[a], None, None, lay, args.batch,
-                      args.own, "relu", "mse", True, 1.0, sgd, 1.0, False)
+        mf.fused_step(X, T, ring, cursor, stage, loss, P[a], P[b], G[b], G[a], None, None, lay, args.batch,
+                      args.own, "relu", "mse", True, 1.0, sgd, 1.0, False, parity=a, gather_self=False)
 
     for i in range(50):
         step(i)
@@ -43,13 +43,15 @@ def main():
     stamps = torch.zeros(8 * 64, dtype=torch.int64, device=dev)
     phase_us = []
     for rep in range(20):
-        mf.fused_step(X, T, ring, cursor, ticket, loss, P[0], P[1], G[1], G[0], None, None, lay, args.batch,
-                      args.own, "relu", "mse", True, 1.0, sgd, 1.0, False, dbg_stamps=stamps)
+        mf.fused_step(X, T, ring, cursor, stage, loss, P[0], P[1], G[1], G[0], None, None, lay, args.batch,
+                      args.own, "relu", "mse", True, 1.0, sgd, 1.0, False, dbg_stamps=stamps, parity=0,
+                      gather_self=False)
         torch.cuda.synchronize()
         st = stamps.view(64, 8).cpu()
         nwg = (args.hidden // 32 + args.own - 1) // args.own
         d = (st[:nwg, 1:5] - st[:nwg, 0:4]).float().mean(0) / 100.0  # 100 MHz ticks -> us
         tot = (st[:nwg, 4].max() - st[:nwg, 0].min()).item() / 100.0
+        d[3] = (st[0, 4] - st[0, 3]).item() / 100.0  # WG0 tail incl. the stager
         phase_us.append(d.tolist() + [tot])
     phase_us = torch.tensor(phase_us).median(0).values.tolist()
     t0 = time.perf_counter()

@@ -121,29 +121,37 @@ def test_mlp2_fused_step_no_update(C, in_dim, hidden, out_dim, batch, act, loss,
     ring.view(-1)[: idx.numel()] = idx
     ring = ring.to(dev())
     cursor = torch.tensor([1], dtype=torch.int32, device=dev())
-    ticket = torch.zeros(1, dtype=torch.int32, device=dev())
+    stage = mf.make_stage(dev())
     loss_ring = torch.zeros(8, device=dev())
-    p_out = torch.full_like(flat, float("nan"))
-    g_prev = torch.zeros_like(flat)
-    g_out = torch.zeros_like(flat)
     scale = 0.5
-    mf.fused_step(X, T, ring, cursor, ticket, loss_ring, flat, p_out, g_prev, g_out, None, None, lay, batch, own,
-                  act, loss, False, scale, {"lr": 0.1}, 1.0, False)
-    torch.cuda.synchronize()
-    assert cursor.item() == 2 and ticket.item() == 0
-    # owners copied every parameter through unchanged
-    for k, v in lay.views(p_out).items():
-        torch.testing.assert_close(v, lay.views(flat)[k], msg=k)
-    step_idx = ring[1, :batch].cpu()
-    ref_loss, ref_g = mf.reference_step(X.cpu(), T.cpu(), step_idx, {k: v.cpu() for k, v in lay.views(flat).items()},
-                                        act, loss, emulate_bf16=True)
-    torch.testing.assert_close(loss_ring[1].cpu(), ref_loss, rtol=1e-3, atol=1e-5)
-    got = lay.views(g_out)
-    for k in ref_g:
-        exp = ref_g[k] * scale
-        tol = 3e-2 * exp.abs().max().item() + 1e-6
-        err = (got[k].cpu() - exp).abs().max().item()
-        assert err <= tol, f"{k}: max err {err} > {tol}"
+    params_cpu = {k: v.cpu() for k, v in lay.views(flat).items()}
+    # step A gathers its own batch (ring row 1) and stages row 2; step B reads the staged batch
+    for parity, gather_self, row in ((0, True, 1), (1, False, 2)):
+        p_out = torch.full_like(flat, float("nan"))
+        g_prev = torch.zeros_like(flat)
+        g_out = torch.zeros_like(flat)
+        mf.fused_step(X, T, ring, cursor, stage, loss_ring, flat, p_out, g_prev, g_out, None, None, lay, batch,
+                      own, act, loss, False, scale, {"lr": 0.1}, 1.0, False, parity=parity,
+                      gather_self=gather_self)
+        torch.cuda.synchronize()
+        if gather_self:
+            assert cursor.item() == 1  # the host advances it after a self-gathering step
+            cursor.add_(1)
+        else:
+            assert cursor.item() == 3
+        nxt = ring[row + 1 if row + 1 < 4 else 0, :batch].long()
+        torch.testing.assert_close(stage[0][1 - parity, :batch, :in_dim].float(), X[nxt].bfloat16().float())
+        for k, v in lay.views(p_out).items():  # owners copied every parameter through unchanged
+            torch.testing.assert_close(v, lay.views(flat)[k], msg=k)
+        step_idx = ring[row, :batch].cpu()
+        ref_loss, ref_g = mf.reference_step(X.cpu(), T.cpu(), step_idx, params_cpu, act, loss, emulate_bf16=True)
+        torch.testing.assert_close(loss_ring[row].cpu(), ref_loss, rtol=1e-3, atol=1e-5)
+        got = lay.views(g_out)
+        for k in ref_g:
+            exp = ref_g[k] * scale
+            tol = 3e-2 * exp.abs().max().item() + 1e-6
+            err = (got[k].cpu() - exp).abs().max().item()
+            assert err <= tol, f"{k}: max err {err} > {tol}"
 
 
 def test_mlp2_fused_step_sgd_update_pingpong(C):
@@ -155,7 +163,7 @@ def test_mlp2_fused_step_sgd_update_pingpong(C):
     lay, X, T, flat, idx = _mlp_case(in_dim, hidden, out_dim, batch, seed=3)
     ring = idx[:128].view(1, 128).contiguous().to(dev())
     cursor = torch.zeros(1, dtype=torch.int32, device=dev())
-    ticket = torch.zeros(1, dtype=torch.int32, device=dev())
+    stage = mf.make_stage(dev())
     loss_ring = torch.zeros(4, device=dev())
     g_prev = torch.randn_like(flat) * 0.01
     mom_in = torch.randn_like(flat) * 0.01
@@ -163,8 +171,8 @@ def test_mlp2_fused_step_sgd_update_pingpong(C):
     p_out = torch.zeros_like(flat)
     g_out = torch.zeros_like(flat)
     sgd = {"lr": 0.05, "momentum": 0.9, "weight_decay": 1e-3, "nesterov": True}
-    mf.fused_step(X, T, ring, cursor, ticket, loss_ring, flat, p_out, g_prev, g_out, mom_in, mom_out, lay, batch, 4,
-                  "relu", "mse", True, 1.0, sgd, 1.0, False)
+    mf.fused_step(X, T, ring, cursor, stage, loss_ring, flat, p_out, g_prev, g_out, mom_in, mom_out, lay, batch, 4,
+                  "relu", "mse", True, 1.0, sgd, 1.0, False, parity=0, gather_self=True)
     torch.cuda.synchronize()
     buf = mom_in.clone()
     exp_p = mf.apply_sgd_reference(flat, g_prev, buf, sgd, first_step=False)
