@@ -25,7 +25,7 @@ hipError_t dta_flat_sumsq(const float*, int64_t, float*, hipStream_t);
 hipError_t dta_flat_clip(float*, int64_t, const float*, float, hipStream_t);
 hipError_t dta_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 hipError_t dta_mlp2_fused_step(const dta::MlpArgs*, hipStream_t);
-size_t dta_mlp2_lds_bytes(int64_t, int);
+size_t dta_mlp2_lds_bytes(int64_t, int, int);
 
 namespace {
 
@@ -164,7 +164,7 @@ void cast_f32_bf16(torch::Tensor src, torch::Tensor dst, int64_t stream) {
 
 // ----------------------------- fused MLP step -----------------------------
 void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
-                     torch::Tensor x_stage, torch::Tensor t_stage, torch::Tensor loss_ring, torch::Tensor p_in, torch::Tensor p_out,
+                     torch::Tensor loss_cursor, torch::Tensor x_stage, torch::Tensor t_stage, torch::Tensor loss_ring, torch::Tensor p_in, torch::Tensor p_out,
                      torch::Tensor g_prev, torch::Tensor g_out, c10::optional<torch::Tensor> mom_in,
                      c10::optional<torch::Tensor> mom_out, std::vector<int64_t> offsets, int64_t in_dim,
                      int64_t hidden, int64_t out_dim, int64_t B, int64_t own_tiles, int64_t act, int64_t loss_type,
@@ -177,6 +177,8 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
   TORCH_CHECK(idx_ring.scalar_type() == torch::kInt32 && idx_ring.dim() == 2, "idx_ring: int32 [steps, stride]");
   check_gpu(cursor, "cursor");
   TORCH_CHECK(cursor.scalar_type() == torch::kInt32 && cursor.numel() >= 1, "cursor: int32[1]");
+  check_gpu(loss_cursor, "loss_cursor");
+  TORCH_CHECK(loss_cursor.scalar_type() == torch::kInt32 && loss_cursor.numel() >= 1, "loss_cursor: int32[1]");
   check_gpu(x_stage, "x_stage");
   TORCH_CHECK(x_stage.scalar_type() == torch::kBFloat16 && x_stage.numel() == 2 * dta::kMlpStageRows * dta::kMlpStageCols,
               "x_stage: bf16 [2, 128, 32]");
@@ -204,7 +206,9 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
                   offsets[2] + out_dim * hidden <= offsets[3] && total >= need && total < (int64_t)1 << 31,
               "fused MLP: overlapping or oversize flat regions");
   const int bpad = ((B + 31) / 32 <= 1) ? 32 : (((B + 31) / 32 <= 2) ? 64 : 128);
-  TORCH_CHECK(dta_mlp2_lds_bytes(total, bpad) <= 160 * 1024, "fused MLP: parameters too large for the LDS image");
+  const bool has_mom_ = mom_in && mom_in->defined();
+  TORCH_CHECK(dta_mlp2_lds_bytes(total, bpad, has_mom_) <= 160 * 1024,
+              "fused MLP: parameters too large for the LDS image");
   TORCH_CHECK(act >= 0 && act <= 3, "fused MLP: unknown activation code");
   for (auto* t : {&p_in, &p_out, &g_prev, &g_out}) {
     TORCH_CHECK(t->numel() == total, "flat buffers must all have the same length");
@@ -226,6 +230,7 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
   a.T = T.data_ptr<float>();
   a.idx_ring = idx_ring.data_ptr<int>();
   a.cursor = cursor.data_ptr<int>();
+  a.loss_cursor = loss_cursor.data_ptr<int>();
   a.x_stage = reinterpret_cast<unsigned short*>(x_stage.data_ptr());
   a.t_stage = t_stage.data_ptr<float>();
   a.parity = (int)(parity & 1);
@@ -370,7 +375,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("flat_sumsq", &flat_sumsq);
   m.def("flat_clip", &flat_clip);
   m.def("cast_f32_bf16", &cast_f32_bf16);
-  m.def("mlp2_fused_step", &mlp2_fused_step, py::arg("X"), py::arg("T"), py::arg("idx_ring"), py::arg("cursor"),
+  m.def("mlp2_fused_step", &mlp2_fused_step, py::arg("X"), py::arg("T"), py::arg("idx_ring"), py::arg("cursor"), py::arg("loss_cursor"),
         py::arg("x_stage"), py::arg("t_stage"), py::arg("loss_ring"), py::arg("p_in"), py::arg("p_out"), py::arg("g_prev"), py::arg("g_out"),
         py::arg("mom_in"), py::arg("mom_out"), py::arg("offsets"), py::arg("in_dim"), py::arg("hidden"),
         py::arg("out_dim"), py::arg("B"), py::arg("own_tiles"), py::arg("act"), py::arg("loss_type"),

@@ -13,7 +13,8 @@ struct MlpArgs {
   const float* X;        // [N, in_dim]   device-resident dataset features
   const float* T;        // [N, out_dim]  targets
   const int* idx_ring;   // [ring_steps, idx_stride] sampler indices
-  int* cursor;           // global step counter (device; read/advanced by ONE wave)
+  int* cursor;           // sampler step counter (device; read/advanced only by the stager workgroup)
+  int* loss_cursor;      // loss-ring position (device; read/advanced only by workgroup 0)
   unsigned short* x_stage;  // [2][kMlpStageRows][kMlpStageCols] bf16 bits: gathered batch
   float* t_stage;        // [2][kMlpStageRows][8]
   float* loss_ring;      // [loss_len]

@@ -31,13 +31,14 @@
 // (p_in != p_out, g_prev != g_out); the host alternates them every step, so an
 // even number of steps captured in one hipGraph replays cleanly.
 //
-// The sampler gather is software-pipelined across steps: while the owner waves
-// run the backward, one spare wave of workgroup 0 reads the device cursor c,
-// gathers the micro-batch of step c+1 (indices from the device index ring) into
-// a staging slot and advances the cursor -- it is the ONLY reader/writer of the
-// cursor, so no cross-workgroup ticket is needed.  Every workgroup of the next
-// step then loads its batch from the staging slot in one round trip, in
-// parallel with the parameter loads.  A captured multi-step graph therefore
+// The sampler gather is software-pipelined across steps: one extra "stager"
+// workgroup (the last block of the grid) reads the device cursor c, gathers the
+// micro-batch of step c+1 (indices from the device index ring) into a staging
+// slot and advances the cursor -- it is the ONLY reader/writer of the cursor, so
+// no cross-workgroup ticket is needed, and its dependent load chain runs beside
+// the compute workgroups instead of on the critical path.  Every workgroup of
+// the next step then loads its batch from the staging slot in one round trip,
+// in parallel with the parameter loads.  A captured multi-step graph therefore
 // walks the index ring without host involvement.
 #include "common.h"
 #include "mlp_fused.h"
@@ -96,19 +97,53 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   float* Tg = reinterpret_cast<float*>(Tw + NWAVE * 2 * 32 * TS);  // [BP][8] targets
   float* Ys = Tg + BP * 8;                                 // [BP][8]
   float* dYw = Ys + BP * 8;                                // [NWAVE][BP][8] wave-private dY
+  float* Mf = dYw + NWAVE * BP * 8;                        // [total] momentum image (momentum only)
 
 #define DTA_STAMP(k) \
   if (a.dbg_stamps && tid == 0) a.dbg_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();
   DTA_STAMP(0);
+  if (a.dbg_stamps && tid == 0) a.dbg_stamps[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memtime();
+
+  // ---------------- the stager workgroup: batch of the NEXT step ----------------
+  if (blockIdx.x == gridDim.x - 1) {
+    if (wave != 0) return;
+    const int cur = *a.cursor;
+    const int* idx = a.idx_ring + (int64_t)((cur + 1) % a.ring_steps) * a.idx_stride;
+    unsigned short* xs = a.x_stage + (size_t)(1 - a.parity) * kMlpStageRows * kMlpStageCols;
+    float* ts = a.t_stage + (size_t)(1 - a.parity) * kMlpStageRows * 8;
+    const int rows = min(a.idx_stride, kMlpStageRows);
+    for (int r = lane; r < rows; r += 64) {  // rows past the batch read valid zero-padded ring entries
+      const int64_t src = idx[r];
+      float x[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) x[k] = k < IN ? a.X[src * IN + k] : 0.f;
+      float t[8];
+#pragma unroll
+      for (int o = 0; o < 8; ++o) t[o] = o < OUT ? a.T[src * OUT + o] : 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f2bf(x[c * 8 + j]);
+        *reinterpret_cast<bf16x8*>(xs + r * kMlpStageCols + c * 8) = v;
+      }
+      *reinterpret_cast<float4*>(ts + r * 8) = make_float4(t[0], t[1], t[2], t[3]);
+      *reinterpret_cast<float4*>(ts + r * 8 + 4) = make_float4(t[4], t[5], t[6], t[7]);
+    }
+    // with gather_self the compute workgroups read the cursor too: the host advances it
+    if (!a.gather_self && lane == 0) *a.cursor = cur + 1;
+    return;
+  }
 
   const int NT = H >> 5;
   const int ct0 = blockIdx.x * a.own_tiles;
   const int ct1 = min(ct0 + a.own_tiles, NT);
   const int h0 = ct0 * 32, h1 = ct1 * 32;
-  const bool stager = blockIdx.x == 0 && wave == NWAVE - 1;
+  const bool stager = blockIdx.x == 0 && wave == NWAVE - 1;  // also computes loss + db2
+  const int lcur = stager ? *a.loss_cursor : 0;
 
   // ---------------- phase 0: loads (params first, then the staged batch) ----------------
-  constexpr int U = 4;
+  constexpr int U = 8;
   const int n4 = (int)(a.total >> 2);
   const bool has_mom = a.mom_in != nullptr;
   float4 pv[U], gv[U], mv[U];
@@ -172,53 +207,48 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
     }
   }
 
-  // pending optimizer update -> LDS image (+ owner write-back)
+  // pending optimizer update -> LDS image(s).  A lean streaming loop: no
+  // per-element region / ownership logic (owners write back from LDS below).
   {
-    const int w1_lo = h0 * IN, w1_hi = h1 * IN;
-    const int b1_lo = o_b1 + h0, b1_hi = o_b1 + h1;
+    const bool plain = !has_mom && a.weight_decay == 0.f && !a.maximize;
+    const float lr_s = a.lr * a.prev_grad_scale;
 #pragma unroll 1
     for (int base = 0; base < n4; base += NTHR * U) {
       if (base > 0) issue(base);
+      if (!a.apply_update) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e4 = base + u * NTHR + tid;
-        if (e4 < n4) {
-          float4 p = pv[u], m = mv[u];
-          if (a.apply_update) {
+        for (int u = 0; u < U; ++u) {
+          const int e4 = base + u * NTHR + tid;
+          if (e4 < n4) {
+            reinterpret_cast<float4*>(Pf)[e4] = pv[u];
+            if (has_mom) reinterpret_cast<float4*>(Mf)[e4] = mv[u];
+          }
+        }
+      } else if (plain) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e4 = base + u * NTHR + tid;
+          if (e4 < n4) {
+            float4 p = pv[u];
+            p.x -= lr_s * gv[u].x;
+            p.y -= lr_s * gv[u].y;
+            p.z -= lr_s * gv[u].z;
+            p.w -= lr_s * gv[u].w;
+            reinterpret_cast<float4*>(Pf)[e4] = p;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e4 = base + u * NTHR + tid;
+          if (e4 < n4) {
+            float4 p = pv[u], m = mv[u];
             p.x = sgd_apply(p.x, gv[u].x, &m.x, a);
             p.y = sgd_apply(p.y, gv[u].y, &m.y, a);
             p.z = sgd_apply(p.z, gv[u].z, &m.z, a);
             p.w = sgd_apply(p.w, gv[u].w, &m.w, a);
-          }
-          reinterpret_cast<float4*>(Pf)[e4] = p;
-          const int e = e4 * 4;
-          int lo, hi;  // owned element range that may intersect this float4
-          if (e < o_b1) {
-            lo = w1_lo;
-            hi = w1_hi;
-          } else if (e < o_w2) {
-            lo = b1_lo;
-            hi = b1_hi;
-          } else if (e < o_b2) {
-            const int row = (e - o_w2) / H;  // H % 4 == 0: the float4 lies in one output row
-            lo = (row < OUT) ? o_w2 + row * H + h0 : 0;
-            hi = (row < OUT) ? o_w2 + row * H + h1 : 0;
-          } else {
-            lo = o_b2;
-            hi = (blockIdx.x == 0) ? o_b2 + OUT : o_b2;
-          }
-          if (e >= lo && e + 4 <= hi) {
-            reinterpret_cast<float4*>(a.p_out)[e4] = p;
-            if (has_mom) reinterpret_cast<float4*>(a.mom_out)[e4] = m;
-          } else if (e + 4 > lo && e < hi) {
-            const float pe[4] = {p.x, p.y, p.z, p.w};
-            const float me[4] = {m.x, m.y, m.z, m.w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-              if (e + c >= lo && e + c < hi) {
-                a.p_out[e + c] = pe[c];
-                if (has_mom) a.mom_out[e + c] = me[c];
-              }
+            reinterpret_cast<float4*>(Pf)[e4] = p;
+            if (has_mom) reinterpret_cast<float4*>(Mf)[e4] = m;
           }
         }
       }
@@ -226,6 +256,23 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   }
   __syncthreads();
   DTA_STAMP(1);
+  // owner write-back of the updated slice (all regions 16-byte aligned: h0 % 32 == 0)
+  {
+    auto copy_out = [&](int lo, int n) {  // n % 4 == 0
+      for (int e4 = tid; e4 < (n >> 2); e4 += NTHR) {
+        const int e = lo + 4 * e4;
+        *reinterpret_cast<float4*>(a.p_out + e) = *reinterpret_cast<const float4*>(Pf + e);
+        if (has_mom) *reinterpret_cast<float4*>(a.mom_out + e) = *reinterpret_cast<const float4*>(Mf + e);
+      }
+    };
+    copy_out(h0 * IN, (h1 - h0) * IN);
+    copy_out(o_b1 + h0, h1 - h0);
+    for (int o = 0; o < OUT; ++o) copy_out(o_w2 + o * H + h0, h1 - h0);
+    if (blockIdx.x == 0 && tid < OUT) {
+      a.p_out[o_b2 + tid] = Pf[o_b2 + tid];
+      if (has_mom) a.mom_out[o_b2 + tid] = Mf[o_b2 + tid];
+    }
+  }
 
   // ---------------- phase 1: forward (transposed) ----------------
   const int nks = (IN + 15) >> 4;  // K = 16 steps over the (zero-padded) input dim
@@ -304,7 +351,7 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   // the rest of the (redundant) forward, spread over all waves
   {
     const int nrest = NT - (ct1 - ct0);
-#pragma unroll 1
+#pragma unroll 2
     for (int t = wave; t < nrest; t += NWAVE) {
       const int ct = t < ct0 ? t : t + (ct1 - ct0);
 #pragma unroll
@@ -328,9 +375,6 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
   // ---------------- phase 2: loss + dY (per wave, no further barrier) ----------------
   float* dYme = dYw + wave * BP * 8;
   float lossr = 0.f;
-  float db2p[8];
-#pragma unroll
-  for (int o = 0; o < 8; ++o) db2p[o] = 0.f;
   if (owner_wave || stager) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -376,10 +420,7 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
       }
       if (hh == 0) {
 #pragma unroll
-        for (int o = 0; o < 8; ++o) {
-          dYme[r * 8 + o] = dy[o];
-          db2p[o] += dy[o];
-        }
+        for (int o = 0; o < 8; ++o) dYme[r * 8 + o] = dy[o];
       }
     }
     wave_lds_fence();
@@ -432,60 +473,45 @@ __global__ void __launch_bounds__(NTHR) mlp2_fused_step_kernel(MlpArgs a) {
       wave_lds_fence();
     }
     const float gs = a.grad_scale;
+    // predicates hoisted out of the register loops (one branch per store group)
+    if (r32 < IN) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int hr = my_ct * 32 + mfma32_row(i, lane);
-      if (r32 < IN) a.g_out[hr * IN + r32] = dw1[i] * gs;
-      else if (r32 == IN) a.g_out[o_b1 + hr] = dw1[i] * gs;
-      if (r32 < OUT) a.g_out[o_w2 + r32 * H + hr] = dw2[i] * gs;
+      for (int i = 0; i < 16; ++i) a.g_out[(my_ct * 32 + mfma32_row(i, lane)) * IN + r32] = dw1[i] * gs;
+    } else if (r32 == IN) {  // rows 8q + 4hh + 0..3 are contiguous: float4 stores
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(a.g_out + o_b1 + my_ct * 32 + 8 * q + 4 * hh) =
+            make_float4(dw1[4 * q] * gs, dw1[4 * q + 1] * gs, dw1[4 * q + 2] * gs, dw1[4 * q + 3] * gs);
+    }
+    if (r32 < OUT) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(a.g_out + o_w2 + r32 * H + my_ct * 32 + 8 * q + 4 * hh) =
+            make_float4(dw2[4 * q] * gs, dw2[4 * q + 1] * gs, dw2[4 * q + 2] * gs, dw2[4 * q + 3] * gs);
     }
   }
 
-  // ------- the stager: loss, db2, and the NEXT step's gathered batch -------
+  // ------- workgroup 0's last wave: loss and db2 -------
   if (stager) {
     const float lsum = wave_sum(lossr);
-#pragma unroll
-    for (int o = 0; o < 8; ++o) db2p[o] = wave_sum(db2p[o]);
-    const int cur = *a.cursor;
     if (lane == 0) {
       const float scale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
-      a.loss_ring[cur % a.loss_len] = lsum * scale;
+      a.loss_ring[lcur % a.loss_len] = lsum * scale;
+      *a.loss_cursor = lcur + 1;
     }
-    if (lane < OUT) {
+    for (int o = 0; o < OUT; ++o) {  // db2[o] = sum_b dY[b][o]
       float v = 0.f;
 #pragma unroll
-      for (int o = 0; o < 8; ++o)
-        if (o == lane) v = db2p[o];
-      a.g_out[o_b2 + lane] = v * a.grad_scale;
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = rt * 32 + r32;
+        if (hh == 0 && r < B) v += dYme[r * 8 + o];
+      }
+      v = wave_sum(v);
+      if (lane == 0) a.g_out[o_b2 + o] = v * a.grad_scale;
     }
-    // gather step cur+1 into the other staging slot (rows beyond the batch read
-    // valid zero-padded ring entries and are masked by the consumer)
-    // (with gather_self nobody else touches the cursor in this launch; the host advances it)
-    const int* idx = a.idx_ring + (int64_t)((cur + 1) % a.ring_steps) * a.idx_stride;
-    unsigned short* xs = a.x_stage + (size_t)(1 - a.parity) * kMlpStageRows * kMlpStageCols;
-    float* ts = a.t_stage + (size_t)(1 - a.parity) * kMlpStageRows * 8;
-    const int rows = min(a.idx_stride, kMlpStageRows);
-    for (int r = lane; r < rows; r += 64) {
-      const int64_t src = idx[r];
-      bf16x8 v[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = c * 8 + j;
-          v[c][j] = f2bf(k < IN ? a.X[src * IN + k] : 0.f);
-        }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(xs + r * kMlpStageCols + c * 8) = v[c];
-      float t[8];
-#pragma unroll
-      for (int o = 0; o < 8; ++o) t[o] = o < OUT ? a.T[src * OUT + o] : 0.f;
-      *reinterpret_cast<float4*>(ts + r * 8) = make_float4(t[0], t[1], t[2], t[3]);
-      *reinterpret_cast<float4*>(ts + r * 8 + 4) = make_float4(t[4], t[5], t[6], t[7]);
-    }
-    if (!a.gather_self && lane == 0) *a.cursor = cur + 1;
   }
   DTA_STAMP(4);
+  if (a.dbg_stamps && tid == 0) a.dbg_stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime();
 #undef DTA_STAMP
 }
 
@@ -516,9 +542,9 @@ static hipError_t launch_act(const MlpArgs& a, int grid, size_t lds, hipStream_t
 
 using namespace dta;
 
-size_t dta_mlp2_lds_bytes(int64_t total, int bpad) {
-  return (size_t)total * 4 + (size_t)bpad * XS * 2 + 32 * (size_t)(bpad + 8) * 2 + NWAVE * 2 * 32 * TS * 2 +
-         2 * (size_t)bpad * 32 + (size_t)NWAVE * bpad * 32;
+size_t dta_mlp2_lds_bytes(int64_t total, int bpad, int has_mom) {
+  return (size_t)total * 4 * (has_mom ? 2 : 1) + (size_t)bpad * XS * 2 + 32 * (size_t)(bpad + 8) * 2 +
+         NWAVE * 2 * 32 * TS * 2 + 2 * (size_t)bpad * 32 + (size_t)NWAVE * bpad * 32;
 }
 
 // Returns hipErrorInvalidValue for shapes the fused kernel does not cover;
@@ -531,10 +557,10 @@ hipError_t dta_mlp2_fused_step(const MlpArgs* args, hipStream_t st) {
     return hipErrorInvalidValue;
   const int RT = (a.B + 31) / 32;
   const int rt = RT <= 1 ? 1 : (RT <= 2 ? 2 : 4);
-  const size_t lds = dta_mlp2_lds_bytes(a.total, rt * 32);
+  const size_t lds = dta_mlp2_lds_bytes(a.total, rt * 32, a.mom_in != nullptr);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int nt = a.hidden / 32;
-  const int grid = (nt + a.own_tiles - 1) / a.own_tiles;
+  const int grid = (nt + a.own_tiles - 1) / a.own_tiles + 1;  // + the stager workgroup
   if (rt == 1) return launch_act<1>(a, grid, lds, st);
   if (rt == 2) return launch_act<2>(a, grid, lds, st);
   return launch_act<4>(a, grid, lds, st);

@@ -53,7 +53,8 @@ def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torc
         return "optimizer is not SGD"
     if g.get("momentum", 0) and g.get("dampening", 0):
         return "SGD dampening not fused"
-    if not mf.supported(module.input_size, module.hidden[0], module.output_size, loader.batch_size):
+    if not mf.supported(module.input_size, module.hidden[0], module.output_size, loader.batch_size,
+                        momentum=bool(g.get("momentum", 0))):
         return "shape outside the fused kernel's limits"
     return None
 

@@ -63,15 +63,17 @@ def make_layout(in_dim: int, hidden: int, out_dim: int) -> MlpLayout:
     return MlpLayout(in_dim, hidden, out_dim, o_w1, o_b1, o_w2, o_b2, total)
 
 
-def lds_bytes(in_dim: int, hidden: int, out_dim: int, batch: int) -> int:
-    """LDS footprint: fp32 image of the flat params + bf16 X tile + small buffers."""
+def lds_bytes(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool = False) -> int:
+    """LDS footprint: fp32 image of the flat params (+ momentum image) + bf16 X
+    tiles + wave-private transpose / dY tiles (host mirror of the kernel's)."""
     rt = (batch + 31) // 32
     bpad = 32 if rt <= 1 else (64 if rt <= 2 else 128)
     total = make_layout(in_dim, hidden, out_dim).total
-    return total * 4 + bpad * 80 + 32 * (bpad + 8) * 2 + 8 * 2 * 32 * 40 * 2 + 2 * bpad * 32 + 8 * bpad * 32
+    return (total * 4 * (2 if momentum else 1) + bpad * 80 + 32 * (bpad + 8) * 2 + 8 * 2 * 32 * 40 * 2
+            + 2 * bpad * 32 + 8 * bpad * 32)
 
 
-def supported(in_dim: int, hidden: int, out_dim: int, batch: int) -> bool:
+def supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool = False) -> bool:
     """Shapes covered by the fused kernel (host mirror of the kernel's limits)."""
     return (
         1 <= in_dim <= 31
@@ -79,7 +81,7 @@ def supported(in_dim: int, hidden: int, out_dim: int, batch: int) -> bool:
         and hidden >= 32
         and hidden % 32 == 0
         and 1 <= batch <= 128
-        and lds_bytes(in_dim, hidden, out_dim, batch) <= LDS_LIMIT
+        and lds_bytes(in_dim, hidden, out_dim, batch, momentum) <= LDS_LIMIT
     )
 
 
@@ -89,7 +91,8 @@ STAGE_ROWS, STAGE_COLS = 128, 32
 def make_stage(device):
     """Double-buffered staging slots for the pipelined batch gather."""
     return (torch.zeros(2, STAGE_ROWS, STAGE_COLS, dtype=torch.bfloat16, device=device),
-            torch.zeros(2, STAGE_ROWS, 8, dtype=torch.float32, device=device))
+            torch.zeros(2, STAGE_ROWS, 8, dtype=torch.float32, device=device),
+            torch.zeros(1, dtype=torch.int32, device=device))  # loss cursor
 
 
 def fused_step(
@@ -105,7 +108,7 @@ def fused_step(
     step's batch is staged into slot ``1 - parity``."""
     C = native()
     C.mlp2_fused_step(
-        X, T, idx_ring, cursor, stage[0], stage[1], loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+        X, T, idx_ring, cursor, stage[2], stage[0], stage[1], loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
         layout.offsets, layout.in_dim, layout.hidden, layout.out_dim, int(batch), int(own_tiles),
         ACTIVATIONS[act], LOSSES[loss], bool(apply_update), int(parity), bool(gather_self), float(grad_scale),
         float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)), float(sgd.get("dampening", 0.0)),

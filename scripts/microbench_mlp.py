@@ -51,8 +51,9 @@ def main():
         nwg = (args.hidden // 32 + args.own - 1) // args.own
         d = (st[:nwg, 1:5] - st[:nwg, 0:4]).float().mean(0) / 100.0  # 100 MHz ticks -> us
         tot = (st[:nwg, 4].max() - st[:nwg, 0].min()).item() / 100.0
-        d[3] = (st[0, 4] - st[0, 3]).item() / 100.0  # WG0 tail incl. the stager
-        phase_us.append(d.tolist() + [tot])
+        d[3] = (st[0, 4] - st[0, 3]).item() / 100.0  # WG0 tail
+        clk = ((st[:nwg, 6] - st[:nwg, 5]).float() / (st[:nwg, 4] - st[:nwg, 0]).float() * 100.0).mean().item()
+        phase_us.append(d.tolist() + [tot, clk])
     phase_us = torch.tensor(phase_us).median(0).values.tolist()
     t0 = time.perf_counter()
     for i in range(args.iters):
@@ -106,7 +107,7 @@ def main():
     torch_us = (time.perf_counter() - t0) / 500 * 1e6
     print(json.dumps({"hidden": args.hidden, "batch": args.batch, "own_tiles": args.own, "eager_us": eager_us,
                       "graph_us_per_step": graph_us, "torch_eager_us": torch_us,
-                      "phase_us[p0,p1,p2,p3,total]": [round(x, 2) for x in phase_us]}))
+                      "phase_us[p0,p1,p2,p3,total,clockMHz]": [round(x, 2) for x in phase_us]}))
 
 
 if __name__ == "__main__":

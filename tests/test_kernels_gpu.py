@@ -126,7 +126,7 @@ def test_mlp2_fused_step_no_update(C, in_dim, hidden, out_dim, batch, act, loss,
     scale = 0.5
     params_cpu = {k: v.cpu() for k, v in lay.views(flat).items()}
     # step A gathers its own batch (ring row 1) and stages row 2; step B reads the staged batch
-    for parity, gather_self, row in ((0, True, 1), (1, False, 2)):
+    for step, (parity, gather_self, row) in enumerate(((0, True, 1), (1, False, 2))):
         p_out = torch.full_like(flat, float("nan"))
         g_prev = torch.zeros_like(flat)
         g_out = torch.zeros_like(flat)
@@ -145,7 +145,8 @@ def test_mlp2_fused_step_no_update(C, in_dim, hidden, out_dim, batch, act, loss,
             torch.testing.assert_close(v, lay.views(flat)[k], msg=k)
         step_idx = ring[row, :batch].cpu()
         ref_loss, ref_g = mf.reference_step(X.cpu(), T.cpu(), step_idx, params_cpu, act, loss, emulate_bf16=True)
-        torch.testing.assert_close(loss_ring[row].cpu(), ref_loss, rtol=1e-3, atol=1e-5)
+        torch.testing.assert_close(loss_ring[step].cpu(), ref_loss, rtol=1e-3, atol=1e-5)
+        assert int(stage[2].item()) == step + 1
         got = lay.views(g_out)
         for k in ref_g:
             exp = ref_g[k] * scale
