@@ -158,6 +158,7 @@ class FullyShardedDataParallel(nn.Module):
         self.prefetch = prefetch
         self.module = module
         self._orig_names = [n for n, p in module.named_parameters() if p.requires_grad]
+        self._sd_keys = list(module.state_dict().keys())  # reference key order (params + buffers)
         policy = _policy_fn(wrap_policy)
 
         # ---- collect units (top-level policy matches, then the root) ----
@@ -343,7 +344,7 @@ class FullyShardedDataParallel(nn.Module):
         if keep:
             for name, b in self.module.named_buffers():
                 out[name] = b.detach().cpu().clone() if offload_to_cpu else b.detach().clone()
-            ordered = {k: out[k] for k in self._orig_names if k in out}
+            ordered = {k: out[k] for k in self._sd_keys if k in out}
             ordered.update({k: v for k, v in out.items() if k not in ordered})
             return ordered
         return {}

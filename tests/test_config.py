@@ -1,0 +1,89 @@
+"""Hydra-compatible config loader (reference conf/ tree + override grammar)."""
+import os
+from pathlib import Path
+
+import pytest
+
+from distributed_training_amd.config import ConfigError, compose, parse_override, prepare_run_dir, split_argv
+
+CONF = Path(__file__).resolve().parent.parent / "conf"
+
+
+def test_defaults_match_reference_keys():
+    cfg = compose(CONF, "config", [])
+    assert cfg.model.input_size == 20 and cfg.model.output_size == 1
+    t = cfg.train
+    assert (t.batch_size, t.total_epochs, t.save_every, t.snapshot_path, t.dataset_size, t.learning_rate) == \
+        (32, 10, 2, "snapshot.pt", 2048, 0.001)
+    assert t.device == "auto" and t.parallel_strategy == "ddp"
+    assert cfg.train.get("nonexistent", "dflt") == "dflt"
+    assert cfg.logging.level == "INFO"
+    assert cfg.logging.file.endswith("train.log")
+    assert cfg.logging.file.startswith(cfg.hydra.runtime.output_dir)
+    assert cfg.hydra.job.chdir is True
+
+
+def test_overrides_set_add_delete_group():
+    cfg = compose(CONF, "config", ["train.batch_size=64", "+train.new_key=abc", "~train.seed", "model=mlp2",
+                                   "++train.learning_rate=0.5", "train.parallel_strategy=fsdp"])
+    assert cfg.train.batch_size == 64
+    assert cfg.train.new_key == "abc"
+    assert "seed" not in cfg.train
+    assert cfg.model.hidden_size == 512 and cfg.model.name == "mlp2"
+    assert cfg.train.learning_rate == 0.5
+    assert cfg.train.parallel_strategy == "fsdp"
+    assert cfg.hydra.runtime.choices.model == "mlp2"
+
+
+def test_override_errors():
+    with pytest.raises(ConfigError):
+        compose(CONF, "config", ["train.not_there=1"])
+    with pytest.raises(ConfigError):
+        compose(CONF, "config", ["+train.batch_size=3"])
+    with pytest.raises(ConfigError):
+        compose(CONF, "config", ["model=does_not_exist"])
+    with pytest.raises(ConfigError):
+        parse_override("noequals")
+
+
+def test_value_parsing_and_interpolation(tmp_path, monkeypatch):
+    d = tmp_path / "c"
+    (d / "grp").mkdir(parents=True)
+    (d / "grp" / "a.yaml").write_text("x: 1\ny: ${grp.x}\n")
+    (d / "main.yaml").write_text(
+        "defaults:\n  - grp: a\n  - _self_\n"
+        "name: run-${now:%Y}\nenv: ${oc.env:DTA_TEST_VAR,fallback}\nlst: [1, 2]\n"
+        "out: ${hydra:runtime.output_dir}/f.txt\nhydra:\n  run:\n    dir: " + str(tmp_path / "o") + "\n")
+    monkeypatch.setenv("DTA_TEST_VAR", "hello")
+    cfg = compose(d, "main", ["grp.x=7", "+flag=true", "+f=1.5e-3", "+s=null"])
+    assert cfg.grp.y == 7
+    assert cfg.name.startswith("run-2")
+    assert cfg.env == "hello"
+    assert cfg.flag is True and abs(cfg.f - 1.5e-3) < 1e-12 and cfg.s is None
+    assert cfg.out == str(tmp_path / "o") + "/f.txt"
+
+
+def test_prepare_run_dir_chdir(tmp_path):
+    cwd = os.getcwd()
+    try:
+        cfg = compose(CONF, "config", [f"hydra.run.dir={tmp_path}/run1"])
+        out = prepare_run_dir(cfg)
+        assert out == tmp_path / "run1"
+        assert os.getcwd() == str(tmp_path / "run1")
+        assert (out / ".hydra" / "config.yaml").exists()
+    finally:
+        os.chdir(cwd)
+
+
+def test_split_argv_and_legacy_cli():
+    ov, rest = split_argv(["5", "2", "--batch_size", "16", "train.loss=mse", "+x=1", "~train.seed"])
+    assert ov == ["train.loss=mse", "+x=1", "~train.seed"]
+    assert rest == ["5", "2", "--batch_size", "16"]
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mmn", CONF.parent / "src" / "multigpu_multi_node.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.parse(["5", "2", "--batch_size", "16", "model=mlp2"]) == [
+        "model=mlp2", "train.total_epochs=5", "train.save_every=2", "train.batch_size=16"]
+    assert mod.parse([]) == []
