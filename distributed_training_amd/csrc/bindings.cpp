@@ -14,6 +14,39 @@
 #include "mlp_fused.h"
 #include "rccl_comm.h"
 
+namespace dta {
+struct AttnArgs {  // mirror of csrc/attention.hip
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  const void* dout;
+  float* delta;
+  float* dq_acc;
+  void* dk;
+  void* dv;
+  int64_t q_sb, q_ss, k_sb, k_ss, v_sb, v_ss;
+  int64_t o_sb, o_ss, do_sb, do_ss;
+  int64_t dk_sb, dk_ss, dv_sb, dv_ss;
+  int B, S, H, Hkv;
+  float scale;
+};
+}  // namespace dta
+hipError_t dta_attn_fwd(const dta::AttnArgs*, int, bool, hipStream_t);
+hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, float*, float*, int64_t, int, float,
+                        hipStream_t);
+hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
+                        void*, void*, int64_t, int, int, int, hipStream_t);
+hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
+hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
+hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
+hipError_t dta_swiglu_bwd(const void*, const void*, void*, int64_t, int, hipStream_t);
+hipError_t dta_rope(void*, const float*, const float*, int, int, int, int, int64_t, int64_t, float, hipStream_t);
+hipError_t dta_cross_entropy(const void*, void*, const int64_t*, float*, int64_t, int64_t, float, int64_t,
+                             hipStream_t);
+hipError_t dta_attn_bwd(const dta::AttnArgs*, int, bool, hipStream_t);
+
 // ---- launchers implemented in the .hip translation units ----
 hipError_t dta_flat_sgd(const float*, float*, const float*, float*, void*, int64_t, float, float, float, float, float,
                         int, int, int, hipStream_t);
@@ -276,6 +309,185 @@ void mlp2_fused_step(torch::Tensor X, torch::Tensor T, torch::Tensor idx_ring, t
   hip_ok(dta_mlp2_fused_step(&a, pick_stream(stream)), "mlp2_fused_step");
 }
 
+// ----------------------------- attention -----------------------------
+// q/k/v/o/dout/dk/dv: [B, S, heads, D] views with a contiguous last dim and a
+// head stride of D (e.g. slices of a fused QKV projection output).
+void check_bshd(const torch::Tensor& t, const char* name, int64_t B, int64_t S, int64_t heads, int64_t D) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == S && t.size(2) == heads && t.size(3) == D, name,
+              " must be [B, S, heads, D]");
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D, name, ": last dim contiguous and head stride == D required");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0,
+              name, ": rows must be 16-byte aligned");
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, bool causal, double scale,
+                                    int64_t stream) {
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
+  TORCH_CHECK(Hkv >= 1 && H % Hkv == 0, "attention: H must be a multiple of Hkv");
+  check_bshd(q, "q", B, S, H, D);
+  check_bshd(k, "k", B, S, Hkv, D);
+  check_bshd(v, "v", B, S, Hkv, D);
+  auto o = torch::empty({B, S, H, D}, q.options());
+  auto lse = torch::empty({B, H, S}, q.options().dtype(torch::kFloat32));
+  dta::AttnArgs a{};
+  a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr(); a.o = o.data_ptr(); a.lse = lse.data_ptr<float>();
+  a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.k_sb = k.stride(0); a.k_ss = k.stride(1);
+  a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.o_sb = o.stride(0); a.o_ss = o.stride(1);
+  a.B = (int)B; a.S = (int)S; a.H = (int)H; a.Hkv = (int)Hkv; a.scale = (float)scale;
+  hip_ok(dta_attn_fwd(&a, (int)D, causal, pick_stream(stream)), "attn_fwd");
+  return {o, lse};
+}
+
+std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
+                                    torch::Tensor o, torch::Tensor lse, bool causal, double scale, int64_t stream) {
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
+  TORCH_CHECK(Hkv >= 1 && H % Hkv == 0, "attention: H must be a multiple of Hkv");
+  check_bshd(q, "q", B, S, H, D);
+  check_bshd(k, "k", B, S, Hkv, D);
+  check_bshd(v, "v", B, S, Hkv, D);
+  check_bshd(o, "o", B, S, H, D);
+  check_bshd(dout, "dout", B, S, H, D);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * S,
+              "lse must be f32 [B, H, S]");
+  auto delta = torch::empty({B, H, S}, lse.options());
+  auto dq_acc = torch::zeros({B, S, H, D}, lse.options());
+  auto dk = torch::empty({B, S, Hkv, D}, q.options());
+  auto dv = torch::empty({B, S, Hkv, D}, q.options());
+  dta::AttnArgs a{};
+  a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr(); a.o = o.data_ptr(); a.lse = lse.data_ptr<float>();
+  a.dout = dout.data_ptr(); a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>();
+  a.dk = dk.data_ptr(); a.dv = dv.data_ptr();
+  a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.k_sb = k.stride(0); a.k_ss = k.stride(1);
+  a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.o_sb = o.stride(0); a.o_ss = o.stride(1);
+  a.do_sb = dout.stride(0); a.do_ss = dout.stride(1);
+  a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1);
+  a.B = (int)B; a.S = (int)S; a.H = (int)H; a.Hkv = (int)Hkv; a.scale = (float)scale;
+  hip_ok(dta_attn_bwd(&a, (int)D, causal, pick_stream(stream)), "attn_bwd");
+  auto dq = torch::empty({B, S, H, D}, q.options());
+  hip_ok(dta_cast_f32_bf16(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.numel(), pick_stream(stream)), "dq cast");
+  return {dq, dk, dv};
+}
+
+// ----------------------------- transformer elementwise / norm ops -----------------------------
+void check_bf16_2d(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16 && t.is_contiguous(), name,
+              " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// returns (y, mean, rstd); mean is empty for RMSNorm
+std::vector<torch::Tensor> norm_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool rms,
+                                    double eps, int64_t stream) {
+  check_bf16_2d(x, "x");
+  check_bf16_2d(w, "weight");
+  const int64_t C = x.size(-1), N = x.numel() / C;
+  TORCH_CHECK(w.numel() == C && C % 8 == 0 && C <= 8192, "norm: C % 8 == 0, C <= 8192, weight [C]");
+  if (!rms) {
+    TORCH_CHECK(b && b->defined(), "LayerNorm needs a bias");
+    check_bf16_2d(*b, "bias");
+    TORCH_CHECK(b->numel() == C, "bias [C]");
+  }
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({N}, x.options().dtype(torch::kFloat32));
+  auto mean = rms ? torch::empty({0}, rstd.options()) : torch::empty({N}, rstd.options());
+  hip_ok(dta_norm_fwd(rms, x.data_ptr(), w.data_ptr(), rms ? nullptr : b->data_ptr(), y.data_ptr(),
+                      rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)C, (float)eps,
+                      pick_stream(stream)),
+         "norm_fwd");
+  return {y, mean, rstd};
+}
+
+// returns (dx, dw, db); dw/db dtype follow the weight
+std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
+                                    torch::Tensor rstd, bool rms, int64_t stream) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(x, "x");
+  check_bf16_2d(w, "weight");
+  const int64_t C = x.size(-1), N = x.numel() / C;
+  TORCH_CHECK(dy.numel() == x.numel() && w.numel() == C, "norm_bwd: shape mismatch");
+  TORCH_CHECK(rstd.numel() == N && (rms || mean.numel() == N), "norm_bwd: stats shape");
+  const int rpb = 64;
+  const int64_t nblk = (N + rpb - 1) / rpb;
+  auto f32 = x.options().dtype(torch::kFloat32);
+  auto dwp = torch::empty({nblk, C}, f32);
+  auto dbp = rms ? torch::empty({0}, f32) : torch::empty({nblk, C}, f32);
+  auto dx = torch::empty_like(x);
+  auto dw = torch::empty({C}, w.options());
+  auto db = rms ? torch::empty({0}, w.options()) : torch::empty({C}, w.options());
+  hip_ok(dta_norm_bwd(rms, dy.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), dx.data_ptr(), dwp.data_ptr<float>(),
+                      rms ? nullptr : dbp.data_ptr<float>(), dw.data_ptr(), rms ? nullptr : db.data_ptr(), N, (int)C,
+                      rpb, 0, pick_stream(stream)),
+         "norm_bwd");
+  return {dx, dw, db};
+}
+
+torch::Tensor gelu_fwd(torch::Tensor x, int64_t stream) {
+  check_bf16_2d(x, "x");
+  auto y = torch::empty_like(x);
+  hip_ok(dta_gelu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), pick_stream(stream)), "gelu_fwd");
+  return y;
+}
+torch::Tensor gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t stream) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(x, "x");
+  TORCH_CHECK(dy.numel() == x.numel(), "gelu_bwd: size mismatch");
+  auto dx = torch::empty_like(x);
+  hip_ok(dta_gelu_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), pick_stream(stream)), "gelu_bwd");
+  return dx;
+}
+torch::Tensor swiglu_fwd(torch::Tensor ab, int64_t stream) {
+  check_bf16_2d(ab, "ab");
+  const int64_t F2 = ab.size(-1), N = ab.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: last dim must be 2F with F % 8 == 0");
+  auto sizes = ab.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto y = torch::empty(sizes, ab.options());
+  hip_ok(dta_swiglu_fwd(ab.data_ptr(), y.data_ptr(), N, (int)(F2 / 2), pick_stream(stream)), "swiglu_fwd");
+  return y;
+}
+torch::Tensor swiglu_bwd(torch::Tensor dy, torch::Tensor ab, int64_t stream) {
+  check_bf16_2d(dy, "dy");
+  check_bf16_2d(ab, "ab");
+  const int64_t F2 = ab.size(-1), N = ab.numel() / F2;
+  TORCH_CHECK(dy.numel() == N * F2 / 2, "swiglu_bwd: size mismatch");
+  auto dab = torch::empty_like(ab);
+  hip_ok(dta_swiglu_bwd(dy.data_ptr(), ab.data_ptr(), dab.data_ptr(), N, (int)(F2 / 2), pick_stream(stream)),
+         "swiglu_bwd");
+  return dab;
+}
+// in place on a [B, S, heads, D] view (last dim contiguous, head stride D)
+void rope_(torch::Tensor x, torch::Tensor cos, torch::Tensor sin, bool inverse, int64_t stream) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 4, "rope: bf16 [B, S, heads, D]");
+  const int64_t B = x.size(0), S = x.size(1), Hh = x.size(2), D = x.size(3);
+  TORCH_CHECK(x.stride(3) == 1 && x.stride(2) == D && D % 8 == 0, "rope: contiguous heads required");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 8 == 0 && x.stride(1) % 4 == 0, "rope: alignment");
+  TORCH_CHECK(cos.is_cuda() && cos.scalar_type() == torch::kFloat32 && cos.is_contiguous() &&
+                  cos.numel() >= S * D / 2 && sin.sizes() == cos.sizes() && sin.is_contiguous(),
+              "rope: cos/sin f32 [>=S, D/2]");
+  hip_ok(dta_rope(x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), (int)B, (int)S, (int)Hh, (int)D,
+                  x.stride(0), x.stride(1), inverse ? -1.f : 1.f, pick_stream(stream)),
+         "rope");
+}
+// fused CE: returns per-row loss (f32); writes grad * grad_scale into dlogits (may be `logits` itself)
+torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor dlogits, torch::Tensor target,
+                                    double grad_scale, int64_t ignore_index, int64_t stream) {
+  check_bf16_2d(logits, "logits");
+  check_bf16_2d(dlogits, "dlogits");
+  TORCH_CHECK(logits.dim() == 2 && dlogits.sizes() == logits.sizes(), "logits [N, V]");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous() &&
+                  target.numel() == logits.size(0),
+              "target int64 [N]");
+  auto loss = torch::empty({logits.size(0)}, logits.options().dtype(torch::kFloat32));
+  hip_ok(dta_cross_entropy(logits.data_ptr(), dlogits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                           logits.size(0), logits.size(1), (float)grad_scale, ignore_index, pick_stream(stream)),
+         "cross_entropy");
+  return loss;
+}
+
 // ----------------------------- RCCL -----------------------------
 ncclDataType_t nccl_dtype(const torch::Tensor& t) {
   switch (t.scalar_type()) {
@@ -383,6 +595,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wd"), py::arg("prev_grad_scale"), py::arg("nesterov"), py::arg("maximize"), py::arg("first_step"),
         py::arg("stream") = -1, py::arg("dbg_stamps") = py::none());
   m.def("mlp2_lds_bytes", &dta_mlp2_lds_bytes);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_", &rope_);
+  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("attn_bwd", &attn_bwd);
   m.def("rccl_load", &dta::rccl_load);
   m.def("rccl_loaded", &dta::rccl_loaded);
   m.def("rccl_unique_id", []() { return py::bytes(dta::rccl_unique_id()); });

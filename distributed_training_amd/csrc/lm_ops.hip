@@ -1,0 +1,465 @@
+// Memory-bound transformer ops for gfx950: LayerNorm / RMSNorm (fwd + bwd),
+// GELU(tanh), SwiGLU, rotary embedding, fused softmax-cross-entropy.
+//
+// All bf16 activations are moved with 16-byte vector accesses (8 x bf16 per
+// lane, cdna_hip_programming.md Guideline 13); statistics in fp32.  One wave
+// (64 lanes) per row for the row-wise ops: a row of C <= 8192 elements lives in
+// registers (C / 512 vectors per lane), so the backward needs no second read.
+#include "common.h"
+
+namespace dta {
+
+__device__ __forceinline__ void load8(const bf16* p, float* f) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void store8(bf16* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+// ---------------------------------------------------------------- norms
+// NV = vectors of 8 per lane (C = 512 * NV).  RMS: no mean, no bias.
+template <int NV, bool RMS>
+__global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                       const bf16* __restrict__ bias, bf16* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int64_t N, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const bf16* xr = x + row * C;
+  float v[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < C) load8(xr + c, v[i]);
+    else
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[i][j];
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(s) / C;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < C)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        ss += d * d;
+      }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / C + eps);
+  if (lane == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  bf16* yr = y + row * C;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 8;
+    if (c < C) {
+      float wv[8], bv[8], o[8];
+      load8(w + c, wv);
+      if (!RMS) load8(bias + c, bv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * wv[j] + (RMS ? 0.f : bv[j]);
+      store8(yr + c, o);
+    }
+  }
+}
+
+// dx per row; per-workgroup partial dgamma / dbeta sums into fp32 [nblk][C]
+template <int NV, bool RMS>
+__global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                       const bf16* __restrict__ w, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, bf16* __restrict__ dx,
+                                                       float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                       int64_t N, int C, int rows_per_block) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dwacc[NV][8], dbacc[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = dbacc[i][j] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  for (int64_t row = r0 + wave; row < min(r0 + rows_per_block, N); row += 4) {
+    const float mu = RMS ? 0.f : mean[row];
+    const float rs = rstd[row];
+    float xh[NV][8], g[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < C) {
+        float xv[8], dv[8], wv[8];
+        load8(x + row * C + c, xv);
+        load8(dy + row * C + c, dv);
+        load8(w + c, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (xv[j] - mu) * rs;
+          g[i][j] = dv[j] * wv[j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          dwacc[i][j] += dv[j] * xh[i][j];
+          dbacc[i][j] += dv[j];
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / C;
+    const float m2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < C) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - m1 - xh[i][j] * m2);
+        store8(dx + row * C + c, o);
+      }
+    }
+  }
+  // reduce the 4 waves' partials through LDS, one row of partials per block
+  __shared__ float red[4][512 * 8 / 8];  // staged 512 floats at a time
+  for (int i = 0; i < NV; ++i) {
+    for (int pass = 0; pass < (RMS ? 1 : 2); ++pass) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // lanes hold 8 consecutive columns: column c = (i*64 + lane)*8 + j
+        red[wave][lane * 8 + j] = pass == 0 ? dwacc[i][j] : dbacc[i][j];
+      }
+      __syncthreads();
+      for (int e = threadIdx.x; e < 512; e += 256) {
+        const int c = i * 512 + e;
+        if (c < C) {
+          const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+          (pass == 0 ? dw_part : db_part)[(int64_t)blockIdx.x * C + c] = v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nrows, int C,
+                                                     bf16* __restrict__ out_bf16, float* __restrict__ out_f32) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * C + c];
+  if (out_bf16) out_bf16[c] = f2bf(s);
+  if (out_f32) out_f32[c] = s;
+}
+
+// ---------------------------------------------------------------- elementwise
+__device__ __forceinline__ float gelu_t(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+__device__ __forceinline__ float gelu_t_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load8(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_t(v[j]);
+    store8(y + i * 8, v);
+  }
+}
+
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                       bf16* __restrict__ dx, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float v[8], g[8];
+    load8(x + i * 8, v);
+    load8(dy + i * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = g[j] * gelu_t_grad(v[j]);
+    store8(dx + i * 8, v);
+  }
+}
+
+// SwiGLU on a fused [N, 2F] projection: y = silu(a) * b, a = cols [0,F), b = cols [F,2F)
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16* __restrict__ ab, bf16* __restrict__ y, int64_t N,
+                                                         int F) {
+  const int64_t n8 = N * (F / 8);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / (F / 8);
+    const int c = (int)(i % (F / 8)) * 8;
+    float av[8], bv[8], o[8];
+    load8(ab + row * 2 * F + c, av);
+    load8(ab + row * 2 * F + F + c, bv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = av[j] / (1.f + __expf(-av[j])) * bv[j];
+    store8(y + row * F + c, o);
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ ab,
+                                                         bf16* __restrict__ dab, int64_t N, int F) {
+  const int64_t n8 = N * (F / 8);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / (F / 8);
+    const int c = (int)(i % (F / 8)) * 8;
+    float av[8], bv[8], g[8], da[8], db[8];
+    load8(ab + row * 2 * F + c, av);
+    load8(ab + row * 2 * F + F + c, bv);
+    load8(dy + row * F + c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.f / (1.f + __expf(-av[j]));
+      const float si = av[j] * sg;
+      db[j] = g[j] * si;
+      da[j] = g[j] * bv[j] * sg * (1.f + av[j] * (1.f - sg));
+    }
+    store8(dab + row * 2 * F + c, da);
+    store8(dab + row * 2 * F + F + c, db);
+  }
+}
+
+// Rotary embedding (rotate-half convention) in place on [B, S, heads, D] rows with
+// token stride `ss` and batch stride `sb`; cos/sin tables [S, D/2] fp32.
+// sign = +1 forward, -1 backward (rotation by -theta).
+__global__ void __launch_bounds__(256) rope_kernel(bf16* __restrict__ x, const float* __restrict__ cs,
+                                                   const float* __restrict__ sn, int B, int S, int heads, int D,
+                                                   int64_t sb, int64_t ss, float sign) {
+  const int half = D / 2;
+  const int64_t total = (int64_t)B * S * heads * (half / 4);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(i % (half / 4)) * 4;
+    int64_t r = i / (half / 4);
+    const int h = r % heads;
+    r /= heads;
+    const int s = r % S;
+    const int b = (int)(r / S);
+    bf16* p = x + (int64_t)b * sb + (int64_t)s * ss + (int64_t)h * D;
+    const bf16x4 x1 = *reinterpret_cast<const bf16x4*>(p + c4);
+    const bf16x4 x2 = *reinterpret_cast<const bf16x4*>(p + half + c4);
+    const float4 cv = *reinterpret_cast<const float4*>(cs + (int64_t)s * half + c4);
+    const float4 sv = *reinterpret_cast<const float4*>(sn + (int64_t)s * half + c4);
+    const float c[4] = {cv.x, cv.y, cv.z, cv.w}, sn4[4] = {sv.x * sign, sv.y * sign, sv.z * sign, sv.w * sign};
+    bf16x4 o1, o2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf2f(x1[j]), bb = bf2f(x2[j]);
+      o1[j] = f2bf(a * c[j] - bb * sn4[j]);
+      o2[j] = f2bf(bb * c[j] + a * sn4[j]);
+    }
+    *reinterpret_cast<bf16x4*>(p + c4) = o1;
+    *reinterpret_cast<bf16x4*>(p + half + c4) = o2;
+  }
+}
+
+// Fused softmax cross-entropy: one workgroup per row; writes loss[row] and
+// d(loss)/d(logits) * grad_scale into `dlogits` (may alias `logits`: in place).
+// Rows with target == ignore_index get zero loss / gradient.
+__global__ void __launch_bounds__(256) cross_entropy_kernel(const bf16* logits, bf16* dlogits,
+                                                            const int64_t* __restrict__ target,
+                                                            float* __restrict__ loss, int64_t V, float grad_scale,
+                                                            int64_t ignore_index) {
+  const int64_t row = blockIdx.x;
+  const bf16* x = logits + row * V;
+  bf16* dx = dlogits + row * V;
+  const int64_t t = target[row];
+  __shared__ float sm[4], ss[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool vec = (V % 8) == 0;
+  // pass 1: online max / sum-exp
+  float m = -INFINITY, s = 0.f;
+  if (vec) {
+    for (int64_t c = (int64_t)threadIdx.x * 8; c < V; c += 256 * 8) {
+      float v[8];
+      load8(x + c, v);
+      float mm = v[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) mm = fmaxf(mm, v[j]);
+      const float mn = fmaxf(m, mm);
+      s = s * __expf(m - mn);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(v[j] - mn);
+      m = mn;
+    }
+  } else {
+    for (int64_t c = threadIdx.x; c < V; c += 256) {
+      const float v = bf2f(x[c]);
+      const float mn = fmaxf(m, v);
+      s = s * __expf(m - mn) + __expf(v - mn);
+      m = mn;
+    }
+  }
+  // combine (m, s) across the wave, then across waves
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float mo = __shfl_xor(m, off, kWave), so = __shfl_xor(s, off, kWave);
+    const float mn = fmaxf(m, mo);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+    m = mn;
+  }
+  if (lane == 0) {
+    sm[wave] = m;
+    ss[wave] = s;
+  }
+  __syncthreads();
+  float M = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+  float Ssum = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) Ssum += sm[w] == -INFINITY ? 0.f : ss[w] * __expf(sm[w] - M);
+  const float lse = M + __logf(Ssum);
+  const bool ignore = t == ignore_index || t < 0 || t >= V;
+  const float xt = ignore ? 0.f : bf2f(x[ignore ? 0 : t]);
+  __syncthreads();  // everyone has read x[t] before it may be overwritten (in place)
+  if (threadIdx.x == 0) loss[row] = ignore ? 0.f : lse - xt;
+  const float gs = ignore ? 0.f : grad_scale;
+  // pass 2: gradient softmax - onehot
+  if (vec) {
+    for (int64_t c = (int64_t)threadIdx.x * 8; c < V; c += 256 * 8) {
+      float v[8];
+      load8(x + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__expf(v[j] - lse) - (c + j == t ? 1.f : 0.f)) * gs;
+      store8(dx + c, v);
+    }
+  } else {
+    for (int64_t c = threadIdx.x; c < V; c += 256) {
+      const float v = bf2f(x[c]);
+      dx[c] = f2bf((__expf(v - lse) - (c == t ? 1.f : 0.f)) * gs);
+    }
+  }
+}
+
+static inline int egrid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+}
+
+}  // namespace dta
+
+using namespace dta;
+
+template <bool RMS>
+static hipError_t norm_fwd_nv(int nv, const bf16* x, const bf16* w, const bf16* b, bf16* y, float* mean, float* rstd,
+                              int64_t N, int C, float eps, hipStream_t st) {
+  dim3 grid((unsigned)((N + 3) / 4)), blk(256);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL((norm_fwd_kernel<1, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    case 2: hipLaunchKernelGGL((norm_fwd_kernel<2, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    case 4: hipLaunchKernelGGL((norm_fwd_kernel<4, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    case 8: hipLaunchKernelGGL((norm_fwd_kernel<8, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    case 16: hipLaunchKernelGGL((norm_fwd_kernel<16, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static int nv_for(int C) {
+  const int v = (C + 511) / 512;
+  if (v <= 1) return 1;
+  if (v <= 2) return 2;
+  if (v <= 4) return 4;
+  if (v <= 8) return 8;
+  if (v <= 16) return 16;
+  return -1;
+}
+
+hipError_t dta_norm_fwd(bool rms, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                        int64_t N, int C, float eps, hipStream_t st) {
+  const int nv = nv_for(C);
+  if (nv < 0 || C % 8) return hipErrorInvalidValue;
+  auto X = reinterpret_cast<const bf16*>(x);
+  auto W = reinterpret_cast<const bf16*>(w);
+  auto Bv = reinterpret_cast<const bf16*>(b);
+  auto Y = reinterpret_cast<bf16*>(y);
+  return rms ? norm_fwd_nv<true>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, st)
+             : norm_fwd_nv<false>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, st);
+}
+
+template <bool RMS>
+static hipError_t norm_bwd_nv(int nv, const bf16* dy, const bf16* x, const bf16* w, const float* mean,
+                              const float* rstd, bf16* dx, float* dwp, float* dbp, int64_t N, int C, int rpb,
+                              hipStream_t st) {
+  dim3 grid((unsigned)((N + rpb - 1) / rpb)), blk(256);
+#define NB(V) hipLaunchKernelGGL((norm_bwd_kernel<V, RMS>), grid, blk, 0, st, dy, x, w, mean, rstd, dx, dwp, dbp, N, C, rpb)
+  switch (nv) {
+    case 1: NB(1); break;
+    case 2: NB(2); break;
+    case 4: NB(4); break;
+    case 8: NB(8); break;
+    case 16: NB(16); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef NB
+  return hipGetLastError();
+}
+
+// dw/db partial workspace: [nblk][C] fp32 each, nblk = ceil(N / rows_per_block)
+hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                        void* dx, float* dw_part, float* db_part, void* dw, void* db, int64_t N, int C,
+                        int rows_per_block, int grads_f32, hipStream_t st) {
+  const int nv = nv_for(C);
+  if (nv < 0 || C % 8) return hipErrorInvalidValue;
+  auto r = rms ? norm_bwd_nv<true>(nv, (const bf16*)dy, (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx,
+                                   dw_part, db_part, N, C, rows_per_block, st)
+               : norm_bwd_nv<false>(nv, (const bf16*)dy, (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx,
+                                    dw_part, db_part, N, C, rows_per_block, st);
+  if (r != hipSuccess) return r;
+  const int nblk = (int)((N + rows_per_block - 1) / rows_per_block);
+  dim3 g((C + 255) / 256);
+  hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, dw_part, nblk, C, grads_f32 ? nullptr : (bf16*)dw,
+                     grads_f32 ? (float*)dw : nullptr);
+  if (!rms)
+    hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, db_part, nblk, C, grads_f32 ? nullptr : (bf16*)db,
+                       grads_f32 ? (float*)db : nullptr);
+  return hipGetLastError();
+}
+
+hipError_t dta_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n / 8);
+  return hipGetLastError();
+}
+hipError_t dta_gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, hipStream_t st) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, (const bf16*)dy, (const bf16*)x,
+                     (bf16*)dx, n / 8);
+  return hipGetLastError();
+}
+hipError_t dta_swiglu_fwd(const void* ab, void* y, int64_t N, int F, hipStream_t st) {
+  if (F % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(egrid(N * F / 8)), dim3(256), 0, st, (const bf16*)ab, (bf16*)y, N, F);
+  return hipGetLastError();
+}
+hipError_t dta_swiglu_bwd(const void* dy, const void* ab, void* dab, int64_t N, int F, hipStream_t st) {
+  if (F % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(egrid(N * F / 8)), dim3(256), 0, st, (const bf16*)dy, (const bf16*)ab,
+                     (bf16*)dab, N, F);
+  return hipGetLastError();
+}
+hipError_t dta_rope(void* x, const float* cs, const float* sn, int B, int S, int heads, int D, int64_t sb, int64_t ss,
+                    float sign, hipStream_t st) {
+  if (D % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * S * heads * (D / 8);
+  hipLaunchKernelGGL(rope_kernel, dim3(egrid(total)), dim3(256), 0, st, (bf16*)x, cs, sn, B, S, heads, D, sb, ss,
+                     sign);
+  return hipGetLastError();
+}
+hipError_t dta_cross_entropy(const void* logits, void* dlogits, const int64_t* target, float* loss, int64_t N,
+                             int64_t V, float grad_scale, int64_t ignore_index, hipStream_t st) {
+  hipLaunchKernelGGL(cross_entropy_kernel, dim3((unsigned)N), dim3(256), 0, st, (const bf16*)logits, (bf16*)dlogits,
+                     target, loss, V, grad_scale, ignore_index);
+  return hipGetLastError();
+}

@@ -78,7 +78,10 @@ LOSSES: Dict[str, Callable] = {
 
 
 def lm_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
-    return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), targets.reshape(-1))
+    """Token cross-entropy; the fused gfx950 kernel on GPU (ops/lm.py)."""
+    from ..ops.lm import cross_entropy
+
+    return cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))
 
 
 class Trainer:
@@ -91,6 +94,10 @@ class Trainer:
         self.epochs_run = 0
         self.optimizer = optimizer
         self.train_data = train_data
+        from ..data.datasets import DeviceDataLoader
+
+        if isinstance(train_data, DeviceDataLoader):
+            train_data.to(env.torch_device if hasattr(env, "torch_device") else torch.device(env.device))
         self._loss_fn = LOSSES.get(config.loss, None) if config.loss != "lm" else lm_loss
         if self._loss_fn is None:
             raise ValueError(f"unknown loss {config.loss!r}")

@@ -1,0 +1,148 @@
+"""GPT-2 (124M "small" by default), random init, for the GPT-2 DDP / FSDP
+configurations of BASELINE.json.
+
+Architecture as GPT-2 / nanoGPT: learned token + position embeddings, pre-LN
+blocks (LayerNorm -> causal self-attention -> residual, LayerNorm -> GELU MLP ->
+residual), final LayerNorm, lm_head tied to the token embedding.  On GPU the
+non-GEMM work runs on the gfx950 kernels of ``ops/lm.py`` (flash attention,
+LayerNorm, GELU, fused cross-entropy); the projections are plain bf16 GEMMs.
+The vocabulary is padded to a multiple of 64 (50257 -> 50304) so the logits
+rows are 16-byte aligned.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+from ..ops import lm
+
+
+@dataclass
+class GPT2Config:
+    n_layer: int = 12
+    n_head: int = 12
+    n_embd: int = 768
+    vocab_size: int = 50257
+    block_size: int = 1024
+    dropout: float = 0.0
+    tie_weights: bool = True
+
+    @property
+    def padded_vocab(self) -> int:
+        return (self.vocab_size + 63) // 64 * 64
+
+    @staticmethod
+    def from_cfg(c) -> "GPT2Config":
+        g = c.get if hasattr(c, "get") else (lambda k, d=None: getattr(c, k, d))
+        return GPT2Config(int(g("n_layer", 12)), int(g("n_head", 12)), int(g("n_embd", 768)),
+                          int(g("vocab_size", 50257)), int(g("block_size", 1024)), float(g("dropout", 0.0) or 0.0),
+                          bool(g("tie_weights", True)))
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, n: int, eps: float = 1e-5):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n))
+        self.bias = nn.Parameter(torch.zeros(n))
+        self.eps = eps
+
+    def forward(self, x):
+        return lm.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.n_head = cfg.n_head
+        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+
+    def forward(self, x):
+        B, S, C = x.shape
+        H = self.n_head
+        qkv = self.c_attn(x).view(B, S, 3, H, C // H)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]  # strided views, read in place by the kernel
+        y = lm.attention(q, k, v, causal=True)
+        return self.c_proj(y.reshape(B, S, C))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+
+    def forward(self, x):
+        return self.c_proj(lm.gelu(self.c_fc(x)))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.ln_1 = LayerNorm(cfg.n_embd)
+        self.attn = CausalSelfAttention(cfg)
+        self.ln_2 = LayerNorm(cfg.n_embd)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class GPT2(nn.Module):
+    block_class = Block
+
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.cfg = cfg
+        self.vocab_size = cfg.vocab_size
+        V = cfg.padded_vocab
+        self.wte = nn.Embedding(V, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.block_size, cfg.n_embd)
+        self.h = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = LayerNorm(cfg.n_embd)
+        self.lm_head = nn.Linear(cfg.n_embd, V, bias=False)
+        if cfg.tie_weights:
+            self.lm_head.weight = self.wte.weight
+        self.activation_checkpointing = False
+        self.apply(self._init)
+        for n, p in self.named_parameters():
+            if n.endswith("c_proj.weight"):
+                nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * cfg.n_layer))
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, 0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, 0.02)
+
+    def enable_activation_checkpointing(self, on: bool = True):
+        self.activation_checkpointing = on
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def forward(self, idx):
+        B, S = idx.shape
+        pos = torch.arange(S, device=idx.device)
+        x = self.wte(idx) + self.wpe(pos)
+        for blk in self.h:
+            if self.activation_checkpointing and torch.is_grad_enabled():
+                x = checkpoint(blk, x, use_reentrant=False)
+            else:
+                x = blk(x)
+        return self.lm_head(self.ln_f(x))
+
+    def flops_per_token(self, seq_len: int) -> float:
+        """Training FLOPs per token (6N + attention), PaLM-style accounting."""
+        n = self.num_params() - self.wpe.weight.numel()
+        c = self.cfg
+        return 6 * n + 12 * c.n_layer * c.n_embd * seq_len

@@ -1,0 +1,137 @@
+"""Llama-3 (8B by default), random init, for the Llama-3 8B FSDP configuration
+of BASELINE.json.
+
+RMSNorm pre-norm blocks, grouped-query attention (32 query / 8 key-value heads)
+with rotary embeddings (theta 500000), SwiGLU FFN (14336), untied output head,
+vocab 128256.  The QKV and gate/up projections are fused (one GEMM each); on
+GPU the non-GEMM work runs on the gfx950 kernels of ``ops/lm.py``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+from torch.utils.checkpoint import checkpoint
+
+from ..ops import lm
+
+
+@dataclass
+class LlamaConfig:
+    n_layer: int = 32
+    n_head: int = 32
+    n_kv_head: int = 8
+    n_embd: int = 4096
+    ffn_hidden: int = 14336
+    vocab_size: int = 128256
+    block_size: int = 8192
+    rope_theta: float = 500000.0
+    norm_eps: float = 1e-5
+    tie_weights: bool = False
+
+    @staticmethod
+    def from_cfg(c) -> "LlamaConfig":
+        g = c.get if hasattr(c, "get") else (lambda k, d=None: getattr(c, k, d))
+        return LlamaConfig(int(g("n_layer", 32)), int(g("n_head", 32)), int(g("n_kv_head", 8)),
+                           int(g("n_embd", 4096)), int(g("ffn_hidden", 14336)), int(g("vocab_size", 128256)),
+                           int(g("block_size", 8192)), float(g("rope_theta", 500000.0)),
+                           float(g("norm_eps", 1e-5)), bool(g("tie_weights", False)))
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, n: int, eps: float):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n))
+        self.eps = eps
+
+    def forward(self, x):
+        return lm.rms_norm(x, self.weight, self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.H, self.Hkv = cfg.n_head, cfg.n_kv_head
+        self.D = cfg.n_embd // cfg.n_head
+        self.wqkv = nn.Linear(cfg.n_embd, (self.H + 2 * self.Hkv) * self.D, bias=False)
+        self.wo = nn.Linear(self.H * self.D, cfg.n_embd, bias=False)
+
+    def forward(self, x, cos, sin):
+        B, S, _ = x.shape
+        H, Hkv, D = self.H, self.Hkv, self.D
+        qkv = self.wqkv(x).view(B, S, H + 2 * Hkv, D)
+        q = lm.apply_rope(qkv[:, :, :H], cos, sin)
+        k = lm.apply_rope(qkv[:, :, H:H + Hkv], cos, sin)
+        v = qkv[:, :, H + Hkv:]
+        y = lm.attention(q, k, v, causal=True)
+        return self.wo(y.reshape(B, S, H * D))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w13 = nn.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
+        self.w2 = nn.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
+
+    def forward(self, x):
+        return self.w2(lm.swiglu(self.w13(x)))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attention_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
+        self.attention = Attention(cfg)
+        self.ffn_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
+        self.feed_forward = FeedForward(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attention(self.attention_norm(x), cos, sin)
+        return x + self.feed_forward(self.ffn_norm(x))
+
+
+class Llama(nn.Module):
+    block_class = Block
+
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.vocab_size = cfg.vocab_size
+        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
+        self.output = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+        if cfg.tie_weights:
+            self.output.weight = self.tok_embeddings.weight
+        cos, sin = lm.rope_tables(cfg.block_size, cfg.n_embd // cfg.n_head, cfg.rope_theta)
+        self.register_buffer("rope_cos", cos, persistent=False)
+        self.register_buffer("rope_sin", sin, persistent=False)
+        self.activation_checkpointing = False
+        std = 0.02
+        for n, p in self.named_parameters():
+            if p.dim() >= 2:
+                s = std / math.sqrt(2 * cfg.n_layer) if n.endswith(("wo.weight", "w2.weight")) else std
+                nn.init.normal_(p, 0.0, s)
+
+    def enable_activation_checkpointing(self, on: bool = True):
+        self.activation_checkpointing = on
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def forward(self, idx):
+        x = self.tok_embeddings(idx)
+        cos, sin = self.rope_cos, self.rope_sin
+        for blk in self.layers:
+            if self.activation_checkpointing and torch.is_grad_enabled():
+                x = checkpoint(blk, x, cos, sin, use_reentrant=False)
+            else:
+                x = blk(x, cos, sin)
+        return self.output(self.norm(x))
+
+    def flops_per_token(self, seq_len: int) -> float:
+        c = self.cfg
+        n = self.num_params() - self.tok_embeddings.weight.numel()
+        return 6 * n + 12 * c.n_layer * c.n_embd * seq_len

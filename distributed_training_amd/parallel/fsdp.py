@@ -86,6 +86,7 @@ class _Unit:
         self.shard_param: Optional[nn.Parameter] = None
         self.full.register_post_accumulate_grad_hook(self._post_backward)
         self._bwd_ready = False
+        self.in_backward = False  # between this unit's pre-backward and post-backward
         self.free()  # storage exists only while the unit is gathered
 
     # ---------------------------------------------------------- storage
@@ -138,6 +139,7 @@ class _Unit:
             g.div_(own.world_size)
         work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
         own._pending_rs.append((self, work, out, g))
+        self.in_backward = False
         if not self.is_root or own.reshard_root_after_backward:
             self.free()
 
@@ -245,6 +247,10 @@ class FullyShardedDataParallel(nn.Module):
 
     def _make_pre_forward(self, u: _Unit):
         def pre(mod, args):
+            if u.in_backward:  # checkpoint recomputation: already gathered
+                u.unshard(async_op=False)
+                u.set_views()
+                return None
             if self._record_order:
                 self._fwd_order.append(u)
             u.unshard(async_op=False)
@@ -259,9 +265,11 @@ class FullyShardedDataParallel(nn.Module):
 
     def _make_post_forward(self, u: _Unit):
         def post(mod, args, output):
-            if self.reshard_after_forward and torch.is_grad_enabled():
-                u.free()
-            elif self.reshard_after_forward and not torch.is_grad_enabled():
+            if u.in_backward:
+                # activation-checkpoint recomputation inside this unit's backward:
+                # the recomputed graph still needs the gathered parameters
+                return output
+            if self.reshard_after_forward:
                 u.free()
             self._register_pre_backward(u, output)
             return output
@@ -276,6 +284,7 @@ class FullyShardedDataParallel(nn.Module):
         def hook(grad):
             if not u._bwd_ready:
                 u._bwd_ready = True
+                u.in_backward = True
                 u.unshard(async_op=False)
                 if self.prefetch:
                     prv = self._next_in_order(u, -1)
@@ -319,6 +328,7 @@ class FullyShardedDataParallel(nn.Module):
         self._pending_rs = []
         self._cb_queued = False
         for u in self.units:  # any unit not used in backward: drop its gathered copy
+            u.in_backward = False
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):
                 u.free()
 

@@ -1,0 +1,168 @@
+"""gfx950 transformer kernels (flash attention, norms, activations, RoPE,
+fused cross-entropy) vs fp32 PyTorch references, forward and backward."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_training_amd.ops import lm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal", [(2, 256, 4, 4, 64, True), (1, 200, 4, 2, 128, True),
+                                                 (2, 128, 2, 2, 64, False), (1, 333, 8, 1, 64, True),
+                                                 (1, 1024, 2, 2, 128, True)])
+def test_flash_attention_fwd_bwd(B, S, H, Hkv, D, causal):
+    torch.manual_seed(0)
+    q = torch.randn(B, S, H, D, device=DEV).bfloat16().requires_grad_()
+    k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
+    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
+    do = torch.randn(B, S, H, D, device=DEV).bfloat16()
+    o = lm.attention(q, k, v, causal=causal)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = lm.attention_reference(qr, kr, vr, causal=causal)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    assert _rel(q.grad, qr.grad) < 2e-2
+    assert _rel(k.grad, kr.grad) < 2e-2
+    assert _rel(v.grad, vr.grad) < 2e-2
+
+
+def test_attention_strided_qkv_views():
+    """q/k/v as strided views of one fused QKV projection (no copies)."""
+    torch.manual_seed(1)
+    B, S, H, D = 2, 64, 3, 64
+    qkv = torch.randn(B, S, 3, H, D, device=DEV).bfloat16()
+    o = lm.attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
+    ref = lm.attention_reference(qkv[:, :, 0].float(), qkv[:, :, 1].float(), qkv[:, :, 2].float(), causal=True)
+    assert _rel(o, ref) < 1e-2
+
+
+@pytest.mark.parametrize("C", [768, 4096, 200 * 8])
+@pytest.mark.parametrize("rms", [False, True])
+def test_norms(C, rms):
+    torch.manual_seed(2)
+    x = (torch.randn(37, C, device=DEV) * 3 + 1).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    dy = torch.randn(37, C, device=DEV).bfloat16()
+    y = lm.rms_norm(x, w) if rms else lm.layer_norm(x, w, b)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    if rms:
+        yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    if not rms:
+        assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_gelu_swiglu_rope():
+    torch.manual_seed(3)
+    x = torch.randn(64, 256, device=DEV).bfloat16().requires_grad_()
+    y = lm.gelu(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    F.gelu(xr, approximate="tanh").backward(dy.float())
+    assert _rel(y, F.gelu(x.detach().float(), approximate="tanh")) < 1e-2 and _rel(x.grad, xr.grad) < 1e-2
+
+    ab = torch.randn(32, 2 * 192, device=DEV).bfloat16().requires_grad_()
+    y = lm.swiglu(ab)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    abr = ab.detach().float().requires_grad_()
+    a, b = abr.chunk(2, -1)
+    (F.silu(a) * b).backward(dy.float())
+    assert _rel(ab.grad, abr.grad) < 1e-2
+
+    B, S, Hh, D = 2, 50, 3, 128
+    cos, sin = lm.rope_tables(64, D, 500000.0, DEV)
+    xq = torch.randn(B, S, Hh, D, device=DEV).bfloat16().requires_grad_()
+    yq = lm.apply_rope(xq, cos, sin)
+    dy = torch.randn_like(yq)
+    yq.backward(dy)
+    xr = xq.detach().float().requires_grad_()
+    lm.rope_reference(xr, cos, sin).backward(dy.float())
+    assert _rel(yq, lm.rope_reference(xq.detach().float(), cos, sin)) < 1e-2
+    assert _rel(xq.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [50304, 1001, 128256])
+def test_fused_cross_entropy(V):
+    torch.manual_seed(4)
+    N = 96
+    logits = (torch.randn(N, V, device=DEV) * 2).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[5] = -100
+    loss = lm.cross_entropy(logits, t)
+    loss.backward()
+    lr = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(lr, t, ignore_index=-100)
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref, rtol=2e-3, atol=2e-3)
+    assert _rel(logits.grad, lr.grad) < 2e-2
+    assert logits.grad[5].abs().sum().item() == 0.0
+
+
+def test_gpt2_tiny_trains_on_gpu():
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    dev = torch.device(DEV, 0)
+    m = GPT2(GPT2Config(n_layer=2, n_head=2, n_embd=128, vocab_size=1000, block_size=128)).to(dev)
+    ddp = DistributedDataParallel(m, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    opt = FusedAdamW(ddp.parameters(), lr=3e-3, weight_decay=0.0)
+    x = torch.randint(0, 1000, (4, 128), device=dev)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        logits = ddp(x[:, :-1])
+        loss = lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), x[:, 1:].reshape(-1))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0] * 0.5, losses
+
+
+def test_llama_tiny_fsdp_trains_on_gpu():
+    from distributed_training_amd.models.llama import Block, Llama, LlamaConfig
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    dev = torch.device(DEV, 0)
+    cfg = LlamaConfig(n_layer=2, n_head=4, n_kv_head=2, n_embd=256, ffn_hidden=512, vocab_size=1024, block_size=256)
+    m = Llama(cfg).to(dev)
+    m.enable_activation_checkpointing()
+    fs = FullyShardedDataParallel(m, comm=RcclComm(0, 1, dev), device=dev, wrap_policy={Block},
+                                  param_dtype=torch.bfloat16)
+    opt = FusedAdamW(fs.parameters(), lr=3e-3, weight_decay=0.0)
+    x = torch.randint(0, 1024, (2, 129), device=dev)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        logits = fs(x[:, :-1])
+        loss = lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), x[:, 1:].reshape(-1))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0] * 0.5, losses
+    sd = fs.full_state_dict(rank0_only=False)
+    assert "layers.0.attention.wqkv.weight" in sd and sd["output.weight"].dtype == torch.float32

@@ -172,3 +172,41 @@ def _comm_ops(rank, ws):
 
 def test_torch_comm_collectives():
     run_gloo(_comm_ops, 3)
+
+
+class CkptNet(Net):
+    def forward(self, x):
+        from torch.utils.checkpoint import checkpoint
+
+        x = self.inp(x)
+        for b in self.blocks:
+            x = checkpoint(b, x, use_reentrant=False)
+        return self.out(x) * self.scale
+
+
+def _fsdp_ckpt(rank, ws):
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    ref = CkptNet()
+    m = copy.deepcopy(ref)
+    fs = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={Block})
+    o1 = torch.optim.SGD(ref.parameters(), lr=0.1)
+    o2 = FusedSGD(fs.parameters(), lr=0.1)
+    for it in range(3):
+        g = torch.Generator().manual_seed(7 + it)
+        X, Y = torch.randn(8 * ws, 20, generator=g), torch.randn(8 * ws, 1, generator=g)
+        o1.zero_grad()
+        F.mse_loss(ref(X), Y).backward()
+        o1.step()
+        o2.zero_grad()
+        F.mse_loss(fs(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+        o2.step()
+    for k, v in fs.full_state_dict(rank0_only=False).items():
+        torch.testing.assert_close(v, ref.state_dict()[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def test_native_fsdp_with_activation_checkpointing():
+    run_gloo(_fsdp_ckpt, 2)
