@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Transformer benchmarks for the GPT-2 small (DDP / FSDP) and Llama-3 8B
+(FSDP) configurations of BASELINE.json: tokens/s (whole job), samples/s,
+model-FLOPs utilisation against the 2.5 PF/s dense bf16 MFMA peak.
+
+    python bench_lm.py --model gpt2 --strategy ddp --batch 8 --seq 1024
+    python bench_lm.py --model gpt2 --strategy fsdp
+    python bench_lm.py --model llama3_8b --strategy fsdp --batch 1 --seq 8192 --ckpt
+    python bench_lm.py --model gpt2 --impl torch   # stock PyTorch-ROCm baseline (SDPA, torch DDP, AdamW)
+    torchrun --nproc-per-node N bench_lm.py --gpus N ...
+
+Synthetic tokens, random-init weights; every timed step is a full
+forward + backward + gradient communication + AdamW update.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_BF16 = 2.5e15  # dense bf16 MFMA peak per MI355X
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="gpt2", choices=["gpt2", "llama3_8b", "llama_1b", "llama_tiny"])
+    ap.add_argument("--strategy", default="ddp", choices=["ddp", "fsdp"])
+    ap.add_argument("--impl", default="native", choices=["native", "torch"])
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU micro-batch (sequences)")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--layers", type=int, default=0, help="override n_layer (0 = config)")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+def model_cfg(name, layers):
+    from distributed_training_amd.models.gpt2 import GPT2Config
+    from distributed_training_amd.models.llama import LlamaConfig
+
+    if name == "gpt2":
+        c = GPT2Config()
+    elif name == "llama3_8b":
+        c = LlamaConfig()
+    elif name == "llama_1b":
+        c = LlamaConfig(n_layer=16, n_head=32, n_kv_head=8, n_embd=2048, ffn_hidden=8192, block_size=8192)
+    else:
+        c = LlamaConfig(n_layer=4, n_head=8, n_kv_head=2, n_embd=512, ffn_hidden=1536, vocab_size=32000,
+                        block_size=4096)
+    if layers:
+        c.n_layer = layers
+    return c
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    torch.manual_seed(0)
+    cfg = model_cfg(args.model, args.layers)
+    is_gpt = args.model == "gpt2"
+    if is_gpt:
+        from distributed_training_amd.models.gpt2 import GPT2 as M
+    else:
+        from distributed_training_amd.models.llama import Llama as M
+    with torch.device("meta"):
+        n_params = sum(p.numel() for p in M(cfg).parameters())
+    with torch.device(dev):  # initialise straight on the GPU (8B params: no host round trip)
+        model = M(cfg)
+    if args.ckpt:
+        model.enable_activation_checkpointing()
+    V = cfg.vocab_size
+    gen = torch.Generator(device=dev).manual_seed(1 + rank)
+    data = torch.randint(0, V, (max(4, 64 // max(1, args.batch)) * args.batch, args.seq + 1), device=dev,
+                         generator=gen)
+
+    if args.impl == "native":
+        from distributed_training_amd.ops import lm
+        from distributed_training_amd.ops.optim import FusedAdamW
+        from distributed_training_amd.parallel.comm import make_comm
+
+        comm = make_comm(dev)
+        model = model.to(dev)
+        if args.strategy == "ddp":
+            from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+            wrapped = DistributedDataParallel(model, comm=comm, device=dev, param_dtype=torch.bfloat16,
+                                              bucket_cap_mb=args.bucket_mb, first_bucket_mb=2.0)
+        else:
+            from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+            wrapped = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy={M.block_class},
+                                               param_dtype=torch.bfloat16)
+        opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
+
+        def loss_fn(logits, y):
+            return lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
+    else:
+        import torch.nn.functional as F
+
+        model = model.to(dev)
+        # stock path: swap the framework ops for torch's (SDPA, F.layer_norm, ...)
+        _patch_torch_ops()
+        if args.strategy == "ddp":
+            wrapped = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local]) if ws > 1 else model
+        else:
+            from torch.distributed.fsdp import FullyShardedDataParallel as TFSDP
+            from torch.distributed.fsdp import MixedPrecision
+            from torch.distributed.fsdp.wrap import ModuleWrapPolicy
+
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29577")
+                dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+            wrapped = TFSDP(model, auto_wrap_policy=ModuleWrapPolicy({M.block_class}), device_id=dev,
+                            mixed_precision=MixedPrecision(param_dtype=torch.bfloat16, reduce_dtype=torch.bfloat16))
+        opt = torch.optim.AdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
+
+        def loss_fn(logits, y):
+            return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), y.reshape(-1))
+
+    nb = data.shape[0] // args.batch
+    state = {"i": 0, "loss": None}
+
+    def step():
+        i = state["i"] % nb
+        state["i"] += 1
+        xb = data[i * args.batch:(i + 1) * args.batch]
+        opt.zero_grad(set_to_none=True)
+        if args.impl == "torch" and args.strategy == "ddp":
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = wrapped(xb[:, :-1])
+        else:
+            logits = wrapped(xb[:, :-1])
+        loss = loss_fn(logits, xb[:, 1:])
+        loss.backward()
+        opt.step()
+        state["loss"] = loss
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if ws > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    tokens = args.batch * args.seq * ws * args.steps
+    flops_tok = 6 * (n_params - (cfg.block_size * cfg.n_embd if is_gpt else 0)) + 12 * cfg.n_layer * cfg.n_embd * args.seq
+    tps = tokens / el
+    mfu = tps * flops_tok / (PEAK_BF16 * ws)
+    out = {"metric": f"tokens/s ({args.model} {args.strategy} bf16)", "value": round(tps, 1), "unit": "tokens/s",
+           "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "dtype": "bf16", "data": "synthetic tokens",
+           "samples_per_s": round(args.batch * ws * args.steps / el, 2), "mfu": round(mfu, 4),
+           "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+           "final_loss": float(state["loss"].item()),
+           "config": {"model": args.model, "layers": cfg.n_layer, "global_batch": args.batch * ws,
+                      "seq_len": args.seq, "parallelism": f"{args.strategy}{ws}", "impl": args.impl,
+                      "activation_checkpointing": args.ckpt}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+        if args.json_out:
+            Path(args.json_out).write_text(json.dumps(out) + "\n")
+    if dist.is_initialized():
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+def _patch_torch_ops():
+    """Route the models' op calls to stock PyTorch (for the baseline)."""
+    import torch
+    import torch.nn.functional as F
+
+    from distributed_training_amd.ops import lm
+
+    def attention(q, k, v, causal=True, scale=None):
+        H, Hkv = q.shape[2], k.shape[2]
+        qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+        return F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale,
+                                              enable_gqa=H != Hkv).transpose(1, 2)
+
+    lm.attention = attention
+    lm.layer_norm = lambda x, w, b, eps=1e-5: F.layer_norm(x, (x.shape[-1],), w, b, eps)
+    lm.rms_norm = lambda x, w, eps=1e-5: F.rms_norm(x, (x.shape[-1],), w, eps)
+    lm.gelu = lambda x: F.gelu(x, approximate="tanh")
+    lm.swiglu = lambda ab: F.silu(ab.chunk(2, -1)[0]) * ab.chunk(2, -1)[1]
+    lm.apply_rope = lm.rope_reference
+
+
+if __name__ == "__main__":
+    main()

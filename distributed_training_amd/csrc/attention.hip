@@ -220,6 +220,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 Ktw[4 * D * TS];   // per wave: K^T [d][32 keys]
   __shared__ __attribute__((aligned(16))) bf16 dSw[4 * BM * TS];  // per wave: dS [q][32 keys]
   __shared__ float lse2[BM], dlt[BM];
+  __shared__ __attribute__((aligned(16))) float dQs[BM * D];  // workgroup-level dQ partial (LDS atomics)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -287,6 +288,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
         lse2[tid] = qr < a.S ? lse_h[qr] * kLog2e : 0.f;
         dlt[tid] = qr < a.S ? dl_h[qr] : 0.f;
       }
+      for (int e = tid; e < BM * D; e += 256) dQs[e] = 0.f;
       __syncthreads();
       // S = Q.K^T and dP = dO.V^T: rows = queries, cols = this wave's keys
       f32x16 s = zero16, dp = zero16;
@@ -347,10 +349,13 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
           dq = mfma32x32x16(sa, kb, dq);  // rows q, cols d
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qr = q0 + mfma32_row(i, lane);
-          if (qr < a.S) atomicAdd(dqb + (int64_t)qr * a.H * D + dt * 32 + r32, dq[i] * a.scale);
-        }
+        for (int i = 0; i < 16; ++i) atomicAdd(&dQs[mfma32_row(i, lane) * D + dt * 32 + r32], dq[i]);
+      }
+      // one global fp32 atomic per element per workgroup (4 waves reduced in LDS first)
+      __syncthreads();
+      for (int e = tid; e < BM * D; e += 256) {
+        const int qr = q0 + e / D;
+        if (qr < a.S) atomicAdd(dqb + (int64_t)qr * a.H * D + (e % D), dQs[e] * a.scale);
       }
     }
   }

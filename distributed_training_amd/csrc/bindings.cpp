@@ -50,7 +50,7 @@ hipError_t dta_attn_bwd(const dta::AttnArgs*, int, bool, hipStream_t);
 // ---- launchers implemented in the .hip translation units ----
 hipError_t dta_flat_sgd(const float*, float*, const float*, float*, void*, int64_t, float, float, float, float, float,
                         int, int, int, hipStream_t);
-hipError_t dta_flat_adam(float*, const float*, float*, float*, float*, void*, int64_t, float*, float, float, float,
+hipError_t dta_flat_adam(float*, const void*, int, float*, float*, float*, void*, int64_t, float*, float, float, float,
                          float, float, float, int, int, int, int, hipStream_t);
 hipError_t dta_step_inc(float*, hipStream_t);
 hipError_t dta_mt_scale_copy(const void* const*, void* const*, const int64_t*, int, int, int, float, hipStream_t);
@@ -115,7 +115,10 @@ void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
                double eps, double wd, double grad_scale, bool adamw, bool maximize, bool amsgrad, bool bump_step,
                int64_t stream) {
   check_f32(p, "param", false);
-  check_f32(g, "grad", false);
+  check_gpu(g, "grad");
+  TORCH_CHECK(g.is_contiguous() && (g.scalar_type() == torch::kFloat32 || g.scalar_type() == torch::kBFloat16),
+              "flat_adam: grad must be contiguous fp32 or bf16");
+  const int g_bf16 = g.scalar_type() == torch::kBFloat16;
   check_f32(m, "exp_avg", false);
   check_f32(v, "exp_avg_sq", false);
   check_f32(step, "step", false);
@@ -133,7 +136,7 @@ void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
     TORCH_CHECK(p_bf16->scalar_type() == torch::kBFloat16 && p_bf16->numel() == n, "p_bf16: bf16 of same size");
     pb = p_bf16->data_ptr();
   }
-  hip_ok(dta_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), fptr(vmax),
+  hip_ok(dta_flat_adam(p.data_ptr<float>(), g.data_ptr(), g_bf16, m.data_ptr<float>(), v.data_ptr<float>(), fptr(vmax),
                        pb, n, step.data_ptr<float>(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
                        (float)grad_scale, adamw, maximize, amsgrad, bump_step, pick_stream(stream)),
          "flat_adam");
@@ -409,7 +412,8 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   const int64_t C = x.size(-1), N = x.numel() / C;
   TORCH_CHECK(dy.numel() == x.numel() && w.numel() == C, "norm_bwd: shape mismatch");
   TORCH_CHECK(rstd.numel() == N && (rms || mean.numel() == N), "norm_bwd: stats shape");
-  const int rpb = 64;
+  // ~512 workgroups (fills 256 CUs twice), a multiple of 4 rows each (one per wave)
+  const int rpb = (int)std::min<int64_t>(1024, std::max<int64_t>(4, ((N + 511) / 512 + 3) / 4 * 4));
   const int64_t nblk = (N + rpb - 1) / rpb;
   auto f32 = x.options().dtype(torch::kFloat32);
   auto dwp = torch::empty({nblk, C}, f32);

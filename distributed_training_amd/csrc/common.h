@@ -22,6 +22,28 @@ __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 // Plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) at -O3.
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// 8-element vector load/store with fp32 conversion (16-byte bf16 / 32-byte fp32)
+__device__ __forceinline__ void load8(const bf16* p, float* f) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void store8(bf16* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+__device__ __forceinline__ void load8(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void store8(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);

@@ -9,18 +9,6 @@
 
 namespace dta {
 
-__device__ __forceinline__ void load8(const bf16* p, float* f) {
-  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = bf2f(v[j]);
-}
-__device__ __forceinline__ void store8(bf16* p, const float* f) {
-  bf16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = f2bf(f[j]);
-  *reinterpret_cast<bf16x8*>(p) = v;
-}
-
 // ---------------------------------------------------------------- norms
 // NV = vectors of 8 per lane (C = 512 * NV).  RMS: no mean, no bias.
 template <int NV, bool RMS>
@@ -150,14 +138,34 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// Column sums of the [nrows, C] partials: 32 columns x 8 row groups per
+// workgroup, 8 independent loads in flight per thread, LDS reduce.
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nrows, int C,
                                                      bf16* __restrict__ out_bf16, float* __restrict__ out_f32) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[(int64_t)r * C + c];
-  if (out_bf16) out_bf16[c] = f2bf(s);
-  if (out_f32) out_f32[c] = s;
+  if (c < C) {
+    int r = rg;
+    for (; r + 56 < nrows; r += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(r + 8 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < nrows; r += 8) s += part[(int64_t)r * C + c];
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][cl];
+    if (out_bf16) out_bf16[c] = f2bf(t);
+    if (out_f32) out_f32[c] = t;
+  }
 }
 
 // ---------------------------------------------------------------- elementwise
@@ -418,7 +426,7 @@ hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, 
                                     dw_part, db_part, N, C, rows_per_block, st);
   if (r != hipSuccess) return r;
   const int nblk = (int)((N + rows_per_block - 1) / rows_per_block);
-  dim3 g((C + 255) / 256);
+  dim3 g((C + 31) / 32);
   hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, dw_part, nblk, C, grads_f32 ? nullptr : (bf16*)dw,
                      grads_f32 ? (float*)dw : nullptr);
   if (!rms)

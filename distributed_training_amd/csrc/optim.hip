@@ -91,7 +91,18 @@ __device__ __forceinline__ float adam_one(float p, float g, float* m, float* v, 
 
 // `step` is a device counter (float) so the update is hipGraph-replayable:
 // the launcher bumps it with a one-thread kernel before this kernel runs.
-__global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+// Gradients are fp32 or bf16 (the bf16 gradient buffer of a mixed-precision
+// flat group is read directly: no fp32 copy of the gradients per step).
+__device__ __forceinline__ float4 load_g4(const float* g, int64_t i) { return reinterpret_cast<const float4*>(g)[i]; }
+__device__ __forceinline__ float4 load_g4(const bf16* g, int64_t i) {
+  const bf16x4 b = reinterpret_cast<const bf16x4*>(g)[i];
+  return make_float4(bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3]));
+}
+__device__ __forceinline__ float load_g1(const float* g, int64_t i) { return g[i]; }
+__device__ __forceinline__ float load_g1(const bf16* g, int64_t i) { return bf2f(g[i]); }
+
+template <typename GT>
+__global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         float* __restrict__ vmax, bf16* __restrict__ p_bf16,
                                                         int64_t n, const float* __restrict__ step,
@@ -103,7 +114,7 @@ __global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, c
   const int64_t n4 = h.vec ? (n >> 2) : 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 gg = load_g4(g, i);
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
     float4 xx = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -124,7 +135,7 @@ __global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, c
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float xm = vmax ? vmax[i] : 0.f;
     float mi = m[i], vi = v[i];
-    float pi = adam_one(p[i], g[i], &mi, &vi, &xm, bc1, bc2_sqrt, h);
+    float pi = adam_one(p[i], load_g1(g, i), &mi, &vi, &xm, bc1, bc2_sqrt, h);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -159,7 +170,20 @@ __global__ void __launch_bounds__(256) mt_scale_copy_kernel(MTArgs a, float scal
   const TS* s = reinterpret_cast<const TS*>(a.src[t]);
   TD* d = reinterpret_cast<TD*>(a.dst[t]);
   const int64_t end = min(c0 + (int64_t)kMTChunk, a.n[t]);
-  for (int64_t i = c0 + threadIdx.x; i < end; i += blockDim.x) d[i] = (TD)((float)s[i] * scale);
+  int64_t i0 = c0;
+  if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+    // 8 elements per thread per iteration (16-byte bf16 / 2x16-byte fp32 accesses)
+    const int64_t vend = c0 + (end - c0) / 8 * 8;
+    for (int64_t i = c0 + threadIdx.x * 8; i < vend; i += blockDim.x * 8) {
+      float v[8];
+      load8(s + i, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= scale;
+      store8(d + i, v);
+    }
+    i0 = vend;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < end; i += blockDim.x) d[i] = (TD)((float)s[i] * scale);
 }
 
 // Sum of squares of a flat buffer -> atomically added into out[0] (fp32).
@@ -232,16 +256,20 @@ hipError_t dta_flat_sgd(const float* p_in, float* p_out, const float* g, float* 
   return hipGetLastError();
 }
 
-hipError_t dta_flat_adam(float* p, const float* g, float* m, float* v, float* vmax, void* p_bf16, int64_t n,
-                         float* step, float lr, float beta1, float beta2, float eps, float wd, float grad_scale,
-                         int adamw, int maximize, int amsgrad, int bump_step, hipStream_t st) {
+hipError_t dta_flat_adam(float* p, const void* g, int g_bf16, float* m, float* v, float* vmax, void* p_bf16,
+                         int64_t n, float* step, float lr, float beta1, float beta2, float eps, float wd,
+                         float grad_scale, int adamw, int maximize, int amsgrad, int bump_step, hipStream_t st) {
   if (bump_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   if (n <= 0) return hipGetLastError();
   auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) % a) == 0; };
-  const int vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
+  const int vec = al(p, 16) && al(g, g_bf16 ? 8 : 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
   AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad, vec};
-  hipLaunchKernelGGL(flat_adam_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p, g, m, v, vmax,
-                     reinterpret_cast<bf16*>(p_bf16), n, step, h);
+  if (g_bf16)
+    hipLaunchKernelGGL(flat_adam_kernel<bf16>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p,
+                       reinterpret_cast<const bf16*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
+  else
+    hipLaunchKernelGGL(flat_adam_kernel<float>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p,
+                       reinterpret_cast<const float*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
   return hipGetLastError();
 }
 

@@ -85,6 +85,8 @@ class FusedSGD(torch.optim.Optimizer):
             flats, singles = _split_params(group["params"])
             for fg, ps in flats:
                 if len(ps) == len(fg.params):
+                    if not fg.prepare_grads_for_step():
+                        continue
                     st = self._flat_state.setdefault(id(fg), {"first": True})
                     if mom and "mom" not in st:
                         st["mom"] = torch.zeros_like(fg.master)
@@ -95,6 +97,7 @@ class FusedSGD(torch.optim.Optimizer):
                                       1.0, nest, maxi, st["first"], -1)
                     st["first"] = False
                 else:
+                    fg.prepare_grads_for_step()
                     for p in ps:
                         self._single_gpu(fg, p, lr, mom, damp, wd, nest, maxi)
             for p in singles:
@@ -134,12 +137,13 @@ class FusedSGD(torch.optim.Optimizer):
             flats, singles = _split_params(group["params"])
             for fg, _ in flats:
                 if id(fg) not in flats_done:
-                    fg.zero_grad()  # keep the grads as flat views
+                    fg.zero_grad(set_to_none)  # views kept unless the engine moves fresh grads in
+
                     flats_done.add(id(fg))
             for p in singles:
                 tag = getattr(p, "_dta_flat", None)
                 if tag is not None:
-                    tag[0].zero_grad()
+                    tag[0].zero_grad(set_to_none)
                 elif p.grad is not None:
                     if set_to_none:
                         p.grad = None
@@ -189,6 +193,8 @@ class FusedAdamW(torch.optim.Optimizer):
             for fg, ps in flats:
                 if len(ps) != len(fg.params):
                     raise ValueError("FusedAdamW: a FlatParamGroup must be optimised as a whole by one param group")
+                if not fg.prepare_grads_for_step():
+                    continue
                 st = self._flat_state.get(id(fg))
                 if st is None:
                     st = {"m": torch.zeros_like(fg.master), "v": torch.zeros_like(fg.master),
@@ -202,7 +208,7 @@ class FusedAdamW(torch.optim.Optimizer):
                         if ams:
                             self.state[p]["max_exp_avg_sq"] = fg._view(st["vmax"], i)
                 pb = fg.compute if fg.mixed else None
-                native().flat_adam(fg.master, _grad32(fg.grad), st["m"], st["v"], st["vmax"], pb, st["step"], lr, b1,
+                native().flat_adam(fg.master, fg.grad, st["m"], st["v"], st["vmax"], pb, st["step"], lr, b1,
                                    b2, eps, wd, 1.0, adamw, maxi, ams, True, -1)
             for p in singles:
                 if p.grad is None:

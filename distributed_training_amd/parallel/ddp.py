@@ -14,6 +14,11 @@ MI355X-first design:
   knob sized for xGMI (``bucket_cap_mb``, default 25 MiB like torch; large
   enough to amortise RCCL launch latency, small enough for >= 4-8 buckets of
   overlap on GPT-2-sized models);
+* ``zero_grad(set_to_none=True)`` drops the views so autograd hands each
+  gradient over without an accumulate-add kernel; when a bucket is ready all
+  its gradients are moved into the bucket slice by ONE multi-tensor copy
+  kernel (with the 1/world_size pre-scale fused when the backend has no
+  ``avg``) -- instead of one ``grad += new`` kernel per parameter;
 * a post-accumulate-grad hook per parameter counts readiness; ready buckets
   are launched strictly in bucket order (identical collective order on every
   rank) on the communicator's own HIP stream (native RCCL, ``ncclAvg``), so
@@ -62,6 +67,7 @@ class DistributedDataParallel(nn.Module):
         if not named:
             raise ValueError("DistributedDataParallel: module has no trainable parameters")
         self.flat: FlatParamGroup = build_flat_group(named, self.device, param_dtype=param_dtype, reverse=True)
+        self.flat.steal_ok = True
         self.buckets = self.flat.make_buckets(range(len(self.flat.params)), int(bucket_cap_mb * MiB),
                                               int(first_bucket_mb * MiB))
         self._param_bucket = {}
@@ -106,6 +112,7 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         self._works = []
         self._callback_queued = False
+        self._pending = [[] for _ in self.buckets]
 
     def _make_hook(self, i: int):
         def hook(p: torch.Tensor) -> None:
@@ -114,9 +121,9 @@ class DistributedDataParallel(nn.Module):
             if not self._callback_queued:
                 Variable._execution_engine.queue_callback(self._finalize)
                 self._callback_queued = True
-            if not self.flat.grad_is_view(i):
-                self.flat.rebind_grad(i)
             b = self._param_bucket[i]
+            if not self.flat.grad_is_view(i):
+                self._pending[b].append(i)  # moved into the bucket by one batched copy at launch
             self._ready[b] += 1
             self._launch_ready()
 
@@ -127,23 +134,54 @@ class DistributedDataParallel(nn.Module):
             self._launch(self._next)
             self._next += 1
 
+    @torch.no_grad()
+    def _gather_into_bucket(self, b: int, scale: float) -> bool:
+        """Copy the bucket's freshly produced (non-view) gradients into its
+        slice, scaled; rebind them as views.  Returns True if the whole slice
+        was already pre-scaled (every gradient went through the copy)."""
+        ids = self._pending[b]
+        if not ids:
+            return False
+        fl = self.flat
+        srcs = [fl.params[i].grad for i in ids]
+        dsts = [fl.grad_view(i) for i in ids]
+        if fl.grad.is_cuda and all(g.is_contiguous() and g.dtype == fl.grad.dtype for g in srcs):
+            from ..ops import native
+
+            native().mt_scale_copy([g.view(-1) for g in srcs], [d.view(-1) for d in dsts], scale, -1)
+        else:
+            for g, d in zip(srcs, dsts):
+                d.copy_(g if scale == 1.0 else g * scale)
+        for i, d in zip(ids, dsts):
+            fl.params[i].grad = d
+        self._pending[b] = []
+        return len(ids) == len(self.buckets[b].param_ids)
+
     def _launch(self, b: int) -> None:
         bk = self.buckets[b]
         sl = self.flat.grad[bk.start:bk.end]
+        prescale = self.world_size > 1 and not self.comm.supports_avg()
+        scaled = self._gather_into_bucket(b, 1.0 / self.world_size if prescale and self._whole(b) else 1.0)
         if self.world_size == 1:
             return
-        if self.comm.supports_avg():
+        if not prescale:
             self._works.append(self.comm.all_reduce(sl, op="avg", async_op=True))
         else:
-            sl.div_(self.world_size)  # pre-divide like the torch Reducer (mul_out by 1/ws)
+            if not scaled:
+                sl.div_(self.world_size)  # pre-divide like the torch Reducer (mul_out by 1/ws)
             self._works.append(self.comm.all_reduce(sl, op="sum", async_op=True))
+
+    def _whole(self, b: int) -> bool:
+        return len(self._pending[b]) == len(self.buckets[b].param_ids)
 
     def _finalize(self) -> None:
         # unused parameters: their (zeroed) grads still take part, in bucket order
         for b in range(self._next, len(self.buckets)):
             for i in self.buckets[b].param_ids:
+                if i in self._pending[b]:
+                    continue
                 if not self.flat.grad_is_view(i):
-                    self.flat.rebind_grad(i)
+                    self.flat.rebind_grad(i)  # unused parameter (None -> zeros) or a foreign grad
             self._launch(b)
         self._next = len(self.buckets)
         for w in self._works:
@@ -164,8 +202,8 @@ class DistributedDataParallel(nn.Module):
         finally:
             self.require_sync = old
 
-    def zero_grad(self, set_to_none: bool = True) -> None:  # noqa: ARG002 - grads stay flat views
-        self.flat.zero_grad()
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        self.flat.zero_grad(set_to_none)
 
     # ------------------------------------------------------------ state
     def state_dict(self, *args, **kwargs):

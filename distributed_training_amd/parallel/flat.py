@@ -63,6 +63,9 @@ class FlatParamGroup:
         self.mixed = param_dtype != torch.float32
         self.compute = self.master if not self.mixed else self.master.to(param_dtype)
         self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=device)
+        # set by an engine whose backward hooks move fresh gradients into the
+        # flat buffer (DDP): zero_grad(set_to_none=True) may then drop the views
+        self.steal_ok = False
         for i, p in enumerate(self.params):
             p.data = self.param_view(i)
             p.grad = self.grad_view(i)
@@ -105,11 +108,31 @@ class FlatParamGroup:
         g = self.params[i].grad
         return g is not None and g.data_ptr() == self.grad_view(i).data_ptr()
 
-    def zero_grad(self) -> None:
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        """``set_to_none``: drop the gradients (autograd then hands fresh
+        tensors over without an accumulate kernel; the DDP engine moves them
+        into the flat buffer in one batched copy per bucket).  Otherwise zero
+        the flat buffer and keep the views."""
+        if set_to_none and self.steal_ok:
+            for p in self.params:
+                p.grad = None
+            return
         self.grad.zero_()
         for i, p in enumerate(self.params):
             if p.grad is None or p.grad.data_ptr() != self.grad_view(i).data_ptr():
                 p.grad = self.grad_view(i)
+
+    def prepare_grads_for_step(self) -> bool:
+        """Before a flat optimizer step: make every gradient its flat view
+        (normally already true after a DDP backward).  Returns False when no
+        parameter has a gradient (torch optimizers skip such parameters)."""
+        if all(self.grad_is_view(i) for i in range(len(self.params))):
+            return True
+        if all(p.grad is None for p in self.params):
+            return False
+        for i in range(len(self.params)):
+            self.rebind_grad(i)
+        return True
 
     def sync_compute_from_master(self) -> None:
         if self.mixed:

@@ -124,8 +124,11 @@ class _Unit:
             self.gathered = True
 
     def set_views(self) -> None:
-        for (mod, attr, _, _), o, n, shp in zip(self.entries, self.offsets, self.numels, self.shapes):
-            setattr(mod, attr, self.full[o:o + n].view(shp))
+        aliases = self.owner._aliases
+        for (mod, attr, name, _), o, n, shp in zip(self.entries, self.offsets, self.numels, self.shapes):
+            view = self.full[o:o + n].view(shp)
+            for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
+                setattr(m2, a2, view)
 
     # ---------------------------------------------------------- backward
     def _post_backward(self, full: torch.Tensor) -> None:
@@ -174,11 +177,19 @@ class FullyShardedDataParallel(nn.Module):
                 for sub in m.modules():
                     covered.add(id(sub))
         param_owner: Dict[int, Tuple[nn.Module, str, str]] = {}
-        for mname, m in module.named_modules():
-            for pname, p in m.named_parameters(recurse=False):
-                if p.requires_grad and id(p) not in param_owner:
-                    full = f"{mname}.{pname}" if mname else pname
+        owners: Dict[int, List[Tuple[nn.Module, str, str]]] = {}
+        for mname, m in module.named_modules(remove_duplicate=False):
+            for pname, p in m.named_parameters(recurse=False, remove_duplicate=False):
+                if not p.requires_grad:
+                    continue
+                full = f"{mname}.{pname}" if mname else pname
+                if all(o[0] is not m or o[1] != pname for o in owners.get(id(p), [])):
+                    owners.setdefault(id(p), []).append((m, pname, full))
+                if id(p) not in param_owner:
                     param_owner[id(p)] = (m, pname, full)
+        # tied parameters (e.g. GPT-2 wte / lm_head): all owners get the same view
+        self._aliases: Dict[str, List[Tuple[nn.Module, str, str]]] = {
+            param_owner[k][2]: v for k, v in owners.items() if len(v) > 1}
         assigned: Set[int] = set()
         self.units: List[_Unit] = []
         for name, m in wrapped:
@@ -215,9 +226,11 @@ class FullyShardedDataParallel(nn.Module):
                 u.shard_param = sp
                 shard_params.append(sp)
                 names.append(f"unit{u.index}")
-                for mod, attr, _, _ in u.entries:  # remove the original parameters from the module tree
-                    del mod._parameters[attr]
-                    setattr(mod, attr, torch.empty(0, dtype=param_dtype, device=self.device))
+                for mod, attr, name, _ in u.entries:  # remove the original parameters from the module tree
+                    for m2, a2, _ in self._aliases.get(name, [(mod, attr, name)]):
+                        if a2 in m2._parameters:
+                            del m2._parameters[a2]
+                        setattr(m2, a2, torch.empty(0, dtype=param_dtype, device=self.device))
         self.shards = FlatParamGroup(shard_params, self.device, param_dtype=param_dtype, names=names)
         self.shard_params = nn.ParameterList(shard_params)
         if sync_module_states and self.world_size > 1:
@@ -350,7 +363,9 @@ class FullyShardedDataParallel(nn.Module):
             if keep:
                 for (_, _, name, _), o, n, shp in zip(u.entries, u.offsets, u.numels, u.shapes):
                     t = full[o:o + n].view(shp).clone()
-                    out[name] = t.cpu() if offload_to_cpu else t
+                    t = t.cpu() if offload_to_cpu else t
+                    for _, _, alias in self._aliases.get(name, [(None, None, name)]):
+                        out[alias] = t
         if keep:
             for name, b in self.module.named_buffers():
                 out[name] = b.detach().cpu().clone() if offload_to_cpu else b.detach().clone()

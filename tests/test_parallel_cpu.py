@@ -56,7 +56,7 @@ def _ddp_parity(rank, ws, bucket_mb, unused, accum):
     g = torch.Generator().manual_seed(100 + rank)
     for it in range(4):
         o1.zero_grad()
-        o2.zero_grad()
+        o2.zero_grad(set_to_none=it % 2 == 0)  # both the steal + batched-copy and the in-place-accumulate paths
         for micro in range(accum):
             x = torch.randn(8, 20, generator=g)
             y = torch.randn(8, 1, generator=g)
@@ -210,3 +210,39 @@ def _fsdp_ckpt(rank, ws):
 
 def test_native_fsdp_with_activation_checkpointing():
     run_gloo(_fsdp_ckpt, 2)
+
+
+def _fsdp_tied(rank, ws):
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_layer=2, n_head=2, n_embd=32, vocab_size=100, block_size=16)
+    ref = GPT2(cfg)
+    m = copy.deepcopy(ref)
+    fs = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={GPT2.block_class})
+    o1 = torch.optim.AdamW(ref.parameters(), lr=1e-2)
+    o2 = FusedAdamW(fs.parameters(), lr=1e-2)
+    g = torch.Generator().manual_seed(3)
+    X = torch.randint(0, 100, (4 * ws, 17), generator=g)
+    for it in range(3):
+        o1.zero_grad()
+        lo = ref(X[:, :-1])
+        F.cross_entropy(lo.reshape(-1, lo.shape[-1]), X[:, 1:].reshape(-1)).backward()
+        o1.step()
+        o2.zero_grad()
+        xs = X[rank * 4:(rank + 1) * 4]
+        lo2 = fs(xs[:, :-1])
+        F.cross_entropy(lo2.reshape(-1, lo2.shape[-1]), xs[:, 1:].reshape(-1)).backward()
+        o2.step()
+    sd = fs.full_state_dict(rank0_only=False)
+    rs = ref.state_dict()
+    assert set(sd) == set(rs) and "lm_head.weight" in sd
+    for k in rs:
+        torch.testing.assert_close(sd[k], rs[k], rtol=1e-4, atol=1e-5, msg=k)
+
+
+def test_native_fsdp_tied_weights_gpt2():
+    run_gloo(_fsdp_tied, 2)
