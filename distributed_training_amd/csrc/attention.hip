@@ -5,66 +5,129 @@
 // are [B, S, heads, D] with an arbitrary row (token) stride, so q/k/v can be
 // read straight out of a fused QKV projection buffer and O is written ready for
 // the output projection (no transposes).  GQA: q head h uses kv head
-// h / (H / Hkv).  Causal or full.
+// h / (H / Hkv).  Causal or full.  D in {64, 128}.
 //
-// FORWARD (one workgroup = 4 waves = 128 query rows of one (batch, head)):
-//   S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 with the KEYS on the accumulator
-//   rows and the QUERIES on the lanes, so each lane owns one query row: the
-//   online-softmax max / sum are per-lane values (plus one lane^32 exchange),
-//   and the rescale of O is a per-lane scalar.  P stays in registers and is the
-//   B operand of O^T = V^T . P (cdna_hip_programming.md §3 "accumulator tile as
-//   operand"; the permuted key order is matched by reading V^T from LDS).
-// BACKWARD (one workgroup = 4 waves = 128 keys of one (batch, kv head)):
-//   keys on the lanes; K and V fragments live in registers; per 32-row query
-//   block S = Q.K^T and dP = dO.V^T are recomputed, P = exp(S - LSE),
-//   dS = P (dP - delta); dV^T += dO^T.P and dK^T += Q^T.dS take P / dS as the
-//   B operand straight from the accumulators; dQ += dS.K goes through a
-//   wave-private LDS transpose of dS and is accumulated with fp32 atomics.
+// Every K/V/Q/dO tile is staged ONCE, row-major, in LDS (row stride D + 32
+// elements: consecutive rows 48 / 16 banks apart, so the 4-row x 2-group
+// pattern of a transposed read is conflict-free) and read both by rows
+// (ds_read_b128, MFMA operands whose k index is the head dim) and by columns
+// with the gfx950 hardware-transpose read ds_read_b64_tr_b16 (operands whose
+// k index is the key / query position).  Tiles are double-buffered in LDS and
+// the next tile's global loads are issued into registers right after the
+// single barrier of each step, so HBM latency hides behind the MFMAs.
+//
+// FORWARD (workgroup = 4 waves x 32 queries of one (batch, head)):
+//   S^T = K . Q^T with the KEYS on the accumulator rows and the QUERIES on the
+//   lanes, so the online-softmax max / sum are per-lane values (+ one lane^32
+//   exchange); P stays in registers and is the B operand of O^T = V^T . P
+//   (accumulator-as-operand, k order permuted; V^T fragments come from the
+//   row-major V tile through transposed reads).
+// BACKWARD, two atomic-free kernels (deterministic, no fp32 dQ buffer):
+//   dK/dV (workgroup = 4 waves x 32 keys of one (batch, kv head)): keys on the
+//     lanes, K/V fragments in registers; per 32-query slice (all q heads of
+//     the group) S = Q.K^T and dP = dO.V^T start from the row constants
+//     -LSE/scale and -delta as initial accumulators, P = exp2(c S),
+//     dS = P dP; dV^T += dO^T.P and dK^T += Q^T.dS take P / dS as the B
+//     operand as they stand (dO^T / Q^T by transposed reads).
+//   dQ (workgroup = 4 waves x 32 queries): the forward's orientation; S^T and
+//     dP^T recomputed per 64-key block, dQ^T += K^T . dS^T.
+//   The 10 B H S^2 D FLOPs of a fused backward become 14 (S and dP are
+//     computed twice) but the dQ float atomics -- bound at ~1.3 TB/s chip-wide
+//     (MI355X_MICROARCH.md 'Global float atomics'), which dominated the fused
+//     version at GPT-2 shapes -- disappear.
 #include "common.h"
+#include "attention.h"
 
 namespace dta {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1.0e30f;
 
-struct AttnArgs {
-  const bf16* q;
-  const bf16* k;
-  const bf16* v;
-  bf16* o;
-  float* lse;           // [B, H, S] natural-log LSE of the scaled scores
-  const bf16* dout;
-  float* delta;         // [B, H, S]  rowsum(dO * O)
-  float* dq_acc;        // [B, S, H, D] fp32 accumulation buffer (zeroed)
-  bf16* dk;
-  bf16* dv;
-  int64_t q_sb, q_ss, k_sb, k_ss, v_sb, v_ss;   // batch / token strides (elements); head stride = D
-  int64_t o_sb, o_ss, do_sb, do_ss;
-  int64_t dk_sb, dk_ss, dv_sb, dv_ss;
-  int B, S, H, Hkv;
-  float scale;
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of
+// row q (columns 4p..4p+3) of a 4 x 16 block; lane i receives column i of the
+// four rows (row q in element q).
+__device__ __forceinline__ bf16x4 lds_tr4(const bf16* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// A-operand fragment of X^T for a 32x32x16 MFMA whose B operand is an
+// accumulator tile used as it stands (its row index is the k index, in the
+// permuted order of cdna_hip_programming.md §3): lane (r32, hh) gets
+// X[row0 + 16s + 8(j>>2) + 4hh + (j&3)][col0 + r32], j = 0..7, from the
+// row-major LDS tile X (row stride ST elements) by two transposed reads.
+template <int ST>
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* X, int row0, int col0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int r = row0 + 16 * s + 4 * (g >> 1) + (i >> 2);
+  const int c = col0 + 16 * (g & 1) + 4 * (i & 3);
+  const bf16x4 lo = lds_tr4(X + r * ST + c);
+  const bf16x4 hi = lds_tr4(X + (r + 8) * ST + c);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Cooperative register staging of an [R][D] bf16 tile (256 threads, 16-byte
+// loads), rows >= nrows zero-filled; then one store into an LDS tile of row
+// stride ST.
+template <int R, int D>
+struct TileRegs {
+  static constexpr int N = R * D / 8 / 256;
+  bf16x8 v[N];
 };
+
+template <int R, int D>
+__device__ __forceinline__ void tile_load(TileRegs<R, D>& t, const bf16* base, int64_t rs, int row0, int nrows,
+                                          int tid) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int l = 0; l < TileRegs<R, D>::N; ++l) {
+    const int e = tid + l * 256, r = e / CPR, c8 = (e % CPR) * 8;
+    if (row0 + r < nrows) {
+      t.v[l] = *reinterpret_cast<const bf16x8*>(base + (int64_t)(row0 + r) * rs + c8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t.v[l][j] = f2bf(0.f);
+    }
+  }
+}
+
+template <int R, int D, int ST>
+__device__ __forceinline__ void tile_store(const TileRegs<R, D>& t, bf16* lds, int tid) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int l = 0; l < TileRegs<R, D>::N; ++l) {
+    const int e = tid + l * 256, r = e / CPR, c8 = (e % CPR) * 8;
+    *reinterpret_cast<bf16x8*>(lds + r * ST + c8) = t.v[l];
+  }
+}
+
+__device__ __forceinline__ f32x16 splat16(float x) {
+  return f32x16{x, x, x, x, x, x, x, x, x, x, x, x, x, x, x, x};
+}
 
 // ------------------------------------------------------------------ forward
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   constexpr int BN = 64;         // keys per block
-  constexpr int KS = D + 8;      // LDS row stride of K tile (bf16)
-  constexpr int VTS = BN + 8;    // LDS row stride of V^T tile
+  constexpr int ST = D + 32;     // LDS row stride (elements)
   constexpr int NKS = D / 16;    // MFMA k-steps over D
   constexpr int NDT = D / 32;    // 32-wide output tiles over D
-  __shared__ __attribute__((aligned(16))) bf16 Ks[BN * KS];
-  __shared__ __attribute__((aligned(16))) bf16 Vt[D * VTS];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * ST];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * ST];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int hk = h / (a.H / a.Hkv);
-  const int q0 = blockIdx.x * 128 + wave * 32;
-  const int qrow = q0 + r32;  // this lane's query row
-  const bf16* qbase = a.q + (int64_t)b * a.q_sb + (int64_t)h * D;
-  const bf16* kbase = a.k + (int64_t)b * a.k_sb + (int64_t)hk * D;
-  const bf16* vbase = a.v + (int64_t)b * a.v_sb + (int64_t)hk * D;
+  const int q0w = blockIdx.x * 128 + wave * 32;
+  const int qrow = q0w + r32;  // this lane's query row
+  const bf16* qbase = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)h * D;
+  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
+  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + (int64_t)hk * D;
 
   // Q fragments (B operand of S^T = K.Q^T): lane (col q, half hh) holds Q[q][16ks + 8hh + j]
   bf16x8 qf[NKS];
@@ -76,65 +139,65 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[ks][j] = f2bf(0.f);
   }
-  const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 oacc[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16;
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = splat16(0.f);
   float m = kNegBig, l = 0.f;
   const float c = a.scale * kLog2e;
 
-  const int wg_q_end = min(blockIdx.x * 128 + 128, a.S);
-  const int kv_end = CAUSAL ? wg_q_end : a.S;
-  for (int k0 = 0; k0 < kv_end; k0 += BN) {
-    // ---- stage K [BN][D] and V^T [D][BN] (16-byte global loads) ----
-    for (int e = tid; e < BN * (D / 8); e += 256) {
-      const int key = e / (D / 8), c8 = (e % (D / 8)) * 8;
-      bf16x8 kv, vv;
-      if (k0 + key < a.S) {
-        kv = *reinterpret_cast<const bf16x8*>(kbase + (int64_t)(k0 + key) * a.k_ss + c8);
-        vv = *reinterpret_cast<const bf16x8*>(vbase + (int64_t)(k0 + key) * a.v_ss + c8);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) kv[j] = vv[j] = f2bf(0.f);
-      }
-      *reinterpret_cast<bf16x8*>(Ks + key * KS + c8) = kv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(c8 + j) * VTS + key] = vv[j];
-    }
+  const int kv_end = CAUSAL ? min((int)blockIdx.x * 128 + 128, a.S) : a.S;
+  const int nblk = (kv_end + BN - 1) / BN;
+  TileRegs<BN, D> kr, vr;
+  tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
+  tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1;
+    tile_store<BN, D, ST>(kr, Ks[buf], tid);
+    tile_store<BN, D, ST>(vr, Vs[buf], tid);
     __syncthreads();
-    // ---- S^T tiles: rows = keys (k0 + t*32 + row), cols = this wave's queries ----
+    if (j + 1 < nblk) {
+      tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
+      tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
+    }
+    const int k0 = j * BN;
+    if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
+    const bf16* Kb = Ks[buf];
+    const bf16* Vb = Vs[buf];
+    // ---- S^T tiles: rows = keys k0 + t*32 + row, cols = this wave's queries ----
     f32x16 st[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      st[t] = zero16;
+      st[t] = splat16(0.f);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (t * 32 + r32) * KS + ks * 16 + hh * 8);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
         st[t] = mfma32x32x16(kf, qf[ks], st[t]);
       }
     }
     // ---- scale, mask, online softmax (per-lane query row) ----
+    const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
     float mblk = kNegBig;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int key = k0 + t * 32 + mfma32_row(i, lane);
         float s = st[t][i] * c;
-        const bool masked = key >= a.S || (CAUSAL && key > qrow);
-        s = masked ? kNegBig : s;
+        if (need_mask) {
+          const int key = k0 + t * 32 + mfma32_row(i, lane);
+          s = (key >= a.S || (CAUSAL && key > qrow)) ? kNegBig : s;
+        }
         st[t][i] = s;
         mblk = fmaxf(mblk, s);
       }
     mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
     const float mnew = fmaxf(m, mblk);
-    const float alpha = exp2f(m - mnew);
+    const float alpha = fexp2(m - mnew);
     float lsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(st[t][i] - mnew);
+        const float p = fexp2(st[t][i] - mnew);
         st[t][i] = p;
         lsum += p;
       }
@@ -145,30 +208,22 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-    // ---- O^T += V^T . P ----
+    // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = f2bf(st[t][8 * s + j]);
-        const int kb = t * 32 + 16 * s + 4 * hh;
+        for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const bf16* vr = Vt + (dt * 32 + r32) * VTS + kb;
-          const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(vr);
-          const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(vr + 8);
-          const bf16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          oacc[dt] = mfma32x32x16(vf, pb, oacc[dt]);
-        }
+        for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<ST>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
       }
-    __syncthreads();
   }
   // ---- epilogue: O = O^T^T / l ; LSE ----
   if (qrow < a.S) {
     const float inv = 1.f / l;
-    bf16* orow = a.o + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * D;
+    bf16* orow = static_cast<bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -182,18 +237,18 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------ backward
-// delta[b,h,q] = sum_d dO * O   (one wave per query row group)
+// delta[b,h,q] = sum_d dO * O   (8 threads per (b, q, h) row)
 template <int D>
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a) {
   const int tid = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * 32 + (tid >> 3);  // 8 threads per (b, q, h) row
+  const int64_t row = (int64_t)blockIdx.x * 32 + (tid >> 3);
   const int64_t total = (int64_t)a.B * a.S * a.H;
   if (row >= total) return;
   const int h = row % a.H;
   const int64_t bq = row / a.H;
   const int q = bq % a.S, b = bq / a.S;
-  const bf16* o = a.o + (int64_t)b * a.o_sb + (int64_t)q * a.o_ss + (int64_t)h * D;
-  const bf16* d = a.dout + (int64_t)b * a.do_sb + (int64_t)q * a.do_ss + (int64_t)h * D;
+  const bf16* o = static_cast<const bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)q * a.o_ss + (int64_t)h * D;
+  const bf16* d = static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)q * a.do_ss + (int64_t)h * D;
   float acc = 0.f;
   for (int c = (tid & 7) * 8; c < D; c += 64) {
     const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + c);
@@ -207,30 +262,26 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a) {
 }
 
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
-  constexpr int BM = 32;        // query rows per inner block
-  constexpr int RS = D + 8;     // row-major tile stride (bf16)
-  constexpr int TS = BM + 8;    // transposed tile stride
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
+  constexpr int BM = 32;        // query rows per slice
+  constexpr int ST = D + 32;    // LDS row stride (elements)
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16 Qs[BM * RS];
-  __shared__ __attribute__((aligned(16))) bf16 dOs[BM * RS];
-  __shared__ __attribute__((aligned(16))) bf16 Qt[D * TS];
-  __shared__ __attribute__((aligned(16))) bf16 dOt[D * TS];
-  __shared__ __attribute__((aligned(16))) bf16 Ktw[4 * D * TS];   // per wave: K^T [d][32 keys]
-  __shared__ __attribute__((aligned(16))) bf16 dSw[4 * BM * TS];  // per wave: dS [q][32 keys]
-  __shared__ float lse2[BM], dlt[BM];
-  __shared__ __attribute__((aligned(16))) float dQs[BM * D];  // workgroup-level dQ partial (LDS atomics)
+  __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * ST];
+  __shared__ __attribute__((aligned(16))) bf16 dOs[2][BM * ST];
+  __shared__ __attribute__((aligned(16))) float rc[2][2][BM];  // [buf][-lse/scale | -delta][q]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int bk = blockIdx.y, b = bk / a.Hkv, hk = bk % a.Hkv;
   const int group = a.H / a.Hkv;
   const int kblk0 = blockIdx.x * 128;
-  const int key = kblk0 + wave * 32 + r32;  // this lane's key
-  const bf16* kbase = a.k + (int64_t)b * a.k_sb + (int64_t)hk * D;
-  const bf16* vbase = a.v + (int64_t)b * a.v_sb + (int64_t)hk * D;
-  const float c = a.scale * kLog2e;
+  const int kw0 = kblk0 + wave * 32;  // this wave's first key
+  const int key = kw0 + r32;          // this lane's key
+  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
+  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + (int64_t)hk * D;
+  const float c = a.scale * kLog2e, inv_scale = 1.f / a.scale;
 
   bf16x8 kf[NKS], vf[NKS];
 #pragma unroll
@@ -243,126 +294,82 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) kf[ks][j] = vf[ks][j] = f2bf(0.f);
     }
   }
-  // wave-private K^T tile for dQ = dS . K  (lane r32 holds key r32: write its d column)
-  bf16* Kt = Ktw + wave * D * TS;
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Kt[(ks * 16 + hh * 8 + j) * TS + r32] = kf[ks][j];
-  bf16* dSt = dSw + wave * BM * TS;
-
-  const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 dvacc[NDT], dkacc[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) dvacc[dt] = dkacc[dt] = zero16;
+  for (int dt = 0; dt < NDT; ++dt) dvacc[dt] = dkacc[dt] = splat16(0.f);
 
-  const int qstart = CAUSAL ? (kblk0 / BM) * BM : 0;
-  for (int hq = hk * group; hq < (hk + 1) * group; ++hq) {
-    const bf16* qbase = a.q + (int64_t)b * a.q_sb + (int64_t)hq * D;
-    const bf16* dobase = a.dout + (int64_t)b * a.do_sb + (int64_t)hq * D;
-    const float* lse_h = a.lse + ((int64_t)b * a.H + hq) * a.S;
-    const float* dl_h = a.delta + ((int64_t)b * a.H + hq) * a.S;
-    float* dqb = a.dq_acc + (int64_t)b * a.S * a.H * D + (int64_t)hq * D;
-    for (int q0 = qstart; q0 < a.S; q0 += BM) {
-      __syncthreads();  // previous block's LDS reads are done
-      for (int e = tid; e < BM * (D / 8); e += 256) {
-        const int qr = e / (D / 8), c8 = (e % (D / 8)) * 8;
-        bf16x8 qv, dv;
-        if (q0 + qr < a.S) {
-          qv = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)(q0 + qr) * a.q_ss + c8);
-          dv = *reinterpret_cast<const bf16x8*>(dobase + (int64_t)(q0 + qr) * a.do_ss + c8);
-        } else {
+  const int qstart = CAUSAL ? kblk0 : 0;
+  const int nslice = (a.S - qstart + BM - 1) / BM;
+  const int total = nslice * group;
+  TileRegs<BM, D> qr, dr;
+  float rcv = 0.f;
+  auto load = [&](int it) {
+    const int hq = hk * group + it / nslice;
+    const int q0 = qstart + (it % nslice) * BM;
+    tile_load(qr, static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, q0, a.S, tid);
+    tile_load(dr, static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, q0, a.S, tid);
+    if (tid < 2 * BM) {
+      const int qq = q0 + (tid & (BM - 1));
+      const int64_t ri = ((int64_t)b * a.H + hq) * a.S + qq;
+      if (tid < BM) rcv = qq < a.S ? -a.lse[ri] * inv_scale : kNegBig;  // q >= S: P = 0
+      else rcv = qq < a.S ? -a.delta[ri] : 0.f;
+    }
+  };
+  load(0);
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    tile_store<BM, D, ST>(qr, Qs[buf], tid);
+    tile_store<BM, D, ST>(dr, dOs[buf], tid);
+    if (tid < 2 * BM) rc[buf][tid >> 5][tid & (BM - 1)] = rcv;
+    __syncthreads();
+    if (it + 1 < total) load(it + 1);
+    const int q0 = qstart + (it % nslice) * BM;
+    if (CAUSAL && q0 + BM - 1 < kw0) continue;  // all of this wave's keys are after the slice
+    const bf16* Qb = Qs[buf];
+    const bf16* Db = dOs[buf];
+    // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
+    f32x16 s, dp;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qv[j] = dv[j] = f2bf(0.f);
-        }
-        *reinterpret_cast<bf16x8*>(Qs + qr * RS + c8) = qv;
-        *reinterpret_cast<bf16x8*>(dOs + qr * RS + c8) = dv;
+    for (int i = 0; i < 16; ++i) {
+      const int qi = mfma32_row(i, lane);
+      s[i] = rc[buf][0][qi];
+      dp[i] = rc[buf][1][qi];
+    }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          Qt[(c8 + j) * TS + qr] = qv[j];
-          dOt[(c8 + j) * TS + qr] = dv[j];
-        }
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qb + r32 * ST + ks * 16 + hh * 8);
+      const bf16x8 da = *reinterpret_cast<const bf16x8*>(Db + r32 * ST + ks * 16 + hh * 8);
+      s = mfma32x32x16(qa, kf[ks], s);
+      dp = mfma32x32x16(da, vf[ks], dp);
+    }
+    const bool need_mask = CAUSAL && q0 < kw0 + 31;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float pv = fexp2(s[i] * c);
+      if (need_mask && key > q0 + mfma32_row(i, lane)) pv = 0.f;
+      s[i] = pv;             // P
+      dp[i] = pv * dp[i];    // dS (unscaled)
+    }
+    // dV^T += dO^T . P ;  dK^T += Q^T . dS
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pb, db;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pb[j] = f2bf(s[8 * st + j]);
+        db[j] = f2bf(dp[8 * st + j]);
       }
-      if (tid < BM) {
-        const int qr = q0 + tid;
-        lse2[tid] = qr < a.S ? lse_h[qr] * kLog2e : 0.f;
-        dlt[tid] = qr < a.S ? dl_h[qr] : 0.f;
-      }
-      for (int e = tid; e < BM * D; e += 256) dQs[e] = 0.f;
-      __syncthreads();
-      // S = Q.K^T and dP = dO.V^T: rows = queries, cols = this wave's keys
-      f32x16 s = zero16, dp = zero16;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + r32 * RS + ks * 16 + hh * 8);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + r32 * RS + ks * 16 + hh * 8);
-        s = mfma32x32x16(qa, kf[ks], s);
-        dp = mfma32x32x16(da, vf[ks], dp);
-      }
-      f32x16 p, ds;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = mfma32_row(i, lane);
-        const int qr = q0 + qi;
-        const bool masked = qr >= a.S || key >= a.S || (CAUSAL && key > qr);
-        const float pv = masked ? 0.f : exp2f(s[i] * c - lse2[qi]);
-        p[i] = pv;
-        ds[i] = pv * (dp[i] - dlt[qi]);
-      }
-      // dV^T += dO^T . P ;  dK^T += Q^T . dS   (P / dS are the B operand as they stand)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pb, db;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pb[j] = f2bf(p[8 * st + j]);
-          db[j] = f2bf(ds[8 * st + j]);
-        }
-        const int qb = 16 * st + 4 * hh;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const bf16* dr = dOt + (dt * 32 + r32) * TS + qb;
-          const bf16* qr = Qt + (dt * 32 + r32) * TS + qb;
-          const bf16x4 d0 = *reinterpret_cast<const bf16x4*>(dr);
-          const bf16x4 d1 = *reinterpret_cast<const bf16x4*>(dr + 8);
-          const bf16x4 q0v = *reinterpret_cast<const bf16x4*>(qr);
-          const bf16x4 q1v = *reinterpret_cast<const bf16x4*>(qr + 8);
-          const bf16x8 dA = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
-          const bf16x8 qA = {q0v[0], q0v[1], q0v[2], q0v[3], q1v[0], q1v[1], q1v[2], q1v[3]};
-          dvacc[dt] = mfma32x32x16(dA, pb, dvacc[dt]);
-          dkacc[dt] = mfma32x32x16(qA, db, dkacc[dt]);
-        }
-      }
-      // dQ[q][d] += dS[q][key] . K[key][d]: dS transposed through the wave's LDS tile
-#pragma unroll
-      for (int i = 0; i < 16; ++i) dSt[mfma32_row(i, lane) * TS + r32] = f2bf(ds[i]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        f32x16 dq = zero16;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8 sa = *reinterpret_cast<const bf16x8*>(dSt + r32 * TS + ks * 16 + hh * 8);
-          const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Kt + (dt * 32 + r32) * TS + ks * 16 + hh * 8);
-          dq = mfma32x32x16(sa, kb, dq);  // rows q, cols d
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) atomicAdd(&dQs[mfma32_row(i, lane) * D + dt * 32 + r32], dq[i]);
-      }
-      // one global fp32 atomic per element per workgroup (4 waves reduced in LDS first)
-      __syncthreads();
-      for (int e = tid; e < BM * D; e += 256) {
-        const int qr = q0 + e / D;
-        if (qr < a.S) atomicAdd(dqb + (int64_t)qr * a.H * D + (e % D), dQs[e] * a.scale);
+        dvacc[dt] = mfma32x32x16(tr_frag<ST>(Db, 0, dt * 32, st, lane), pb, dvacc[dt]);
+        dkacc[dt] = mfma32x32x16(tr_frag<ST>(Qb, 0, dt * 32, st, lane), db, dkacc[dt]);
       }
     }
   }
   // ---- epilogue: dK = (dK^T)^T * scale, dV = (dV^T)^T ----
   if (key < a.S) {
-    bf16* dkr = a.dk + (int64_t)b * a.dk_sb + (int64_t)key * a.dk_ss + (int64_t)hk * D;
-    bf16* dvr = a.dv + (int64_t)b * a.dv_sb + (int64_t)key * a.dv_ss + (int64_t)hk * D;
+    bf16* dkr = static_cast<bf16*>(a.dk) + (int64_t)b * a.dk_sb + (int64_t)key * a.dk_ss + (int64_t)hk * D;
+    bf16* dvr = static_cast<bf16*>(a.dv) + (int64_t)b * a.dv_sb + (int64_t)key * a.dv_ss + (int64_t)hk * D;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -374,6 +381,108 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
                            f2bf(dvacc[dt][4 * g + 3])};
         *reinterpret_cast<bf16x4*>(dkr + d0) = kv;
         *reinterpret_cast<bf16x4*>(dvr + d0) = vv;
+      }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int BN = 64;
+  constexpr int ST = D + 32;
+  constexpr int NKS = D / 16;
+  constexpr int NDT = D / 32;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * ST];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * ST];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int hk = h / (a.H / a.Hkv);
+  const int q0w = blockIdx.x * 128 + wave * 32;
+  const int qrow = q0w + r32;
+  const bf16* qbase = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)h * D;
+  const bf16* dobase = static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)h * D;
+  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
+  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + (int64_t)hk * D;
+  const float c = a.scale * kLog2e;
+
+  bf16x8 qf[NKS], df[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    if (qrow < a.S) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)qrow * a.q_ss + ks * 16 + hh * 8);
+      df[ks] = *reinterpret_cast<const bf16x8*>(dobase + (int64_t)qrow * a.do_ss + ks * 16 + hh * 8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = df[ks][j] = f2bf(0.f);
+    }
+  }
+  const int64_t ri = ((int64_t)b * a.H + h) * a.S + qrow;
+  const float s_init = qrow < a.S ? -a.lse[ri] / a.scale : kNegBig;
+  const float dp_init = qrow < a.S ? -a.delta[ri] : 0.f;
+  f32x16 dqacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = splat16(0.f);
+
+  const int kv_end = CAUSAL ? min((int)blockIdx.x * 128 + 128, a.S) : a.S;
+  const int nblk = (kv_end + BN - 1) / BN;
+  TileRegs<BN, D> kr, vr;
+  tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
+  tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
+  for (int j = 0; j < nblk; ++j) {
+    const int buf = j & 1;
+    tile_store<BN, D, ST>(kr, Ks[buf], tid);
+    tile_store<BN, D, ST>(vr, Vs[buf], tid);
+    __syncthreads();
+    if (j + 1 < nblk) {
+      tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
+      tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
+    }
+    const int k0 = j * BN;
+    if (CAUSAL && k0 > q0w + 31) continue;
+    const bf16* Kb = Ks[buf];
+    const bf16* Vb = Vs[buf];
+    const bool need_mask = CAUSAL && k0 + BN - 1 > q0w;
+    // S^T = K.Q^T - LSE/scale, dP^T = V.dO^T - delta: rows = keys, cols = queries.
+    // Keys >= S are zero rows of K and V: they add nothing to dQ.
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 s = splat16(s_init), dp = splat16(dp_init);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(Kb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(Vb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
+        s = mfma32x32x16(ka, qf[ks], s);
+        dp = mfma32x32x16(va, df[ks], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = fexp2(s[i] * c);
+        if (need_mask && k0 + t * 32 + mfma32_row(i, lane) > qrow) pv = 0.f;
+        dp[i] *= pv;  // dS^T
+      }
+      // dQ^T += K^T . dS^T  (K^T by transposed reads; dS^T as it stands)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 db;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) db[jj] = f2bf(dp[8 * s2 + jj]);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+          dqacc[dt] = mfma32x32x16(tr_frag<ST>(Kb, t * 32, dt * 32, s2, lane), db, dqacc[dt]);
+      }
+    }
+  }
+  if (qrow < a.S) {
+    bf16* dqr = static_cast<bf16*>(a.dq) + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * D;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x4 qv = {f2bf(dqacc[dt][4 * g] * a.scale), f2bf(dqacc[dt][4 * g + 1] * a.scale),
+                           f2bf(dqacc[dt][4 * g + 2] * a.scale), f2bf(dqacc[dt][4 * g + 3] * a.scale)};
+        *reinterpret_cast<bf16x4*>(dqr + dt * 32 + 8 * g + 4 * hh) = qv;
       }
   }
 }
@@ -394,9 +503,14 @@ template <int D>
 static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
-  dim3 grid((a.S + 127) / 128, a.B * a.Hkv);
-  if (causal) hipLaunchKernelGGL((attn_bwd_kernel<D, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_bwd_kernel<D, false>), grid, dim3(256), 0, st, a);
+  dim3 gkv((a.S + 127) / 128, a.B * a.Hkv), gq((a.S + 127) / 128, a.B * a.H);
+  if (causal) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 

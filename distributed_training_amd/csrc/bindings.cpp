@@ -14,25 +14,7 @@
 #include "mlp_fused.h"
 #include "rccl_comm.h"
 
-namespace dta {
-struct AttnArgs {  // mirror of csrc/attention.hip
-  const void* q;
-  const void* k;
-  const void* v;
-  void* o;
-  float* lse;
-  const void* dout;
-  float* delta;
-  float* dq_acc;
-  void* dk;
-  void* dv;
-  int64_t q_sb, q_ss, k_sb, k_ss, v_sb, v_ss;
-  int64_t o_sb, o_ss, do_sb, do_ss;
-  int64_t dk_sb, dk_ss, dv_sb, dv_ss;
-  int B, S, H, Hkv;
-  float scale;
-};
-}  // namespace dta
+#include "attention.h"
 hipError_t dta_attn_fwd(const dta::AttnArgs*, int, bool, hipStream_t);
 hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, float*, float*, int64_t, int, float,
                         hipStream_t);
@@ -356,21 +338,20 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::
   TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * S,
               "lse must be f32 [B, H, S]");
   auto delta = torch::empty({B, H, S}, lse.options());
-  auto dq_acc = torch::zeros({B, S, H, D}, lse.options());
+  auto dq = torch::empty({B, S, H, D}, q.options());
   auto dk = torch::empty({B, S, Hkv, D}, q.options());
   auto dv = torch::empty({B, S, Hkv, D}, q.options());
   dta::AttnArgs a{};
   a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr(); a.o = o.data_ptr(); a.lse = lse.data_ptr<float>();
-  a.dout = dout.data_ptr(); a.delta = delta.data_ptr<float>(); a.dq_acc = dq_acc.data_ptr<float>();
+  a.dout = dout.data_ptr(); a.delta = delta.data_ptr<float>(); a.dq = dq.data_ptr();
   a.dk = dk.data_ptr(); a.dv = dv.data_ptr();
   a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.k_sb = k.stride(0); a.k_ss = k.stride(1);
   a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.o_sb = o.stride(0); a.o_ss = o.stride(1);
   a.do_sb = dout.stride(0); a.do_ss = dout.stride(1);
+  a.dq_sb = dq.stride(0); a.dq_ss = dq.stride(1);
   a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1);
   a.B = (int)B; a.S = (int)S; a.H = (int)H; a.Hkv = (int)Hkv; a.scale = (float)scale;
   hip_ok(dta_attn_bwd(&a, (int)D, causal, pick_stream(stream)), "attn_bwd");
-  auto dq = torch::empty({B, S, H, D}, q.options());
-  hip_ok(dta_cast_f32_bf16(dq_acc.data_ptr<float>(), dq.data_ptr(), dq.numel(), pick_stream(stream)), "dq cast");
   return {dq, dk, dv};
 }
 

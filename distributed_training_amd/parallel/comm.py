@@ -211,6 +211,10 @@ class RcclComm(Communicator):
         return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t])
 
     def all_gather_into(self, out, inp, async_op=False):
+        if self.world_size == 1:  # single rank: a device copy on the current stream
+            if out.data_ptr() != inp.data_ptr():
+                out.view(-1).copy_(inp.view(-1))
+            return CommWork() if async_op else None
         return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp])
 
     def reduce_scatter_into(self, out, inp, op="sum", async_op=False):

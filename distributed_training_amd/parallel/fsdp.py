@@ -78,6 +78,17 @@ class _Unit:
             off = _align(off + n, 16)
         self.total = _align(max(off, 16), ws * 16)
         self.shard_size = self.total // ws
+        # split sizes covering [0, total): parameter pieces and padding gaps
+        self._split_sizes, self._piece_index = [], []
+        pos = 0
+        for o, n in zip(self.offsets, self.numels):
+            if o > pos:
+                self._split_sizes.append(o - pos)
+            self._piece_index.append(len(self._split_sizes))
+            self._split_sizes.append(n)
+            pos = o + n
+        if self.total > pos:
+            self._split_sizes.append(self.total - pos)
         dt = owner.param_dtype
         self.full = torch.zeros(self.total, dtype=dt, device=owner.device).requires_grad_(True)
         self._nbytes = self.full.untyped_storage().nbytes()
@@ -124,9 +135,15 @@ class _Unit:
             self.gathered = True
 
     def set_views(self) -> None:
+        """Point the module attributes at views of the gathered flat buffer.
+        The views come from ONE ``split_with_sizes`` (padding segments
+        included), so backward builds the unit's flat gradient with a single
+        concatenation -- per-slice views would each allocate a zero-filled
+        full-size gradient and add it in (O(params x unit size) traffic)."""
         aliases = self.owner._aliases
-        for (mod, attr, name, _), o, n, shp in zip(self.entries, self.offsets, self.numels, self.shapes):
-            view = self.full[o:o + n].view(shp)
+        pieces = self.full.split(self._split_sizes)
+        for (mod, attr, name, _), k, shp in zip(self.entries, self._piece_index, self.shapes):
+            view = pieces[k].view(shp)
             for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
                 setattr(m2, a2, view)
 
@@ -136,12 +153,15 @@ class _Unit:
         own._queue_final_callback()
         g = full.grad
         full.grad = None
-        out = torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
-        op = "avg" if own.comm.supports_avg() else "sum"
-        if op == "sum" and own.world_size > 1:
-            g.div_(own.world_size)
-        work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
-        own._pending_rs.append((self, work, out, g))
+        if own.world_size == 1:  # the whole gradient is this rank's shard: no collective, no copy
+            own._pending_rs.append((self, CommWork(), g, g))
+        else:
+            out = torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
+            op = "avg" if own.comm.supports_avg() else "sum"
+            if op == "sum":
+                g.div_(own.world_size)
+            work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
+            own._pending_rs.append((self, work, out, g))
         self.in_backward = False
         if not self.is_root or own.reshard_root_after_backward:
             self.free()

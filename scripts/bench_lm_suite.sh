@@ -1,11 +1,14 @@
 #!/bin/bash
-# GPT-2 small / Llama benchmarks on one GPU: native vs stock PyTorch (GPU box).
+# GPT-2 small / Llama benchmarks on one GPU (GPU box).  Usage:
+#   bash scripts/bench_lm_suite.sh "--model gpt2 --strategy ddp" "--model gpt2 --strategy fsdp --impl torch" ...
+# (no arguments: GPT-2 DDP + FSDP, native and stock PyTorch)
 cd "$(dirname "$0")/.."
 export PYTHONPATH=$PWD
 OUT=gpurun_out/lm_suite.log
-run() { timeout -k 10 300 python bench_lm.py "$@" --json-out /tmp/lm.json > /tmp/lm.log 2>&1 && cat /tmp/lm.json >> $OUT || { echo "FAIL $*" >> $OUT; tail -20 /tmp/lm.log >> $OUT; return 1; }; }
-
-
-run --model gpt2 --strategy fsdp --batch 8 --seq 1024 --steps 20 --warmup 5 || exit 1
-run --model gpt2 --strategy fsdp --batch 8 --seq 1024 --steps 20 --warmup 5 --impl torch || exit 1
-run --model llama_tiny --strategy fsdp --batch 4 --seq 2048 --steps 10 --warmup 3 || exit 1
+mkdir -p gpurun_out
+run() { timeout -k 10 300 python bench_lm.py $1 --json-out /tmp/lm.json > /tmp/lm.log 2>&1 && cat /tmp/lm.json >> $OUT || { echo "FAIL $1" >> $OUT; tail -20 /tmp/lm.log >> $OUT; return 1; }; }
+if [ $# -eq 0 ]; then
+  set -- "--model gpt2 --strategy ddp" "--model gpt2 --strategy ddp --impl torch" \
+         "--model gpt2 --strategy fsdp" "--model gpt2 --strategy fsdp --impl torch"
+fi
+for cfg in "$@"; do run "$cfg" || exit 1; done
