@@ -41,6 +41,13 @@ hipError_t dta_flat_clip(float*, int64_t, const float*, float, hipStream_t);
 hipError_t dta_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 hipError_t dta_mlp2_fused_step(const dta::MlpArgs*, hipStream_t);
 size_t dta_mlp2_lds_bytes(int64_t, int, int);
+hipError_t dta_p2p_create(int, int, int64_t, void**, void*);
+int dta_p2p_handle_bytes();
+hipError_t dta_p2p_open(void*, const void*);
+int dta_p2p_num_wg(int64_t);
+hipError_t dta_p2p_allreduce(void*, float*, int64_t, float, int, hipStream_t);
+hipError_t dta_p2p_error(void*, int*);
+void dta_p2p_destroy(void*);
 
 namespace {
 
@@ -563,6 +570,51 @@ class PyRcclComm {
 
 }  // namespace
 
+// One-shot intra-node all-reduce over peer (xGMI) memory: csrc/p2p_allreduce.hip
+class PyP2PAllReduce {
+ public:
+  PyP2PAllReduce(int rank, int world, int64_t max_elems) : world_(world), max_elems_(max_elems) {
+    std::string h(dta_p2p_handle_bytes(), '\0');
+    hip_ok(dta_p2p_create(rank, world, max_elems, &state_, h.data()), "p2p create");
+    handle_ = h;
+  }
+  ~PyP2PAllReduce() { destroy(); }
+  py::bytes handle() const { return py::bytes(handle_); }
+  void open(std::vector<py::bytes> handles) {
+    TORCH_CHECK((int)handles.size() == world_, "p2p open: need one handle per rank");
+    std::string all;
+    for (auto& h : handles) {
+      std::string s = h;
+      TORCH_CHECK((int)s.size() == dta_p2p_handle_bytes(), "p2p open: bad handle size");
+      all += s;
+    }
+    hip_ok(dta_p2p_open(state_, all.data()), "p2p open");
+  }
+  void all_reduce(torch::Tensor t, double scale, int64_t timeout_iters, int64_t stream) {
+    check_f32(t, "tensor");
+    TORCH_CHECK(t.numel() <= max_elems_, "p2p all_reduce: tensor larger than the slot capacity");
+    hip_ok(dta_p2p_allreduce(state_, t.data_ptr<float>(), t.numel(), (float)scale, (int)timeout_iters,
+                             pick_stream(stream)),
+           "p2p all_reduce");
+  }
+  int error() const {
+    int e = 0;
+    hip_ok(dta_p2p_error(state_, &e), "p2p error");
+    return e;
+  }
+  void destroy() {
+    if (state_) dta_p2p_destroy(state_);
+    state_ = nullptr;
+  }
+  int64_t max_elems() const { return max_elems_; }
+
+ private:
+  void* state_ = nullptr;
+  int world_;
+  int64_t max_elems_;
+  std::string handle_;
+};
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_training_amd native runtime (gfx950 HIP kernels + RCCL communicator)";
   m.def("flat_sgd", &flat_sgd);
@@ -598,6 +650,15 @@ PYBIND11_MODULE(_C, m) {
     if (dta::rccl_loaded()) dta::rccl_api().GetVersion(&v);
     return v;
   });
+  m.def("p2p_num_wg", &dta_p2p_num_wg);
+  py::class_<PyP2PAllReduce>(m, "P2PAllReduce")
+      .def(py::init<int, int, int64_t>())
+      .def("handle", &PyP2PAllReduce::handle)
+      .def("open", &PyP2PAllReduce::open)
+      .def("all_reduce", &PyP2PAllReduce::all_reduce)
+      .def("error", &PyP2PAllReduce::error)
+      .def("destroy", &PyP2PAllReduce::destroy)
+      .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())
       .def("all_reduce", &PyRcclComm::all_reduce)

@@ -143,6 +143,8 @@ class FusedMLPProgram:
     @torch.no_grad()
     def store_to_module(self) -> None:
         self.flush()
+        if hasattr(self.comm, "check_errors"):
+            self.comm.check_errors()  # a p2p all-reduce that timed out on a dead peer raises here
         v = self.layout.views(self.P[self.parity])
         for name, p in self.module.named_parameters():
             tag = getattr(p, "_dta_flat", None)

@@ -189,6 +189,16 @@ class RcclComm(Communicator):
             self._comm = C.RcclComm(uid, world_size, rank, device.index if device.index is not None else 0)
         # dedicated high-priority stream for collectives (lower number = higher priority)
         self.stream = torch.cuda.Stream(device=device, priority=stream_priority)
+        # one-shot xGMI all-reduce for small fp32 buckets (intra-node, self-tested)
+        self._p2p = None
+        if world_size > 1 and store is not None:
+            from .p2p import maybe_create
+
+            def _min(t):
+                self._comm.all_reduce(t, "min", int(torch.cuda.current_stream(device).cuda_stream))
+                torch.cuda.current_stream(device).synchronize()
+
+            self._p2p = maybe_create(rank, world_size, device, store, _min, tag=tag)
 
     def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor]) -> Optional[CommWork]:
         cur = torch.cuda.current_stream(self.device)
@@ -208,6 +218,10 @@ class RcclComm(Communicator):
         return True
 
     def all_reduce(self, t, op="sum", async_op=False):
+        if self._p2p_ok(t, op):
+            sc = 1.0 / self.world_size if op == "avg" else 1.0
+            h, it = self._p2p._h, self._p2p.timeout_iters
+            return self._enqueue(lambda s: h.all_reduce(t, sc, it, s), async_op, [t])
         return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t])
 
     def all_gather_into(self, out, inp, async_op=False):
@@ -226,11 +240,25 @@ class RcclComm(Communicator):
     def all_to_all_single(self, out, inp):
         self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp])
 
+    def _p2p_ok(self, t: torch.Tensor, op: str) -> bool:
+        return self._p2p is not None and op in ("sum", "avg") and self._p2p.supports(t)
+
     def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
         """Enqueue on ``stream`` (default: current) with no stream hop: used
         inside hipGraph-captured step programs."""
         s = stream or torch.cuda.current_stream(self.device)
+        if self._p2p_ok(t, op):
+            self._p2p.all_reduce(t, 1.0 / self.world_size if op == "avg" else 1.0, stream=s)
+            return
         self._comm.all_reduce(t, op, int(s.cuda_stream))
+
+    @property
+    def p2p_enabled(self) -> bool:
+        return self._p2p is not None
+
+    def check_errors(self) -> None:
+        if self._p2p is not None:
+            self._p2p.check()
 
     def barrier(self):
         x = torch.zeros(1, device=self.device)
