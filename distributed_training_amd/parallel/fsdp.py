@@ -246,11 +246,16 @@ class FullyShardedDataParallel(nn.Module):
                 u.shard_param = sp
                 shard_params.append(sp)
                 names.append(f"unit{u.index}")
-                for mod, attr, name, _ in u.entries:  # remove the original parameters from the module tree
+                del full
+                for mod, attr, name, p in u.entries:  # remove the original parameters from the module tree
                     for m2, a2, _ in self._aliases.get(name, [(mod, attr, name)]):
                         if a2 in m2._parameters:
                             del m2._parameters[a2]
                         setattr(m2, a2, torch.empty(0, dtype=param_dtype, device=self.device))
+                    # release the original storage even if the caller still holds the Parameter
+                    # (e.g. an optimizer built before wrapping): 8B params = 32 GB of fp32
+                    p.data = torch.empty(0, dtype=p.dtype, device=p.device)
+                u.entries = [(m, a, n, None) for m, a, n, _ in u.entries]
         self.shards = FlatParamGroup(shard_params, self.device, param_dtype=param_dtype, names=names)
         self.shard_params = nn.ParameterList(shard_params)
         if sync_module_states and self.world_size > 1:
