@@ -48,6 +48,7 @@ int dta_p2p_num_wg(int64_t);
 hipError_t dta_p2p_allreduce(void*, float*, int64_t, float, int, hipStream_t);
 hipError_t dta_p2p_error(void*, int*);
 void dta_p2p_destroy(void*);
+void dta_p2p_set_ll(void*, int);
 
 namespace {
 
@@ -607,6 +608,7 @@ class PyP2PAllReduce {
     state_ = nullptr;
   }
   int64_t max_elems() const { return max_elems_; }
+  void set_ll(bool ll) { dta_p2p_set_ll(state_, ll ? 1 : 0); }
 
  private:
   void* state_ = nullptr;
@@ -658,6 +660,7 @@ PYBIND11_MODULE(_C, m) {
       .def("all_reduce", &PyP2PAllReduce::all_reduce)
       .def("error", &PyP2PAllReduce::error)
       .def("destroy", &PyP2PAllReduce::destroy)
+      .def("set_ll", &PyP2PAllReduce::set_ll)
       .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())

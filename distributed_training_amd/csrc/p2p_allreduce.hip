@@ -10,7 +10,8 @@
 // results.  One kernel launch, graph-capturable, no host involvement.
 //
 // Protocol (per workgroup w, which owns one contiguous chunk of the bucket):
-//   epoch e = ++epoch_ctr[w] (device counter: hipGraph replays advance it);
+//   epoch e = ++epoch_ctr (device counter, one value per call for all
+//   workgroups: hipGraph replays advance it);
 //   parity p = e & 1 selects one of two slot sets, so a slot is only rewritten
 //   two epochs later, after every peer has signalled epoch e+1 -- which it does
 //   only after it finished reading epoch e.
@@ -20,6 +21,13 @@
 //             on timeout an error flag is raised and the kernel exits, so a
 //             dead peer can never hang the GPU)
 //   reduce  : data[chunk] = scale * sum_q (q == rank ? data : slot[p][q])
+// LL mode (default): every element travels as one 8-byte store {f32 bits,
+// epoch} into the peer's slot, so no release fence, no flag and no extra
+// round trip are needed: the receiver polls each element until its tag equals
+// the epoch (slot reuse is safe by the same two-epoch argument: a rank only
+// starts epoch e+2 after receiving every peer's epoch e+1 data, which each
+// peer sends only after it finished reading epoch e).  Twice the bytes on the
+// link, which is free at the bucket sizes this path is used for.
 // The shared buffer is allocated uncached (hipDeviceMallocUncached, as RCCL's
 // low-latency buffers are) so remote writes are never hidden behind stale L2
 // lines, and exported with hipIpcGetMemHandle (dmabuf IPC).
@@ -47,7 +55,63 @@ struct P2PArgs {
   int* epoch_ctr;                   // [kP2PMaxWG], local, not shared
   int* err;
   int timeout_iters;
+  uint64_t* peer_ll[kP2PMaxRanks];  // LL slots [2][world][max_elems] of {f32, epoch}
+  const uint64_t* local_ll;
 };
+
+// The epoch is global per call: every workgroup slot counter advances together
+// (workgroup 0 also advances the counters of workgroups this launch did not
+// use), so element i alternates parity on every call even when consecutive
+// calls split the buffer into different chunks -- otherwise a slot could be
+// rewritten while a peer still reads it, or carry a stale tag that matches.
+__device__ __forceinline__ void advance_epochs(const P2PArgs& a, int epoch) {
+  if (threadIdx.x == 0) a.epoch_ctr[blockIdx.x] = epoch;
+  if (blockIdx.x == 0)
+    for (int x = gridDim.x + threadIdx.x; x < kP2PMaxWG; x += blockDim.x) a.epoch_ctr[x] = epoch;
+}
+
+__global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_ll_kernel(P2PArgs a) {
+  const int w = blockIdx.x, tid = threadIdx.x;
+  const int64_t c0 = (int64_t)w * a.chunk;
+  const int64_t c1 = min(c0 + a.chunk, a.n);
+  const unsigned epoch = (unsigned)a.epoch_ctr[w] + 1u;
+  const int par = epoch & 1;
+  const int W = a.world;
+  // push: {value, epoch} into slot [par][rank] of every peer
+  for (int64_t i = c0 + tid; i < c1; i += kP2PThreads) {
+    const uint64_t v = (uint64_t)__float_as_uint(a.data[i]) | ((uint64_t)epoch << 32);
+    for (int q = 0; q < W; ++q) {
+      if (q == a.rank) continue;
+      __hip_atomic_store(a.peer_ll[q] + ((int64_t)par * W + a.rank) * a.max_elems + i, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // receive + reduce in rank order
+  for (int64_t i = c0 + tid; i < c1; i += kP2PThreads) {
+    float acc = 0.f;
+    for (int q = 0; q < W; ++q) {
+      if (q == a.rank) {
+        acc += a.data[i];
+        continue;
+      }
+      const uint64_t* src = a.local_ll + ((int64_t)par * W + q) * a.max_elems + i;
+      uint64_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      int it = 0;
+      while ((unsigned)(v >> 32) != epoch) {
+        if (++it > a.timeout_iters) {
+          atomicOr(a.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      acc += __uint_as_float((unsigned)(v & 0xffffffffu));
+    }
+    a.data[i] = acc * a.scale;
+  }
+  __syncthreads();
+  advance_epochs(a, (int)epoch);
+}
 
 __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_kernel(P2PArgs a) {
   const int w = blockIdx.x, tid = threadIdx.x;
@@ -112,14 +176,15 @@ __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_kernel(P2PArgs a) {
         acc += q == a.rank ? a.data[i] : a.local_data[((int64_t)par * W + q) * a.max_elems + i];
       a.data[i] = acc * a.scale;
     }
-  if (tid == 0) a.epoch_ctr[w] = epoch;
+  advance_epochs(a, epoch);
 }
 
 struct P2PState {
   int rank = 0, world = 1;
   int64_t max_elems = 0;
-  char* buf = nullptr;  // shared: slots [2][world][max_elems] f32, then flags [2][kP2PMaxWG][world] i32
-  size_t flags_off = 0, bytes = 0;
+  char* buf = nullptr;  // shared: slots [2][world][max_elems] f32, flags [2][kP2PMaxWG][world] i32, LL slots
+  size_t flags_off = 0, ll_off = 0, bytes = 0;
+  int ll = 1;
   int* epoch = nullptr;
   int* err = nullptr;
   char* peers[kP2PMaxRanks] = {};
@@ -138,7 +203,8 @@ hipError_t dta_p2p_create(int rank, int world, int64_t max_elems, void** state_o
   s->world = world;
   s->max_elems = (max_elems + 3) / 4 * 4;
   s->flags_off = ((size_t)2 * world * s->max_elems * sizeof(float) + 4095) / 4096 * 4096;
-  s->bytes = s->flags_off + (size_t)2 * kP2PMaxWG * world * sizeof(int);
+  s->ll_off = (s->flags_off + (size_t)2 * kP2PMaxWG * world * sizeof(int) + 4095) / 4096 * 4096;
+  s->bytes = s->ll_off + (size_t)2 * world * s->max_elems * sizeof(uint64_t);
   hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&s->buf), s->bytes, hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(s->buf, 0, s->bytes);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->epoch), kP2PMaxWG * sizeof(int) + 64);
@@ -184,6 +250,8 @@ int dta_p2p_num_wg(int64_t n) {
   return (int)(g < 1 ? 1 : (g > kP2PMaxWG ? kP2PMaxWG : g));
 }
 
+void dta_p2p_set_ll(void* state, int ll) { static_cast<P2PState*>(state)->ll = ll; }
+
 hipError_t dta_p2p_allreduce(void* state, float* data, int64_t n, float scale, int timeout_iters, hipStream_t st) {
   auto* s = static_cast<P2PState*>(state);
   if (!s->opened || n <= 0 || n > s->max_elems || (reinterpret_cast<uintptr_t>(data) & 15)) return hipErrorInvalidValue;
@@ -199,14 +267,17 @@ hipError_t dta_p2p_allreduce(void* state, float* data, int64_t n, float scale, i
   for (int q = 0; q < s->world; ++q) {
     a.peer_data[q] = reinterpret_cast<float*>(s->peers[q]);
     a.peer_flags[q] = reinterpret_cast<int*>(s->peers[q] + s->flags_off);
+    a.peer_ll[q] = reinterpret_cast<uint64_t*>(s->peers[q] + s->ll_off);
   }
+  a.local_ll = reinterpret_cast<const uint64_t*>(s->buf + s->ll_off);
   a.local_flags = reinterpret_cast<int*>(s->buf + s->flags_off);
   a.local_data = reinterpret_cast<const float*>(s->buf);
   a.epoch_ctr = s->epoch;
   a.err = s->err;
   a.timeout_iters = timeout_iters;
   const int grid = (int)((n + a.chunk - 1) / a.chunk);
-  hipLaunchKernelGGL(p2p_allreduce_kernel, dim3(grid), dim3(kP2PThreads), 0, st, a);
+  if (s->ll) hipLaunchKernelGGL(p2p_allreduce_ll_kernel, dim3(grid), dim3(kP2PThreads), 0, st, a);
+  else hipLaunchKernelGGL(p2p_allreduce_kernel, dim3(grid), dim3(kP2PThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -27,7 +27,8 @@ class P2PAllReduce:
     no rank is left waiting on a key that never appears."""
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store, tag: str = "default",
-                 max_elems: int = DEFAULT_MAX_ELEMS, timeout_iters: int = DEFAULT_TIMEOUT_ITERS):
+                 max_elems: int = DEFAULT_MAX_ELEMS, timeout_iters: int = DEFAULT_TIMEOUT_ITERS,
+                 protocol: str = "ll"):
         from ..ops import native
 
         self.rank, self.world_size, self.device = rank, world_size, device
@@ -51,6 +52,10 @@ class P2PAllReduce:
         self.max_elems = self._h.max_elems
         with torch.cuda.device(device):
             self._h.open(handles)
+        if protocol not in ("ll", "flag"):
+            raise ValueError(f"unknown p2p protocol {protocol!r}")
+        self.protocol = protocol
+        self._h.set_ll(protocol == "ll")  # identical on every rank (same argument everywhere)
 
     def supports(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and 0 < t.numel() <= self.max_elems
@@ -84,7 +89,8 @@ def maybe_create(rank: int, world_size: int, device: torch.device, store, verify
     ok = 1.0
     p2p = None
     try:
-        p2p = P2PAllReduce(rank, world_size, device, store, tag=tag)
+        p2p = P2PAllReduce(rank, world_size, device, store, tag=tag,
+                           protocol=os.environ.get("DTA_P2P_PROTOCOL", "ll"))
         for n in (5, 4099, 70001):  # scalar tail, 1 and many workgroups
             x = torch.arange(n, device=device, dtype=torch.float32) * (rank + 1)
             p2p.all_reduce(x, 1.0)

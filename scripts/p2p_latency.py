@@ -18,13 +18,13 @@ import torch.multiprocessing as mp
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-def worker(rank, ws, port, elems, reps, q):
+def worker(rank, ws, port, elems, reps, q, protocol):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from distributed_training_amd.parallel.p2p import P2PAllReduce
 
     torch.cuda.set_device(0)
-    p2p = P2PAllReduce(rank, ws, torch.device("cuda", 0), dist.distributed_c10d._get_default_store(), tag="lat")
+    p2p = P2PAllReduce(rank, ws, torch.device("cuda", 0), dist.distributed_c10d._get_default_store(), tag="lat", protocol=protocol)
     x = torch.ones(elems, device="cuda")
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--procs", type=int, default=2)
     ap.add_argument("--elems", type=int, default=11280)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--protocol", default="ll")
     a = ap.parse_args()
     import socket
 
@@ -65,13 +66,13 @@ def main():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    ps = [ctx.Process(target=worker, args=(r, a.procs, port, a.elems, a.reps, q)) for r in range(a.procs)]
+    ps = [ctx.Process(target=worker, args=(r, a.procs, port, a.elems, a.reps, q, a.protocol)) for r in range(a.procs)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(300)
     us = q.get() if not q.empty() else None
-    print(json.dumps({"procs": a.procs, "elems": a.elems, "us_per_allreduce": us}))
+    print(json.dumps({"procs": a.procs, "elems": a.elems, "protocol": a.protocol, "us_per_allreduce": us}))
 
 
 if __name__ == "__main__":

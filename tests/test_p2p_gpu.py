@@ -31,10 +31,10 @@ def _expected(xs_local, ws):
     return acc
 
 
-def _worker(rank, ws):
+def _worker(rank, ws, protocol):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    p2p = _make(rank, ws, "t1")
+    p2p = _make(rank, ws, "t1", protocol=protocol)
     g = torch.Generator(device="cpu").manual_seed(10 + rank)
     # sizes: scalar tail, one workgroup, several, many (64 WG cap), slot capacity
     for n in (1, 5, 2048, 4099, 11280, 70001, 262144):
@@ -80,11 +80,11 @@ def _worker(rank, ws):
     p2p.destroy()
 
 
-def _timeout_worker(rank, ws):
+def _timeout_worker(rank, ws, protocol):
     import torch.distributed as dist
 
     torch.cuda.set_device(0)
-    p2p = _make(rank, ws, "t2", timeout_iters=1 << 12)
+    p2p = _make(rank, ws, "t2", timeout_iters=1 << 12, protocol=protocol)
     x = torch.ones(1000, device="cuda")
     if rank == 0:  # the peer never joins: the kernel must give up and flag the error
         p2p.all_reduce(x, 1.0)
@@ -95,13 +95,16 @@ def _timeout_worker(rank, ws):
     p2p.destroy()
 
 
-def test_p2p_allreduce_two_processes_one_gpu():
-    run_gloo(_worker, 2)
+@pytest.mark.parametrize("protocol", ["ll", "flag"])
+def test_p2p_allreduce_two_processes_one_gpu(protocol):
+    run_gloo(_worker, 2, protocol)
 
 
-def test_p2p_allreduce_four_processes_one_gpu():
-    run_gloo(_worker, 4)
+@pytest.mark.parametrize("protocol", ["ll", "flag"])
+def test_p2p_allreduce_four_processes_one_gpu(protocol):
+    run_gloo(_worker, 4, protocol)
 
 
-def test_p2p_allreduce_timeout_flags_error():
-    run_gloo(_timeout_worker, 2)
+@pytest.mark.parametrize("protocol", ["ll", "flag"])
+def test_p2p_allreduce_timeout_flags_error(protocol):
+    run_gloo(_timeout_worker, 2, protocol)
