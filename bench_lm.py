@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--layers", type=int, default=0, help="override n_layer (0 = config)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--tunableop", action="store_true",
+                    help="let PyTorch's TunableOp pick the hipBLASLt/rocBLAS solution per GEMM shape (tuned in warmup)")
     return ap.parse_args()
 
 
@@ -64,6 +66,10 @@ def model_cfg(name, layers):
 
 def main():
     args = parse()
+    if args.tunableop:
+        os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
+        os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "1")
+        os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", f"/tmp/tunableop_{args.model}_%d.csv")
     import torch
     import torch.distributed as dist
 
@@ -148,9 +154,11 @@ def main():
         if args.impl == "torch" and args.strategy == "ddp":
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 logits = wrapped(xb[:, :-1])
-        else:
-            logits = wrapped(xb[:, :-1])
-        loss = loss_fn(logits, xb[:, 1:])
+            loss = loss_fn(logits, xb[:, 1:])
+        elif args.impl == "torch":
+            loss = loss_fn(wrapped(xb[:, :-1]), xb[:, 1:])
+        else:  # LM head + loss fused inside the model
+            loss = wrapped(xb[:, :-1], xb[:, 1:])
         loss.backward()
         opt.step()
         state["loss"] = loss
@@ -184,7 +192,7 @@ def main():
            "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
            "final_loss": float(state["loss"].item()),
            "config": {"model": args.model, "layers": cfg.n_layer, "global_batch": args.batch * ws,
-                      "seq_len": args.seq, "parallelism": f"{args.strategy}{ws}", "impl": args.impl,
+                      "seq_len": args.seq, "parallelism": f"{args.strategy}{ws}", "impl": args.impl, "tunableop": args.tunableop,
                       "activation_checkpointing": args.ckpt}}
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -208,9 +216,33 @@ def _patch_torch_ops():
         return F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale,
                                               enable_gqa=H != Hkv).transpose(1, 2)
 
+    def attention_packed(qkv, n_head, n_kv_head, causal=True, scale=None, rope=None):
+        q, k, v = lm._split_qkv(qkv, n_head, n_kv_head)
+        if rope is not None:
+            q, k = lm.rope_reference(q, *rope), lm.rope_reference(k, *rope)
+        return attention(q, k, v, causal, scale)
+
+    def add_ln(x, res, w, b, eps=1e-5):
+        xn = x + res
+        return xn, F.layer_norm(xn, (xn.shape[-1],), w, b, eps)
+
+    def add_rms(x, res, w, eps=1e-5):
+        xn = x + res
+        return xn, F.rms_norm(xn, (xn.shape[-1],), w, eps)
+
+    def linear_ce(x, w, target, ignore_index=-100):
+        logits = F.linear(x, w)
+        return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1),
+                               ignore_index=ignore_index)
+
     lm.attention = attention
+    lm.attention_packed = attention_packed
     lm.layer_norm = lambda x, w, b, eps=1e-5: F.layer_norm(x, (x.shape[-1],), w, b, eps)
     lm.rms_norm = lambda x, w, eps=1e-5: F.rms_norm(x, (x.shape[-1],), w, eps)
+    lm.add_layer_norm = add_ln
+    lm.add_rms_norm = add_rms
+    lm.linear = F.linear
+    lm.linear_cross_entropy = linear_ce
     lm.gelu = lambda x: F.gelu(x, approximate="tanh")
     lm.swiglu = lambda ab: F.silu(ab.chunk(2, -1)[0]) * ab.chunk(2, -1)[1]
     lm.apply_rope = lm.rope_reference

@@ -17,9 +17,10 @@
 #include "attention.h"
 hipError_t dta_attn_fwd(const dta::AttnArgs*, int, bool, hipStream_t);
 hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, float*, float*, int64_t, int, float,
-                        hipStream_t);
+                        const void*, void*, hipStream_t);
 hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
-                        void*, void*, int64_t, int, int, int, hipStream_t);
+                        void*, void*, int64_t, int, int, int, const void*, hipStream_t);
+hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
 hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
@@ -333,8 +334,11 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
   return {o, lse};
 }
 
+// dq / dk / dv may be given (e.g. views of one packed dQKV buffer, any token stride); else allocated
 std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
-                                    torch::Tensor o, torch::Tensor lse, bool causal, double scale, int64_t stream) {
+                                    torch::Tensor o, torch::Tensor lse, bool causal, double scale, int64_t stream,
+                                    c10::optional<torch::Tensor> dq_out, c10::optional<torch::Tensor> dk_out,
+                                    c10::optional<torch::Tensor> dv_out) {
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
   TORCH_CHECK(Hkv >= 1 && H % Hkv == 0, "attention: H must be a multiple of Hkv");
@@ -346,9 +350,12 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::
   TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.is_contiguous() && lse.numel() == B * H * S,
               "lse must be f32 [B, H, S]");
   auto delta = torch::empty({B, H, S}, lse.options());
-  auto dq = torch::empty({B, S, H, D}, q.options());
-  auto dk = torch::empty({B, S, Hkv, D}, q.options());
-  auto dv = torch::empty({B, S, Hkv, D}, q.options());
+  auto dq = dq_out && dq_out->defined() ? *dq_out : torch::empty({B, S, H, D}, q.options());
+  auto dk = dk_out && dk_out->defined() ? *dk_out : torch::empty({B, S, Hkv, D}, q.options());
+  auto dv = dv_out && dv_out->defined() ? *dv_out : torch::empty({B, S, Hkv, D}, q.options());
+  check_bshd(dq, "dq", B, S, H, D);
+  check_bshd(dk, "dk", B, S, Hkv, D);
+  check_bshd(dv, "dv", B, S, Hkv, D);
   dta::AttnArgs a{};
   a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr(); a.o = o.data_ptr(); a.lse = lse.data_ptr<float>();
   a.dout = dout.data_ptr(); a.delta = delta.data_ptr<float>(); a.dq = dq.data_ptr();
@@ -370,9 +377,10 @@ void check_bf16_2d(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
-// returns (y, mean, rstd); mean is empty for RMSNorm
+// returns (y, mean, rstd, x_new); mean is empty for RMSNorm.  With `res`: x_new = x + res is
+// normalised (fused residual add) and returned; otherwise x_new is empty.
 std::vector<torch::Tensor> norm_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool rms,
-                                    double eps, int64_t stream) {
+                                    double eps, int64_t stream, c10::optional<torch::Tensor> res) {
   check_bf16_2d(x, "x");
   check_bf16_2d(w, "weight");
   const int64_t C = x.size(-1), N = x.numel() / C;
@@ -382,25 +390,37 @@ std::vector<torch::Tensor> norm_fwd(torch::Tensor x, torch::Tensor w, c10::optio
     check_bf16_2d(*b, "bias");
     TORCH_CHECK(b->numel() == C, "bias [C]");
   }
+  const bool has_res = res && res->defined();
+  if (has_res) {
+    check_bf16_2d(*res, "res");
+    TORCH_CHECK(res->numel() == x.numel(), "norm: residual shape mismatch");
+  }
   auto y = torch::empty_like(x);
+  auto xsum = has_res ? torch::empty_like(x) : torch::empty({0}, x.options());
   auto rstd = torch::empty({N}, x.options().dtype(torch::kFloat32));
   auto mean = rms ? torch::empty({0}, rstd.options()) : torch::empty({N}, rstd.options());
   hip_ok(dta_norm_fwd(rms, x.data_ptr(), w.data_ptr(), rms ? nullptr : b->data_ptr(), y.data_ptr(),
                       rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)C, (float)eps,
-                      pick_stream(stream)),
+                      has_res ? res->data_ptr() : nullptr, has_res ? xsum.data_ptr() : nullptr, pick_stream(stream)),
          "norm_fwd");
-  return {y, mean, rstd};
+  return {y, mean, rstd, xsum};
 }
 
 // returns (dx, dw, db); dw/db dtype follow the weight
+// dres: gradient arriving on the residual stream, added into dx in the same pass
 std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
-                                    torch::Tensor rstd, bool rms, int64_t stream) {
+                                    torch::Tensor rstd, bool rms, int64_t stream, c10::optional<torch::Tensor> dres) {
   check_bf16_2d(dy, "dy");
   check_bf16_2d(x, "x");
   check_bf16_2d(w, "weight");
   const int64_t C = x.size(-1), N = x.numel() / C;
   TORCH_CHECK(dy.numel() == x.numel() && w.numel() == C, "norm_bwd: shape mismatch");
   TORCH_CHECK(rstd.numel() == N && (rms || mean.numel() == N), "norm_bwd: stats shape");
+  const bool has_dres = dres && dres->defined();
+  if (has_dres) {
+    check_bf16_2d(*dres, "dres");
+    TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: residual grad shape mismatch");
+  }
   // ~512 workgroups (fills 256 CUs twice), a multiple of 4 rows each (one per wave)
   const int rpb = (int)std::min<int64_t>(1024, std::max<int64_t>(4, ((N + 511) / 512 + 3) / 4 * 4));
   const int64_t nblk = (N + rpb - 1) / rpb;
@@ -413,9 +433,23 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   hip_ok(dta_norm_bwd(rms, dy.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), dx.data_ptr(), dwp.data_ptr<float>(),
                       rms ? nullptr : dbp.data_ptr<float>(), dw.data_ptr(), rms ? nullptr : db.data_ptr(), N, (int)C,
-                      rpb, 0, pick_stream(stream)),
+                      rpb, 0, has_dres ? dres->data_ptr() : nullptr, pick_stream(stream)),
          "norm_bwd");
   return {dx, dw, db};
+}
+
+// bias gradient = column sums of dy [N, C] (bf16), returned in `dtype`'s float type (bf16 or f32)
+torch::Tensor bias_grad(torch::Tensor dy, bool out_f32, int64_t stream) {
+  check_bf16_2d(dy, "dy");
+  const int64_t C = dy.size(-1), N = dy.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bias_grad: C % 8 == 0 required");
+  const int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(256, (N + 63) / 64));
+  auto part = torch::empty({nsplit, C}, dy.options().dtype(torch::kFloat32));
+  auto out = torch::empty({C}, dy.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  hip_ok(dta_bias_grad(dy.data_ptr(), N, (int)C, part.data_ptr<float>(), nsplit, out.data_ptr(), out_f32 ? 1 : 0,
+                       pick_stream(stream)),
+         "bias_grad");
+  return out;
 }
 
 torch::Tensor gelu_fwd(torch::Tensor x, int64_t stream) {
@@ -635,15 +669,20 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream") = -1, py::arg("dbg_stamps") = py::none());
   m.def("mlp2_lds_bytes", &dta_mlp2_lds_bytes);
   m.def("attn_fwd", &attn_fwd);
-  m.def("norm_fwd", &norm_fwd);
-  m.def("norm_bwd", &norm_bwd);
+  m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("rms"), py::arg("eps"),
+        py::arg("stream") = -1, py::arg("res") = py::none());
+  m.def("norm_bwd", &norm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
+        py::arg("rms"), py::arg("stream") = -1, py::arg("dres") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),
+        py::arg("dk") = py::none(), py::arg("dv") = py::none());
   m.def("rccl_load", &dta::rccl_load);
   m.def("rccl_loaded", &dta::rccl_loaded);
   m.def("rccl_unique_id", []() { return py::bytes(dta::rccl_unique_id()); });

@@ -12,10 +12,13 @@ namespace dta {
 // ---------------------------------------------------------------- norms
 // NV = vectors of 8 per lane (C = 512 * NV).  RMS: no mean, no bias.
 template <int NV, bool RMS>
+// res != nullptr: fused residual add, x_new = bf16(x + res) is written to
+// xsum and normalised (the pre-LN block's "x = x + sublayer(x); y = LN(x)").
 __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                        const bf16* __restrict__ bias, bf16* __restrict__ y,
                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                       int64_t N, int C, float eps) {
+                                                       int64_t N, int C, float eps, const bf16* __restrict__ res,
+                                                       bf16* __restrict__ xsum) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= N) return;
@@ -25,10 +28,23 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 8;
-    if (c < C) load8(xr + c, v[i]);
-    else
+    if (c < C) {
+      load8(xr + c, v[i]);
+      if (res) {
+        float r[8];
+        load8(res + row * C + c, r);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = f2bf(v[i][j] + r[j]);
+          v[i][j] = bf2f(o[j]);  // normalise exactly the bf16 value that is stored
+        }
+        *reinterpret_cast<bf16x8*>(xsum + row * C + c) = o;
+      }
+    } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += v[i][j];
   }
@@ -71,7 +87,8 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
                                                        const bf16* __restrict__ w, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, bf16* __restrict__ dx,
                                                        float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                       int64_t N, int C, int rows_per_block) {
+                                                       int64_t N, int C, int rows_per_block,
+                                                       const bf16* __restrict__ dres) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float dwacc[NV][8], dbacc[NV][8];
 #pragma unroll
@@ -112,6 +129,12 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - m1 - xh[i][j] * m2);
+        if (dres) {  // gradient arriving on the residual stream (fused accumulate)
+          float r[8];
+          load8(dres + row * C + c, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
         store8(dx + row * C + c, o);
       }
     }
@@ -165,6 +188,35 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
     for (int g = 0; g < 8; ++g) t += red[g][cl];
     if (out_bf16) out_bf16[c] = f2bf(t);
     if (out_f32) out_f32[c] = t;
+  }
+}
+
+// Partial column sums of a bf16 [N, C] matrix (bias gradients): a workgroup
+// is 64 column lanes (8 columns each, 16-byte loads) x 4 row lanes over one
+// row split; the [nsplit, C] fp32 partials are finished by colsum_kernel.
+__global__ void __launch_bounds__(256) colsum_bf16_partial_kernel(const bf16* __restrict__ x, int64_t N, int C,
+                                                                   int rows_per_split, float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + cl) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t r1 = min(r0 + rows_per_split, N);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+#pragma unroll 4
+    for (int64_t r = r0 + rl; r < r1; r += 4) {
+      float v[8];
+      load8(x + r * C + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cl * 8 + j] = acc[j];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 512; e += 256) {
+    const int cc = blockIdx.x * 512 + e;
+    if (cc < C) part[(int64_t)blockIdx.y * C + cc] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
   }
 }
 
@@ -361,14 +413,14 @@ using namespace dta;
 
 template <bool RMS>
 static hipError_t norm_fwd_nv(int nv, const bf16* x, const bf16* w, const bf16* b, bf16* y, float* mean, float* rstd,
-                              int64_t N, int C, float eps, hipStream_t st) {
+                              int64_t N, int C, float eps, const bf16* res, bf16* xsum, hipStream_t st) {
   dim3 grid((unsigned)((N + 3) / 4)), blk(256);
   switch (nv) {
-    case 1: hipLaunchKernelGGL((norm_fwd_kernel<1, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
-    case 2: hipLaunchKernelGGL((norm_fwd_kernel<2, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
-    case 4: hipLaunchKernelGGL((norm_fwd_kernel<4, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
-    case 8: hipLaunchKernelGGL((norm_fwd_kernel<8, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
-    case 16: hipLaunchKernelGGL((norm_fwd_kernel<16, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps); break;
+    case 1: hipLaunchKernelGGL((norm_fwd_kernel<1, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps, res, xsum); break;
+    case 2: hipLaunchKernelGGL((norm_fwd_kernel<2, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps, res, xsum); break;
+    case 4: hipLaunchKernelGGL((norm_fwd_kernel<4, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps, res, xsum); break;
+    case 8: hipLaunchKernelGGL((norm_fwd_kernel<8, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps, res, xsum); break;
+    case 16: hipLaunchKernelGGL((norm_fwd_kernel<16, RMS>), grid, blk, 0, st, x, w, b, y, mean, rstd, N, C, eps, res, xsum); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -385,23 +437,26 @@ static int nv_for(int C) {
 }
 
 hipError_t dta_norm_fwd(bool rms, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                        int64_t N, int C, float eps, hipStream_t st) {
+                        int64_t N, int C, float eps, const void* res, void* xsum, hipStream_t st) {
   const int nv = nv_for(C);
   if (nv < 0 || C % 8) return hipErrorInvalidValue;
   auto X = reinterpret_cast<const bf16*>(x);
   auto W = reinterpret_cast<const bf16*>(w);
   auto Bv = reinterpret_cast<const bf16*>(b);
   auto Y = reinterpret_cast<bf16*>(y);
-  return rms ? norm_fwd_nv<true>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, st)
-             : norm_fwd_nv<false>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, st);
+  auto R = reinterpret_cast<const bf16*>(res);
+  auto XS = reinterpret_cast<bf16*>(xsum);
+  return rms ? norm_fwd_nv<true>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, R, XS, st)
+             : norm_fwd_nv<false>(nv, X, W, Bv, Y, mean, rstd, N, C, eps, R, XS, st);
 }
 
 template <bool RMS>
 static hipError_t norm_bwd_nv(int nv, const bf16* dy, const bf16* x, const bf16* w, const float* mean,
                               const float* rstd, bf16* dx, float* dwp, float* dbp, int64_t N, int C, int rpb,
-                              hipStream_t st) {
+                              const bf16* dres, hipStream_t st) {
   dim3 grid((unsigned)((N + rpb - 1) / rpb)), blk(256);
-#define NB(V) hipLaunchKernelGGL((norm_bwd_kernel<V, RMS>), grid, blk, 0, st, dy, x, w, mean, rstd, dx, dwp, dbp, N, C, rpb)
+#define NB(V) \
+  hipLaunchKernelGGL((norm_bwd_kernel<V, RMS>), grid, blk, 0, st, dy, x, w, mean, rstd, dx, dwp, dbp, N, C, rpb, dres)
   switch (nv) {
     case 1: NB(1); break;
     case 2: NB(2); break;
@@ -417,13 +472,13 @@ static hipError_t norm_bwd_nv(int nv, const bf16* dy, const bf16* x, const bf16*
 // dw/db partial workspace: [nblk][C] fp32 each, nblk = ceil(N / rows_per_block)
 hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                         void* dx, float* dw_part, float* db_part, void* dw, void* db, int64_t N, int C,
-                        int rows_per_block, int grads_f32, hipStream_t st) {
+                        int rows_per_block, int grads_f32, const void* dres, hipStream_t st) {
   const int nv = nv_for(C);
   if (nv < 0 || C % 8) return hipErrorInvalidValue;
   auto r = rms ? norm_bwd_nv<true>(nv, (const bf16*)dy, (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx,
-                                   dw_part, db_part, N, C, rows_per_block, st)
+                                   dw_part, db_part, N, C, rows_per_block, (const bf16*)dres, st)
                : norm_bwd_nv<false>(nv, (const bf16*)dy, (const bf16*)x, (const bf16*)w, mean, rstd, (bf16*)dx,
-                                    dw_part, db_part, N, C, rows_per_block, st);
+                                    dw_part, db_part, N, C, rows_per_block, (const bf16*)dres, st);
   if (r != hipSuccess) return r;
   const int nblk = (int)((N + rows_per_block - 1) / rows_per_block);
   dim3 g((C + 31) / 32);
@@ -432,6 +487,17 @@ hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, 
   if (!rms)
     hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, db_part, nblk, C, grads_f32 ? nullptr : (bf16*)db,
                        grads_f32 ? (float*)db : nullptr);
+  return hipGetLastError();
+}
+
+hipError_t dta_bias_grad(const void* dy, int64_t N, int C, float* part, int nsplit, void* out, int out_f32,
+                         hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const int rps = (int)((N + nsplit - 1) / nsplit);
+  hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3((C + 511) / 512, nsplit), dim3(256), 0, st, (const bf16*)dy, N,
+                     C, rps, part);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, nsplit, C,
+                     out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr);
   return hipGetLastError();
 }
 

@@ -175,8 +175,11 @@ class Trainer:
     # ------------------------------------------------------------------ loop
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         self.optimizer.zero_grad()
-        output = self.model(source)
-        loss = self._loss_fn(output, targets)
+        if self.config.loss == "lm":  # transformer LMs fuse the head and the loss (models/gpt2.py, llama.py)
+            loss = self.model(source, targets)
+        else:
+            output = self.model(source)
+            loss = self._loss_fn(output, targets)
         loss.backward()
         if self.config.grad_clip:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.grad_clip)

@@ -54,28 +54,32 @@ class LayerNorm(nn.Module):
     def forward(self, x):
         return lm.layer_norm(x, self.weight, self.bias, self.eps)
 
+    def add_forward(self, x, res):
+        """``(x + res, LN(x + res))`` in one kernel; ``res=None`` -> ``(x, LN(x))``."""
+        if res is None:
+            return x, self(x)
+        return lm.add_layer_norm(x, res, self.weight, self.bias, self.eps)
+
 
 class CausalSelfAttention(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
         self.n_head = cfg.n_head
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.c_attn = lm.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = lm.Linear(cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         B, S, C = x.shape
-        H = self.n_head
-        qkv = self.c_attn(x).view(B, S, 3, H, C // H)
-        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]  # strided views, read in place by the kernel
-        y = lm.attention(q, k, v, causal=True)
+        # q/k/v are read in place from the projection output; dq/dk/dv land in one packed buffer
+        y = lm.attention_packed(self.c_attn(x), self.n_head, self.n_head, causal=True)
         return self.c_proj(y.reshape(B, S, C))
 
 
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.c_fc = lm.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         return self.c_proj(lm.gelu(self.c_fc(x)))
@@ -89,9 +93,14 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd)
         self.mlp = MLP(cfg)
 
-    def forward(self, x):
-        x = x + self.attn(self.ln_1(x))
-        return x + self.mlp(self.ln_2(x))
+    def forward(self, x, h=None):
+        """``h``: the previous block's MLP output, not yet added to the
+        residual stream -- the add is fused into this block's ln_1 (and this
+        block's MLP output is handed on the same way), so no residual add runs
+        as a separate kernel, forward or backward.  Returns ``(x, h)``."""
+        x, y = self.ln_1.add_forward(x, h)
+        x, y = self.ln_2.add_forward(x, self.attn(y))
+        return x, self.mlp(y)
 
 
 class GPT2(nn.Module):
@@ -130,16 +139,22 @@ class GPT2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx):
+    def forward(self, idx, targets=None):
+        """Logits ``[B, S, V]``; with ``targets``, the mean token cross-entropy
+        (LM head and loss fused: the logits are never materialised twice)."""
         B, S = idx.shape
         pos = torch.arange(S, device=idx.device)
         x = self.wte(idx) + self.wpe(pos)
+        h = None
         for blk in self.h:
             if self.activation_checkpointing and torch.is_grad_enabled():
-                x = checkpoint(blk, x, use_reentrant=False)
+                x, h = checkpoint(blk, x, h, use_reentrant=False)
             else:
-                x = blk(x)
-        return self.lm_head(self.ln_f(x))
+                x, h = blk(x, h)
+        _, y = self.ln_f.add_forward(x, h)
+        if targets is not None:
+            return lm.linear_cross_entropy(y, self.lm_head.weight, targets)
+        return self.lm_head(y)
 
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (6N + attention), PaLM-style accounting."""

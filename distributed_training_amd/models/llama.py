@@ -49,6 +49,12 @@ class RMSNorm(nn.Module):
     def forward(self, x):
         return lm.rms_norm(x, self.weight, self.eps)
 
+    def add_forward(self, x, res):
+        """``(x + res, RMSNorm(x + res))`` in one kernel; ``res=None`` -> ``(x, RMSNorm(x))``."""
+        if res is None:
+            return x, self(x)
+        return lm.add_rms_norm(x, res, self.weight, self.eps)
+
 
 class Attention(nn.Module):
     def __init__(self, cfg: LlamaConfig):
@@ -60,13 +66,9 @@ class Attention(nn.Module):
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
-        H, Hkv, D = self.H, self.Hkv, self.D
-        qkv = self.wqkv(x).view(B, S, H + 2 * Hkv, D)
-        q = lm.apply_rope(qkv[:, :, :H], cos, sin)
-        k = lm.apply_rope(qkv[:, :, H:H + Hkv], cos, sin)
-        v = qkv[:, :, H + Hkv:]
-        y = lm.attention(q, k, v, causal=True)
-        return self.wo(y.reshape(B, S, H * D))
+        # RoPE + GQA attention on the packed projection output (one packed dQKV in backward)
+        y = lm.attention_packed(self.wqkv(x), self.H, self.Hkv, causal=True, rope=(cos, sin))
+        return self.wo(y.reshape(B, S, self.H * self.D))
 
 
 class FeedForward(nn.Module):
@@ -87,9 +89,11 @@ class Block(nn.Module):
         self.ffn_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
         self.feed_forward = FeedForward(cfg)
 
-    def forward(self, x, cos, sin):
-        x = x + self.attention(self.attention_norm(x), cos, sin)
-        return x + self.feed_forward(self.ffn_norm(x))
+    def forward(self, x, cos, sin, h=None):
+        """Residual adds fused into the norms (see GPT-2 ``Block``); returns ``(x, h)``."""
+        x, y = self.attention_norm.add_forward(x, h)
+        x, y = self.ffn_norm.add_forward(x, self.attention(y, cos, sin))
+        return x, self.feed_forward(y)
 
 
 class Llama(nn.Module):
@@ -121,15 +125,20 @@ class Llama(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx):
+    def forward(self, idx, targets=None):
+        """Logits; with ``targets``, the mean token cross-entropy (head + loss fused)."""
         x = self.tok_embeddings(idx)
         cos, sin = self.rope_cos, self.rope_sin
+        h = None
         for blk in self.layers:
             if self.activation_checkpointing and torch.is_grad_enabled():
-                x = checkpoint(blk, x, cos, sin, use_reentrant=False)
+                x, h = checkpoint(blk, x, cos, sin, h, use_reentrant=False)
             else:
-                x = blk(x, cos, sin)
-        return self.output(self.norm(x))
+                x, h = blk(x, cos, sin, h)
+        _, y = self.norm.add_forward(x, h)
+        if targets is not None:
+            return lm.linear_cross_entropy(y, self.output.weight, targets)
+        return self.output(y)
 
     def flops_per_token(self, seq_len: int) -> float:
         c = self.cfg

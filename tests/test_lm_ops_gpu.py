@@ -166,3 +166,111 @@ def test_llama_tiny_fsdp_trains_on_gpu():
     assert losses[-1] < losses[0] * 0.5, losses
     sd = fs.full_state_dict(rank0_only=False)
     assert "layers.0.attention.wqkv.weight" in sd and sd["output.weight"].dtype == torch.float32
+
+
+@pytest.mark.parametrize("H,Hkv,D,rope", [(4, 4, 64, False), (4, 2, 128, True), (8, 1, 64, True)])
+def test_packed_attention_with_rope(H, Hkv, D, rope):
+    """Attention on the packed QKV projection output: packed dQKV gradient, RoPE fused."""
+    torch.manual_seed(3)
+    B, S = 2, 160
+    qkv = (torch.randn(B, S, (H + 2 * Hkv) * D, device=DEV) * 0.5).bfloat16().requires_grad_()
+    cos, sin = lm.rope_tables(S, D, 10000.0, device=DEV)
+    do = torch.randn(B, S, H, D, device=DEV).bfloat16()
+    o = lm.attention_packed(qkv, H, Hkv, causal=True, rope=(cos, sin) if rope else None)
+    o.backward(do)
+    ref_in = qkv.detach().float().requires_grad_()
+    q, k, v = lm._split_qkv(ref_in, H, Hkv)
+    if rope:
+        q, k = lm.rope_reference(q, cos, sin), lm.rope_reference(k, cos, sin)
+    orf = lm.attention_reference(q.float(), k.float(), v.float(), causal=True)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    assert _rel(qkv.grad, ref_in.grad) < 2e-2
+
+
+@pytest.mark.parametrize("rms", [False, True])
+def test_add_norm_fused_residual(rms):
+    torch.manual_seed(4)
+    N, C = 300, 768
+    x = torch.randn(N, C, device=DEV).bfloat16().requires_grad_()
+    r = torch.randn(N, C, device=DEV).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    gx = torch.randn(N, C, device=DEV).bfloat16()
+    gy = torch.randn(N, C, device=DEV).bfloat16()
+    if rms:
+        xn, y = lm.add_rms_norm(x, r, w)
+    else:
+        xn, y = lm.add_layer_norm(x, r, w, b)
+    (xn.float() * gx.float()).sum().add((y.float() * gy.float()).sum()).backward()
+    xf, rf, wf, bf = (t.detach().float().requires_grad_() for t in (x, r, w, b))
+    xs = (xf + rf).bfloat16().float()  # the kernel normalises the stored bf16 sum
+    xs = xf + rf + (xs - (xf + rf)).detach()
+    if rms:
+        yr = xs * torch.rsqrt(xs.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    else:
+        yr = F.layer_norm(xs, (C,), wf, bf, 1e-5)
+    ((xf + rf) * gx.float()).sum().add((yr * gy.float()).sum()).backward()
+    assert _rel(xn, xf + rf) < 1e-2 and _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xf.grad) < 2e-2 and _rel(r.grad, rf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 2e-2
+    if not rms:
+        assert _rel(b.grad, bf.grad) < 2e-2
+
+
+def test_linear_native_bias_grad():
+    torch.manual_seed(5)
+    x = torch.randn(4, 300, 768, device=DEV).bfloat16().requires_grad_()
+    w = (0.05 * torch.randn(2304, 768, device=DEV)).bfloat16().requires_grad_()
+    b = torch.randn(2304, device=DEV).bfloat16().requires_grad_()
+    dy = torch.randn(4, 300, 2304, device=DEV).bfloat16()
+    lm.linear(x, w, b).backward(dy)
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    F.linear(xf, wf, bf).backward(dy.float())
+    assert _rel(b.grad, bf.grad) < 1e-2
+    assert _rel(w.grad, wf.grad) < 1e-2 and _rel(x.grad, xf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [50304, 1000])
+def test_linear_cross_entropy_fused_head(V):
+    torch.manual_seed(6)
+    N, C = 257, 256
+    x = (0.5 * torch.randn(N, C, device=DEV)).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[::7] = -100
+    loss = lm.linear_cross_entropy(x, w, t)
+    (loss * 3.0).backward()
+    xf, wf = (z.detach().float().requires_grad_() for z in (x, w))
+    lr = F.cross_entropy(xf @ wf.t(), t, ignore_index=-100)
+    (lr * 3.0).backward()
+    assert abs(loss.item() - lr.item()) < 2e-2 * abs(lr.item())
+    assert _rel(x.grad, xf.grad) < 3e-2 and _rel(w.grad, wf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("arch", ["gpt2", "llama"])
+def test_fused_model_matches_fp32_reference(arch):
+    """The whole fused GPU model (packed attention, fused residual norms, native
+    bias grads, fused head+CE) against the same weights run through the
+    unfused CPU fp32 path."""
+    import copy
+
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(7)
+    if arch == "gpt2":
+        m = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1000, block_size=128))
+    else:
+        m = Llama(LlamaConfig(n_layer=2, n_head=4, n_kv_head=2, n_embd=256, ffn_hidden=512, vocab_size=1000,
+                              block_size=128))
+    ref = copy.deepcopy(m).float()
+    g = m.to(DEV).bfloat16()
+    idx = torch.randint(0, 1000, (2, 97))
+    loss = g(idx[:, :-1].to(DEV), idx[:, 1:].to(DEV))
+    loss.backward()
+    lr = ref(idx[:, :-1], idx[:, 1:])
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 2e-2 * lr.item()
+    for (n, p), (_, q) in zip(g.named_parameters(), ref.named_parameters()):
+        assert _rel(p.grad, q.grad.to(DEV)) < 6e-2, n
