@@ -21,6 +21,9 @@ hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, floa
 hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
                         void*, void*, int64_t, int, int, int, const void*, hipStream_t);
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
+int dta_gemm_tn_split(int, int, int);
+hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int,
+                       hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
 hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
@@ -438,6 +441,29 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   return {dx, dw, db};
 }
 
+// C[M, N] = A^T B for A [K, M], B [K, N] bf16 row-major (the weight gradient dY^T X); split = 0: auto
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) { return dta_gemm_tn_split((int)M, (int)N, (int)K) > 0; }
+
+torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
+              "gemm_tn: bf16 GPU operands");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0), "gemm_tn: A [K, M], B [K, N]");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "gemm_tn: 16-byte aligned rows required");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  const int sp = split > 0 ? (int)split : dta_gemm_tn_split((int)M, (int)N, (int)K);
+  TORCH_CHECK(sp > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
+  auto c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  torch::Tensor slab;
+  if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
+  hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,
+                     sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, pick_stream(stream)),
+         "gemm_tn");
+  return c;
+}
+
 // bias gradient = column sums of dy [N, C] (bf16), returned in `dtype`'s float type (bf16 or f32)
 torch::Tensor bias_grad(torch::Tensor dy, bool out_f32, int64_t stream) {
   check_bf16_2d(dy, "dy");
@@ -679,6 +705,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out_f32") = false, py::arg("split") = 0,
+        py::arg("stream") = -1);
+  m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("gemm_tn_split", &dta_gemm_tn_split);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),

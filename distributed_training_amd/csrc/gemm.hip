@@ -1,0 +1,221 @@
+// Weight-gradient GEMM for gfx950:  C[M, N] = A^T . B  with A [K, M] and
+// B [K, N] both row-major (K = tokens).  This is dW = dY^T . X of every
+// Linear layer (the "dW" GEMM of §7.1 gemm.hip).
+//
+// Why a hand-written kernel: at transformer shapes the weight gradient has a
+// small output (768 x 3072 for GPT-2 small = 144 tiles of 128 x 128) and a
+// long reduction (K = B*S = 8192 tokens), so a library GEMM that tiles only the
+// output under-fills 256 CUs (measured: hipBLASLt 170-400 TF/s on these three
+// shapes, 144-216 workgroups).  Here the reduction is split over a third grid
+// dimension (split-K) so the launch has >= 256 workgroups, and the fp32 slabs
+// are summed by a small vectorised reduce kernel into the bf16 gradient.
+//
+// Both operands have the reduction index as their ROW index, so both MFMA
+// fragments are read column-wise: tiles are staged row-major in LDS (256-B rows,
+// 16-B chunks XOR-swizzled so row reads and transposed reads are bank-conflict
+// free, cdna_hip_programming.md T10 layout (b)) and fragments come from
+// ds_read_b64_tr_b16.  Workgroup = 4 waves (2 x 2), 128 x 128 output tile, each
+// wave 64 x 64 = 2 x 2 v_mfma_f32_32x32x16_bf16 tiles; BK = 64 tokens per
+// LDS stage, double-buffered, the next stage's 16-B global loads in flight in
+// registers while the current stage is multiplied (one barrier per stage).
+#include "common.h"
+
+namespace dta {
+
+constexpr int kGtBM = 128, kGtBN = 128, kGtBK = 64;
+constexpr int kGtTileBytes = kGtBK * 256;  // one [64][128] bf16 tile
+
+// byte offset of 16-byte chunk `ch` (0..15) of row `row` in a 256-B-row tile
+__device__ __forceinline__ int gt_off(int row, int ch) {
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ bf16x4 gt_tr4(const char* lds, int byte_off) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lds + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// MFMA operand fragment X^T for k-step s and 32 columns starting at c0 of the
+// [64 k][128 col] tile: lane l gets X[16s + 8(l>>5) + j][c0 + (l & 31)], j = 0..7.
+__device__ __forceinline__ bf16x8 gt_frag(const char* tile, int s, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = 16 * s + 8 * (g >> 1) + (i >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int ch = col >> 3, sub = (col & 7) * 2;
+  const bf16x4 lo = gt_tr4(tile, gt_off(row, ch) + sub);
+  const bf16x4 hi = gt_tr4(tile, gt_off(row + 4, ch) + sub);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+struct GemmTnArgs {
+  const bf16* a;  // [K, M], row stride lda
+  const bf16* b;  // [K, N], row stride ldb
+  void* c;        // split == 1: bf16/f32 [M, N]; split > 1: f32 slabs [split][M][N]
+  int64_t lda, ldb, ldc;
+  int M, N, K, split, k_per_split;
+  int tiles_m, tiles_n;
+  int out_f32;
+};
+
+template <bool SLAB>
+__global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kGtTileBytes];  // [buf][A|B][64][256 B]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // bijective XCD remap: consecutive logical tiles (same split, neighbouring
+  // output tiles -> shared A/B panels) land on the same XCD's L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int sp = wg / tiles, t = wg % tiles;
+  const int tm = t / g.tiles_n, tn = t % g.tiles_n;
+  const int m0 = tm * kGtBM, n0 = tn * kGtBN;
+  const int kbeg = sp * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int ntile = (kend - kbeg) / kGtBK;
+
+  // staging: 4 chunks of A and 4 of B per thread per stage (chunk e: row e>>4, 16-B chunk e&15)
+  bf16x8 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int e = tid + 256 * l, row = e >> 4, ch = e & 15;
+      ra[l] = *reinterpret_cast<const bf16x8*>(g.a + (int64_t)(k0 + row) * g.lda + m0 + ch * 8);
+      rb[l] = *reinterpret_cast<const bf16x8*>(g.b + (int64_t)(k0 + row) * g.ldb + n0 + ch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* ta = lds + buf * 2 * kGtTileBytes;
+    char* tb = ta + kGtTileBytes;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int e = tid + 256 * l, row = e >> 4, ch = e & 15;
+      *reinterpret_cast<bf16x8*>(ta + gt_off(row, ch)) = ra[l];
+      *reinterpret_cast<bf16x8*>(tb + gt_off(row, ch)) = rb[l];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (ntile > 0) {
+    gload(kbeg);
+    lstore(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < ntile; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntile) gload(kbeg + (kt + 1) * kGtBK);
+    const char* ta = lds + buf * 2 * kGtTileBytes;
+    const char* tb = ta + kGtTileBytes;
+#pragma unroll
+    for (int s = 0; s < kGtBK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = gt_frag(ta, s, wm * 64 + 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = gt_frag(tb, s, wn * 64 + 32 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32x32x16(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < ntile) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j] rows m = m0 + wm*64 + 32i + mfma32_row(e), cols n = n0 + wn*64 + 32j + (lane & 31)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * 64 + 32 * i + mfma32_row(e, lane);
+        if (SLAB) {
+          static_cast<float*>(g.c)[((int64_t)sp * g.M + m) * g.N + n] = acc[i][j][e];
+        } else if (g.out_f32) {
+          static_cast<float*>(g.c)[(int64_t)m * g.ldc + n] = acc[i][j][e];
+        } else {
+          static_cast<bf16*>(g.c)[(int64_t)m * g.ldc + n] = f2bf(acc[i][j][e]);
+        }
+      }
+    }
+}
+
+// out[M, N] = sum_s slab[s][M][N]   (bf16 or f32 out, 4 elements per thread)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int split, int64_t mn,
+                                                            void* out, int out_f32) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i4 * 4 >= mn) return;
+  float4 acc = reinterpret_cast<const float4*>(slab)[i4];
+  for (int s = 1; s < split; ++s) {
+    const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)s * mn)[i4];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  if (out_f32) {
+    reinterpret_cast<float4*>(out)[i4] = acc;
+  } else {
+    bf16x4 o = {f2bf(acc.x), f2bf(acc.y), f2bf(acc.z), f2bf(acc.w)};
+    reinterpret_cast<bf16x4*>(out)[i4] = o;
+  }
+}
+
+}  // namespace dta
+
+using namespace dta;
+
+// Split until the launch has >= 256 workgroups (one per CU; measured best on the
+// GPT-2 shapes), each split >= 4 stages deep.
+int dta_gemm_tn_split(int M, int N, int K) {
+  if (M % kGtBM || N % kGtBN || K % kGtBK) return 0;
+  const int tiles = (M / kGtBM) * (N / kGtBN);
+  int split = 1;
+  while (tiles * split < 256 && K / (split * 2) >= 4 * kGtBK && (K / kGtBK) % (split * 2) == 0) split *= 2;
+  return split;
+}
+
+// c: [M, N] (bf16 or f32, row stride ldc); slab: f32 [split * M * N] when split > 1
+hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int M, int N,
+                       int K, int split, float* slab, int out_f32, hipStream_t st) {
+  if (M % kGtBM || N % kGtBN || K % kGtBK || split < 1 || (K / kGtBK) % split) return hipErrorInvalidValue;
+  GemmTnArgs g{};
+  g.a = static_cast<const bf16*>(a);
+  g.b = static_cast<const bf16*>(b);
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.split = split;
+  g.k_per_split = K / split;
+  g.tiles_m = M / kGtBM;
+  g.tiles_n = N / kGtBN;
+  g.out_f32 = out_f32;
+  const int grid = g.tiles_m * g.tiles_n * split;
+  if (split == 1) {
+    g.c = c;
+    hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(grid), dim3(256), 0, st, g);
+  } else {
+    if (ldc != N) return hipErrorInvalidValue;
+    g.c = slab;
+    hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(grid), dim3(256), 0, st, g);
+    const int64_t mn = (int64_t)M * N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256)), dim3(256), 0, st, slab, split, mn,
+                       c, out_f32);
+  }
+  return hipGetLastError();
+}

@@ -207,6 +207,23 @@ def rms_norm(x, w, eps: float = 1e-5):
 
 
 # ------------------------------------------------------------------ linear
+_WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this hipBLASLt fills the chip by itself
+
+
+def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW = dy^T x.  Small outputs with a long token reduction (GPT-2: 768 x 768 ..
+    3072 x 768 over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip),
+    which fills 256 CUs where a library GEMM tiling only the output does not
+    (measured 1.4-1.8x on the attention projections); large outputs stay on
+    hipBLASLt."""
+    K, M = dy2.shape
+    N = x2.shape[1]
+    if (M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and (M // 128) * (N // 128) <= _WGRAD_NATIVE_MAX_TILES
+            and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
+        return native().gemm_tn(dy2, x2.contiguous() if x2.stride(0) % 8 else x2, False, 0, -1)
+    return torch.mm(dy2.t(), x2)
+
+
 class _Linear(Function):
     """y = x W^T + b: GEMMs on hipBLASLt, bias gradient on the native
     column-sum kernel (one 16-byte-load pass over dy)."""
@@ -227,7 +244,7 @@ class _Linear(Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w).view(*x.shape[:-1], w.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dy2.t(), x.reshape(-1, x.shape[-1]))
+            dw = _weight_grad(dy2, x.reshape(-1, x.shape[-1]))
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = native().bias_grad(dy2, False, -1)
         return dx, dw, db

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Weight-gradient GEMM (C = A^T B, K = tokens): native split-K MFMA kernel vs
+torch.mm (hipBLASLt) on the GPT-2 small / Llama-3 8B shapes."""
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from distributed_training_amd.ops import native  # noqa: E402
+
+SHAPES = [  # (K tokens, M = out features, N = in features)
+    (8192, 2304, 768), (8192, 768, 768), (8192, 3072, 768), (8192, 768, 3072),
+    (8192, 6144, 4096), (8192, 4096, 4096), (8192, 28672, 4096), (8192, 4096, 14336),
+]
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+def main():
+    C = native()
+    for K, M, N in SHAPES:
+        a = torch.randn(K, M, device="cuda").bfloat16()
+        b = torch.randn(K, N, device="cuda").bfloat16()
+        fl = 2.0 * K * M * N
+        t_ref = timeit(lambda: torch.mm(a.t(), b))
+        row = {"K": K, "M": M, "N": N, "torch_us": round(t_ref, 1), "torch_TF": round(fl / t_ref / 1e6, 1)}
+        for sp in (1, 2, 4, 8, 0):
+            if (K // 64) % max(sp, 1):
+                continue
+            t = timeit(lambda: C.gemm_tn(a, b, False, sp))
+            row[f"native_s{sp}_us"] = round(t, 1)
+        row["auto_split"] = C.gemm_tn_split(M, N, K)
+        best = min(v for k, v in row.items() if k.startswith("native_"))
+        row["native_best_TF"] = round(fl / best / 1e6, 1)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -274,3 +274,24 @@ def test_fused_model_matches_fp32_reference(arch):
     assert abs(loss.item() - lr.item()) < 2e-2 * lr.item()
     for (n, p), (_, q) in zip(g.named_parameters(), ref.named_parameters()):
         assert _rel(p.grad, q.grad.to(DEV)) < 6e-2, n
+
+
+@pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
+                                         (4096, 2304, 768, 0)])
+def test_gemm_tn_weight_gradient(K, M, N, split):
+    """C = A^T B (dW = dY^T X) on the split-K MFMA kernel vs fp32 torch."""
+    from distributed_training_amd.ops import native
+
+    torch.manual_seed(8)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    ref = a.float().t() @ b.float()
+    c = native().gemm_tn(a, b, False, split)
+    assert c.shape == (M, N) and c.dtype == torch.bfloat16
+    assert _rel(c, ref) < 1e-2
+    c32 = native().gemm_tn(a, b, True, split)
+    assert _rel(c32, ref) < 1e-3
+    # A as a row-strided view (e.g. a slice of a wider activation)
+    wide = torch.randn(K, M + 128, device=DEV).bfloat16()
+    c2 = native().gemm_tn(wide[:, 64:64 + M], b, True, split)
+    assert _rel(c2, wide[:, 64:64 + M].float().t() @ b.float()) < 1e-3
