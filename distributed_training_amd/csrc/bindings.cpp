@@ -45,6 +45,8 @@ hipError_t dta_flat_clip(float*, int64_t, const float*, float, hipStream_t);
 hipError_t dta_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 hipError_t dta_mlp2_fused_step(const dta::MlpArgs*, hipStream_t);
 size_t dta_mlp2_lds_bytes(int64_t, int, int);
+hipError_t dta_mlp_persistent(const dta::MlpPArgs*, int, hipStream_t);
+size_t dta_mlp_persistent_lds_bytes(int, int, int, int);
 hipError_t dta_p2p_create(int, int, int64_t, void**, void*);
 int dta_p2p_handle_bytes();
 hipError_t dta_p2p_open(void*, const void*);
@@ -677,6 +679,72 @@ class PyP2PAllReduce {
   std::string handle_;
 };
 
+// Persistent single-workgroup MLP train loop: `nsteps` full steps in one launch
+void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
+                    torch::Tensor loss_ring, torch::Tensor loss_cursor, torch::Tensor mom_started, torch::Tensor P,
+                    c10::optional<torch::Tensor> M, std::vector<int64_t> offsets, int64_t total, int64_t in_dim,
+                    int64_t hidden, int64_t out_dim, int64_t B, int64_t nsteps, int64_t act, int64_t loss_type,
+                    double grad_scale, double lr, double momentum, double dampening, double wd, bool nesterov,
+                    bool maximize, int64_t stream, c10::optional<torch::Tensor> dbg, int64_t dbg_step) {
+  check_gpu(Xp, "Xp");
+  TORCH_CHECK(Xp.scalar_type() == torch::kBFloat16 && Xp.dim() == 2 && Xp.size(1) == 32 &&
+                  reinterpret_cast<uintptr_t>(Xp.data_ptr()) % 16 == 0,
+              "Xp: bf16 [N, 32] (features | 1 | 0), 16-byte aligned");
+  check_f32(T, "T", false);
+  check_gpu(idx_ring, "idx_ring");
+  TORCH_CHECK(idx_ring.scalar_type() == torch::kInt32 && idx_ring.dim() == 2 && idx_ring.size(1) >= B,
+              "idx_ring: int32 [steps, >= B]");
+  for (auto* t : {&cursor, &loss_cursor, &mom_started})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt32 && t->numel() >= 1, "int32 device counters");
+  check_f32(loss_ring, "loss_ring", false);
+  check_f32(P, "P", false);
+  TORCH_CHECK(offsets.size() == 4 && P.numel() >= total, "mlp_persistent: layout");
+  TORCH_CHECK(T.numel() == Xp.size(0) * out_dim, "mlp_persistent: X/T shapes");
+  const bool has_m = M && M->defined();
+  if (has_m) {
+    check_f32(*M, "M", false);
+    TORCH_CHECK(M->numel() >= total, "momentum size");
+  }
+  TORCH_CHECK(momentum == 0.0 || has_m, "momentum needs a buffer");
+  dta::MlpPArgs a{};
+  a.Xp = Xp.data_ptr();
+  a.T = T.data_ptr<float>();
+  a.idx_ring = idx_ring.data_ptr<int>();
+  a.cursor = cursor.data_ptr<int>();
+  a.loss_ring = loss_ring.data_ptr<float>();
+  a.loss_cursor = loss_cursor.data_ptr<int>();
+  a.mom_started = mom_started.data_ptr<int>();
+  a.P = P.data_ptr<float>();
+  a.M = has_m ? M->data_ptr<float>() : nullptr;
+  a.o_w1 = (int)offsets[0];
+  a.o_b1 = (int)offsets[1];
+  a.o_w2 = (int)offsets[2];
+  a.o_b2 = (int)offsets[3];
+  a.total = (int)total;
+  a.in_dim = (int)in_dim;
+  a.hidden = (int)hidden;
+  a.out_dim = (int)out_dim;
+  a.B = (int)B;
+  a.ring_steps = (int)idx_ring.size(0);
+  a.idx_stride = (int)idx_ring.size(1);
+  a.loss_len = (int)loss_ring.numel();
+  a.nsteps = (int)nsteps;
+  a.loss_type = (int)loss_type;
+  a.grad_scale = (float)grad_scale;
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.weight_decay = (float)wd;
+  a.nesterov = nesterov;
+  a.maximize = maximize;
+  if (dbg && dbg->defined()) {
+    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= 64, "dbg: int64 [64]");
+    a.dbg = reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>());
+    a.dbg_step = (int)dbg_step;
+  }
+  hip_ok(dta_mlp_persistent(&a, (int)act, pick_stream(stream)), "mlp_persistent");
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_training_amd native runtime (gfx950 HIP kernels + RCCL communicator)";
   m.def("flat_sgd", &flat_sgd);
@@ -694,6 +762,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("wd"), py::arg("prev_grad_scale"), py::arg("nesterov"), py::arg("maximize"), py::arg("first_step"),
         py::arg("stream") = -1, py::arg("dbg_stamps") = py::none());
   m.def("mlp2_lds_bytes", &dta_mlp2_lds_bytes);
+  m.def("mlp_persistent", &mlp_persistent, py::arg("Xp"), py::arg("T"), py::arg("idx_ring"), py::arg("cursor"),
+        py::arg("loss_ring"), py::arg("loss_cursor"), py::arg("mom_started"), py::arg("P"), py::arg("M"),
+        py::arg("offsets"), py::arg("total"), py::arg("in_dim"), py::arg("hidden"), py::arg("out_dim"),
+        py::arg("B"), py::arg("nsteps"), py::arg("act"), py::arg("loss_type"), py::arg("grad_scale"),
+        py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
+        py::arg("maximize"), py::arg("stream") = -1, py::arg("dbg") = py::none(), py::arg("dbg_step") = 0);
+  m.def("mlp_persistent_lds_bytes", &dta_mlp_persistent_lds_bytes);
   m.def("attn_fwd", &attn_fwd);
   m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("rms"), py::arg("eps"),
         py::arg("stream") = -1, py::arg("res") = py::none());

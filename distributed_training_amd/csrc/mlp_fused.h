@@ -39,4 +39,25 @@ struct MlpArgs {
   unsigned long long* dbg_stamps;
 };
 
+// Persistent single-workgroup train loop (csrc/mlp_persistent.hip)
+struct MlpPArgs {
+  const void* Xp;        // [Ntot][32] bf16: features, 1.0 at column in, zeros after (prepared once)
+  const float* T;        // [Ntot][out]
+  const int* idx_ring;   // [ring_steps][idx_stride]
+  int* cursor;           // ring row of the next step (advanced by nsteps)
+  float* loss_ring;      // mean loss per step
+  int* loss_cursor;
+  int* mom_started;      // 0 until the first momentum update
+  float* P;              // flat fp32 params (in/out)
+  float* M;              // flat fp32 momentum (in/out) or null
+  int o_w1, o_b1, o_w2, o_b2, total;
+  int in_dim, hidden, out_dim, B;
+  int ring_steps, idx_stride, loss_len, nsteps;
+  int loss_type;
+  float grad_scale, lr, momentum, dampening, weight_decay;
+  int nesterov, maximize;
+  unsigned long long* dbg;  // diagnostic s_memtime stamps [waves][8] of one step (nullptr = off)
+  int dbg_step;
+};
+
 }  // namespace dta

@@ -1,0 +1,465 @@
+// Persistent single-workgroup train loop for the 2-layer MLP (the headline
+// benchmark model, BASELINE.json: Linear(in, H) -> act -> Linear(H, out),
+// SGD, 32 samples per step).
+//
+// Why this shape of kernel: one step of this model is ~2 MFLOP on ~45 KB of
+// parameters -- three orders of magnitude below what a launch, an HBM round
+// trip or a grid-wide barrier costs.  So the whole training loop runs inside
+// ONE workgroup of 8 waves on one CU: the fp32 master parameters (and SGD
+// momentum) are loaded into LDS once, `nsteps` full steps run back to back
+// with only two workgroup barriers each, and the parameters are written back
+// at the end.  Nothing is skipped: every step gathers its batch in
+// DistributedSampler order, runs forward, loss, backward and the SGD update.
+//
+// Per step (wave w owns hidden tiles w, w+8, ...; 32 hidden units each):
+//   forward  : H^T = W1 . X^T on v_mfma_f32_32x32x16_bf16 (hidden on the
+//              accumulator rows, samples on the lanes; b1 is the initial
+//              accumulator), act in registers, y partial = W2 . act(H) per lane
+//              -> LDS                                              [barrier 1]
+//   loss     : wave 0 sums the 8 partials + b2, loss (MSE / soft-target CE),
+//              dY -> LDS (fp32, and bf16 into the spare columns of the batch
+//              tile), b2 update; the next batch tile is written  [barrier 2]
+//   backward : dH = act'(H) * (W2^T dY) lane-locally; one B operand
+//              [X | 1 | dY] (32 columns) serves both weight gradients:
+//                 act(H)^T . [X|1|dY] -> columns in+1.. = dW2
+//                 dH^T     . [X|1|dY] -> columns 0..in-1 = dW1, column in = db1
+//              (A = act(H)^T / dH^T from a wave-private LDS image through
+//              ds_read_b64_tr_b16, B = the batch tile likewise), and each lane
+//              applies SGD to the parameters its accumulator column owns.
+// The batch of step s+1 is gathered while step s computes (index ring rows
+// two steps ahead, feature rows one step ahead, both in registers).
+#include "common.h"
+#include "mlp_fused.h"
+
+namespace dta {
+
+constexpr int kMpWaves = 8;
+constexpr int kMpThreads = kMpWaves * 64;
+constexpr int kMpXs = 32;            // batch tile columns (bf16): X | 1 | dY | 0
+constexpr int kMpImgPad = 32;        // bf16 pad per activation-image row (rows 64 B apart mod 256 B)
+
+
+__device__ __forceinline__ bf16x4 mp_tr4(const bf16* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// Natural-k-order transposed fragment of a row-major LDS image X (row stride
+// ST elements): lane l gets X[16s + 8(l>>5) + j][c0 + (l & 31)], j = 0..7.
+__device__ __forceinline__ bf16x8 mp_trfrag(const bf16* X, int ST, int s, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = 16 * s + 8 * (g >> 1) + (i >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const bf16x4 lo = mp_tr4(X + row * ST + col);
+  const bf16x4 hi = mp_tr4(X + (row + 4) * ST + col);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS ops, not
+// its global loads / stores.  __syncthreads() is a release fence + s_barrier,
+// and the fence waits vmcnt(0) -- it would expose the latency of the next
+// batch's prefetch loads and of the per-step loss store at every barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+#define MP_STAMP(k)                                                                             \
+  do {                                                                                          \
+    if (a.dbg && s == a.dbg_step && lane == 0) a.dbg[wave * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+// Activation image [32 samples][IMG]: 8-byte granules XOR-swizzled by row so
+// the per-lane column writes (32 lanes = 32 rows of one granule column) spread
+// over the banks instead of landing 16-way on two of them; the transposed
+// reads use the same map (each lane supplies its own address).
+__device__ __forceinline__ int img_off(int row, int col, int IMG) {
+  return row * IMG + (((col >> 2) ^ ((row >> 1) & 7)) << 2) + (col & 3);
+}
+
+__device__ __forceinline__ bf16x8 img_trfrag(const bf16* X, int IMG, int s, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = 16 * s + 8 * (g >> 1) + (i >> 2);
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const bf16x4 lo = mp_tr4(X + img_off(row, col, IMG));
+  const bf16x4 hi = mp_tr4(X + img_off(row + 4, col, IMG));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+struct SgdH {
+  float lr, mom, damp, wd;
+  int nesterov, maximize, first;
+};
+
+__device__ __forceinline__ void sgd_apply(float* p, float* m, float g, const SgdH& h) {
+  if (h.maximize) g = -g;
+  float w = *p;
+  if (h.wd != 0.f) g += h.wd * w;
+  if (h.mom != 0.f) {
+    const float b = h.first ? g : h.mom * (*m) + (1.f - h.damp) * g;
+    *m = b;
+    g = h.nesterov ? g + h.mom * b : b;
+  }
+  *p = w - h.lr * g;
+}
+
+// OUT: output width, TPW: hidden tiles per wave (H <= 256 TPW), PLAIN: SGD
+// without momentum / weight decay / maximize (the update is p -= lr * g)
+template <int ACT, int OUT, int TPW, bool PLAIN>
+__global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) {
+  static_assert(OUT == 1, "the persistent loop serves single-output heads");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int IN = a.in_dim, H = a.hidden, B = a.B, NT = H / 32;
+  const int IMG = H + kMpImgPad;  // activation image row stride (elements)
+
+  // ---- LDS carve ----
+  float* Pf = reinterpret_cast<float*>(smem);                       // [total]
+  float* Mf = Pf + a.total;                                         // [total] if momentum
+  char* q = reinterpret_cast<char*>(Mf + (a.M ? a.total : 0));
+  bf16* Xs = reinterpret_cast<bf16*>(q);                            // [2][32][kMpXs]
+  q += 2 * 32 * kMpXs * 2;
+  bf16* Img = reinterpret_cast<bf16*>(q);                           // [32][IMG]
+  q += 32 * IMG * 2;
+  float* Ypart = reinterpret_cast<float*>(q);                       // [waves][OUT][32]
+  q += kMpWaves * OUT * 32 * 4;
+  float* dYf = reinterpret_cast<float*>(q);                         // [OUT][32]
+  q += OUT * 32 * 4;
+  float* Ts = reinterpret_cast<float*>(q);                          // [2][32][OUT]
+  q += 2 * 32 * OUT * 4;
+  float* lossbuf = reinterpret_cast<float*>(q);                     // [1]
+  q += 16;
+  bf16* Wb = reinterpret_cast<bf16*>(q);                            // [H][32] bf16 W1 (k >= in zero)
+
+  // ---- load parameters (+ momentum), build the bf16 W1 fragment image ----
+  for (int i = tid; i < a.total; i += kMpThreads) {
+    Pf[i] = a.P[i];
+    if (a.M) Mf[i] = a.M[i];
+  }
+  for (int i = tid; i < H * 32; i += kMpThreads) {
+    const int h = i >> 5, k = i & 31;
+    Wb[i] = f2bf(k < IN ? a.P[a.o_w1 + h * IN + k] : 0.f);
+  }
+  int c0 = *a.cursor;
+  int lcur = *a.loss_cursor;
+  int first = a.M ? (*a.mom_started == 0) : 0;
+
+  // ---- batch pipeline: idx two steps ahead, features one step ahead ----
+  // threads [256, 256 + 32): idx of sample r for a step; feature loads: sample = tid-256 (r < B)
+  const bool gthr = tid >= 256 && tid < 256 + 32;
+  const int gr = tid - 256;
+  auto ring_row = [&](int s) { return (c0 + s) % a.ring_steps; };
+  int idx_next = 0;     // sample index of row gr for step s+1
+  bf16x8 xv[4];         // padded feature row gr of step s+1 (X | 1 | 0), 4 x 16-B loads, no branches
+  float tv[OUT];
+  const bf16* Xp = static_cast<const bf16*>(a.Xp);
+  // unconditional loads (a select around a load makes hipcc wait vmcnt(0) on it):
+  // ring rows are always allocated; samples >= B re-read column B-1 and are masked at the store
+  const int gcol = gr < B ? gr : B - 1;
+  auto load_idx = [&](int s) -> int { return a.idx_ring[(int64_t)ring_row(s) * a.idx_stride + gcol]; };
+  auto load_rows = [&](int sample) {
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(Xp + (int64_t)sample * kMpXs);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xv[c] = xr[c];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) tv[o] = a.T[(int64_t)sample * OUT + o];
+  };
+  auto store_rows = [&](int buf) {
+    // row gr of the batch tile: X | 1 | 0 (the dY columns are written by the loss phase)
+    bf16x8* row = reinterpret_cast<bf16x8*>(Xs + (buf * 32 + gr) * kMpXs);
+    const bool live = gr < B;
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) row[c] = live ? xv[c] : z;
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) Ts[(buf * 32 + gr) * OUT + o] = live ? tv[o] : 0.f;
+  };
+  if (gthr) {
+    load_rows(load_idx(0));
+    store_rows(0);
+    idx_next = load_idx(1);
+  }
+  if (tid == 0) *lossbuf = 0.f;
+  __syncthreads();
+
+  const SgdH hbase{a.lr, a.momentum, a.dampening, a.weight_decay, a.nesterov, a.maximize, 0};
+  const float lscale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
+
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int cb = s & 1;
+    const bf16* Xb = Xs + cb * 32 * kMpXs;
+    MP_STAMP(0);
+    // prefetch: features of step s+1, index of step s+2
+    if (gthr && s + 1 < a.nsteps) {
+      load_rows(idx_next);
+      idx_next = load_idx(s + 2);
+    }
+    // ================= forward (own tiles) =================
+    float yp[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) yp[o] = 0.f;
+    // B operand X^T: lane (col = sample r32), k = 16ks + 8hh + j  (row read of the batch tile)
+    const bf16x8 xb0 = *reinterpret_cast<const bf16x8*>(Xb + r32 * kMpXs + hh * 8);
+    const bf16x8 xb1 = *reinterpret_cast<const bf16x8*>(Xb + r32 * kMpXs + 16 + hh * 8);
+    f32x16 hpre[TPW];
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int t = wave + kMpWaves * tt;
+      if (t < NT) {
+        const int h0 = t * 32;
+        f32x16 acc;
+        // b1 as the initial accumulator: rows 8g + 4hh + 0..3 are consecutive -> float4 reads
+        float w2v[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = *reinterpret_cast<const float4*>(Pf + a.o_b1 + h0 + 8 * g + 4 * hh);
+          const float4 wv = *reinterpret_cast<const float4*>(Pf + a.o_w2 + h0 + 8 * g + 4 * hh);
+          acc[4 * g] = bv.x; acc[4 * g + 1] = bv.y; acc[4 * g + 2] = bv.z; acc[4 * g + 3] = bv.w;
+          w2v[4 * g] = wv.x; w2v[4 * g + 1] = wv.y; w2v[4 * g + 2] = wv.z; w2v[4 * g + 3] = wv.w;
+        }
+        // A operand W1: lane (row h = h0 + r32), k = 16ks + 8hh + j: one 16-B read of the bf16 image
+        const bf16* wr = Wb + (h0 + r32) * 32 + hh * 8;
+        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(wr), xb0, acc);
+        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(wr + 16), xb1, acc);
+        hpre[tt] = acc;
+        // layer 2 partial: y[sample] += W2[h] * act(hpre[h][sample]) over this lane's 16 rows
+#pragma unroll
+        for (int i = 0; i < 16; ++i) yp[0] += w2v[i] * act_fwd(ACT, acc[i]);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      yp[o] += __shfl_xor(yp[o], 32, kWave);
+      if (hh == 0) Ypart[(wave * OUT + o) * 32 + r32] = yp[o];
+    }
+    MP_STAMP(1);
+    lds_barrier();  // ---------------- barrier 1
+    MP_STAMP(2);
+    // ================= loss, dY, b2 (wave 0); next batch tile (staging threads) =================
+    if (wave == 0) {
+      const int r = r32;
+      float lossr = 0.f;
+      float dy[OUT];
+      if (hh == 0 && r < B) {
+        float y[OUT], t[OUT];
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          float acc = Pf[a.o_b2 + o];
+#pragma unroll
+          for (int w = 0; w < kMpWaves; ++w) acc += Ypart[(w * OUT + o) * 32 + r];
+          y[o] = acc;
+          t[o] = Ts[(cb * 32 + r) * OUT + o];
+        }
+        if (a.loss_type == LOSS_MSE) {
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) {
+            const float d = y[o] - t[o];
+            lossr += d * d;
+            dy[o] = 2.f * d * lscale;
+          }
+        } else {
+          float m = -INFINITY, sx = 0.f, tsum = 0.f;
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) m = fmaxf(m, y[o]);
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) {
+            sx += __expf(y[o] - m);
+            tsum += t[o];
+          }
+          const float lse = m + __logf(sx);
+#pragma unroll
+          for (int o = 0; o < OUT; ++o) {
+            lossr -= t[o] * (y[o] - lse);
+            dy[o] = (__expf(y[o] - lse) * tsum - t[o]) * lscale;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) dy[o] = 0.f;
+      }
+      // grads are averaged over ranks by the caller's grad_scale (1 for one rank)
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) dy[o] *= a.grad_scale;
+      if (hh == 0) {
+        bf16* row = const_cast<bf16*>(Xb) + r * kMpXs;
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          dYf[o * 32 + r] = dy[o];
+          row[IN + 1 + o] = f2bf(dy[o]);
+        }
+      }
+      // db2 = sum over samples; loss
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) {
+        const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
+        if (lane == 0) {
+          SgdH hs = hbase;
+          hs.first = first;
+          sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hs);
+        }
+      }
+      const float lsum = wave_sum(hh == 0 ? lossr : 0.f);
+      if (lane == 0) {
+        a.loss_ring[lcur % a.loss_len] = lsum * lscale;
+        ++lcur;
+      }
+    }
+    if (gthr && s + 1 < a.nsteps) store_rows(cb ^ 1);
+    MP_STAMP(3);
+    lds_barrier();  // ---------------- barrier 2
+    MP_STAMP(4);
+    // ================= backward + SGD (own tiles) =================
+    SgdH hs = hbase;
+    hs.first = first;
+    const float dyv = dYf[r32];
+    // parameter owned by accumulator column c = r32 at hidden row h: p[base + h * stride]
+    //   c < IN: W1[h][c] (from dW1 = C1)   c == IN: b1[h] (C1)   c == IN + 1: W2[0][h] (C2)
+    const int c = r32;
+    const bool upd = c <= IN + 1;
+    const bool from_c2 = c == IN + 1;
+    const int pbase = c < IN ? a.o_w1 + c : (c == IN ? a.o_b1 : a.o_w2);
+    const int pstride = c < IN ? IN : 1;
+    // B operand [X | 1 | dY] of both gradient GEMMs (same for every tile)
+    const bf16x8 xf0 = mp_trfrag(Xb, kMpXs, 0, 0, lane), xf1 = mp_trfrag(Xb, kMpXs, 1, 0, lane);
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int t = wave + kMpWaves * tt;
+      if (t < NT) {
+        const int h0 = t * 32;
+        f32x16 dh;
+        // act(H) -> image columns [h0, h0+32): lane (sample r32) writes rows 8g+4hh..+3 of its column
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 wv = *reinterpret_cast<const float4*>(Pf + a.o_w2 + h0 + 8 * g + 4 * hh);  // pre-update W2
+          const float w2g[4] = {wv.x, wv.y, wv.z, wv.w};
+          bf16x4 hv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e;
+            const float x = hpre[tt][i];
+            hv[e] = f2bf(act_fwd(ACT, x));
+            dh[i] = w2g[e] * dyv * act_bwd(ACT, x);
+          }
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = hv;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // gradient GEMMs: rows = hidden units of this tile, columns = [X | 1 | dY]
+        f32x16 c2, c1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c2[i] = c1[i] = 0.f;
+        c2 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c2);
+        c2 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // act(H) reads done before dH overwrites the image
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x4 dv = {f2bf(dh[4 * g]), f2bf(dh[4 * g + 1]), f2bf(dh[4 * g + 2]), f2bf(dh[4 * g + 3])};
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = dv;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tt == 0) MP_STAMP(6);
+        c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
+        c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
+        // SGD: all 16 parameters (and momenta) of this lane read first, then written
+        if (upd) {
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {  // 8 parameters at a time: all read, then all written
+            float pv[8], mv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int off = pbase + (h0 + mfma32_row(8 * half + u, lane)) * pstride;
+              pv[u] = Pf[off];
+              mv[u] = PLAIN ? 0.f : Mf[off];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int i = 8 * half + u;
+              float g = from_c2 ? c2[i] : c1[i];
+              if (!PLAIN) {
+                if (hs.maximize) g = -g;
+                if (hs.wd != 0.f) g += hs.wd * pv[u];
+                if (hs.mom != 0.f) {
+                  mv[u] = hs.first ? g : hs.mom * mv[u] + (1.f - hs.damp) * g;
+                  g = hs.nesterov ? g + hs.mom * mv[u] : mv[u];
+                }
+              }
+              pv[u] -= hs.lr * g;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int h = h0 + mfma32_row(8 * half + u, lane);
+              const int off = pbase + h * pstride;
+              Pf[off] = pv[u];
+              if (!PLAIN && hs.mom != 0.f) Mf[off] = mv[u];
+              if (c < IN) Wb[h * 32 + c] = f2bf(pv[u]);
+            }
+          }
+        }
+        if (tt == 0) MP_STAMP(7);
+      }
+    }
+    MP_STAMP(5);
+    first = 0;
+    // no barrier here: the next forward reads only this wave's own rows of
+    // W1 / b1 / W2 (updated above by this wave) and b2 / the next batch tile,
+    // both published before barrier 2 of this step
+  }
+  __syncthreads();
+  for (int i = tid; i < a.total; i += kMpThreads) {
+    a.P[i] = Pf[i];
+    if (a.M) a.M[i] = Mf[i];
+  }
+  if (tid == 0) {
+    *a.cursor = (c0 + a.nsteps) % a.ring_steps;
+    *a.loss_cursor = lcur;
+    if (a.M && a.nsteps > 0) *a.mom_started = 1;
+  }
+}
+
+}  // namespace dta
+
+using namespace dta;
+
+size_t dta_mlp_persistent_lds_bytes(int total, int hidden, int out_dim, int has_mom) {
+  return (size_t)total * 4 * (has_mom ? 2 : 1) + 2 * 32 * kMpXs * 2 + 32 * (hidden + kMpImgPad) * 2 +
+         kMpWaves * out_dim * 32 * 4 + out_dim * 32 * 4 + 2 * 32 * out_dim * 4 + 16 + (size_t)hidden * 32 * 2;
+}
+
+template <int ACT, int OUT, int TPW, bool PLAIN>
+static hipError_t mp_launch(const MlpPArgs& a, size_t lds, hipStream_t st) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_persistent_kernel<ACT, OUT, TPW, PLAIN>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((mlp_persistent_kernel<ACT, OUT, TPW, PLAIN>), dim3(1), dim3(kMpThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+// Instantiated for the shapes this path serves (out = 1, H <= 512: the toy /
+// 2-layer MLP configurations); wider heads or hidden layers spill registers here
+// and run on the multi-workgroup kernel (csrc/mlp_fused.hip) instead.
+template <int ACT>
+static hipError_t mp_launch_out(const MlpPArgs& a, size_t lds, hipStream_t st) {
+  if (a.out_dim != 1 || a.hidden > 512) return hipErrorInvalidValue;
+  const bool plain = a.momentum == 0.f && a.weight_decay == 0.f && !a.maximize;
+  return plain ? mp_launch<ACT, 1, 2, true>(a, lds, st) : mp_launch<ACT, 1, 2, false>(a, lds, st);
+}
+
+hipError_t dta_mlp_persistent(const MlpPArgs* a, int act, hipStream_t st) {
+  if (a->B < 1 || a->B > 32 || a->in_dim < 1 || a->in_dim + 1 + a->out_dim > kMpXs || a->hidden % 32 ||
+      a->out_dim != 1 || a->hidden > 512 ||
+      a->nsteps < 1)
+    return hipErrorInvalidValue;
+  const size_t lds = dta_mlp_persistent_lds_bytes(a->total, a->hidden, a->out_dim, a->M != nullptr);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  switch (act) {
+    case ACT_NONE: return mp_launch_out<ACT_NONE>(*a, lds, st);
+    case ACT_RELU: return mp_launch_out<ACT_RELU>(*a, lds, st);
+    case ACT_GELU_TANH: return mp_launch_out<ACT_GELU_TANH>(*a, lds, st);
+    case ACT_SILU: return mp_launch_out<ACT_SILU>(*a, lds, st);
+    default: return hipErrorInvalidValue;
+  }
+}

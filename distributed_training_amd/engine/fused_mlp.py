@@ -60,8 +60,18 @@ def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torc
 
 
 class FusedMLPProgram:
+    """Two execution modes:
+
+    * persistent (one rank, full batches, shapes within the persistent kernel's
+      limits): ``csrc/mlp_persistent.hip`` runs up to ~1000 complete steps per
+      launch in one workgroup with the parameters resident in LDS;
+    * per-step (otherwise, and for DDP across ranks): the multi-workgroup fused
+      step kernel + gradient all-reduce, hipGraph-replayed.
+    """
+
     def __init__(self, module, optimizer, loader, comm, loss: str = "mse", graph_steps: int = 32,
-                 own_tiles: Optional[int] = None, allreduce_world1: bool = True, loss_len: int = 4096):
+                 own_tiles: Optional[int] = None, allreduce_world1: bool = True, loss_len: int = 4096,
+                 persistent: Optional[bool] = None):
         self.module = module
         self.opt = optimizer
         self.loader = loader
@@ -90,9 +100,19 @@ class FusedMLPProgram:
         self.X = self.X.float().contiguous()
         self.Y = self.Y.float().contiguous()
         self.steps_per_epoch = S = max(1, len(loader))
-        # index ring: whole epochs, at least one graph beyond an epoch, so uploads
-        # for epoch e+1 can be enqueued while epoch e's steps are still queued
-        k = max(2, -(-2 * self.graph_steps // S) + 1)
+        import os
+
+        full_batches = len(loader.sampler) % self.B == 0
+        if persistent is None:
+            persistent = os.environ.get("DTA_MLP_PERSISTENT", "1") != "0"
+        self.persistent = bool(persistent and self.ws == 1 and full_batches and mf.persistent_supported(
+            module.input_size, H, module.output_size, self.B, momentum=bool(self.hyper()["momentum"])))
+        self.chunk_steps = 1024
+        # index ring: whole epochs, at least one graph (or one persistent launch)
+        # beyond an epoch, so uploads for epoch e+1 can be enqueued while epoch
+        # e's steps are still queued
+        ahead = self.chunk_steps if self.persistent else 2 * self.graph_steps
+        k = max(2, -(-ahead // S) + 1)
         self.R = S * k
         self.ring = torch.zeros(self.R, self.B, dtype=torch.int32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -108,6 +128,9 @@ class FusedMLPProgram:
         self._batch_of: Dict[int, int] = {}
         self._staging: List = []   # (pinned tensor, event) kept alive until the copy ran
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.loss_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
+        self.Xp = mf.pad_features(self.X) if self.persistent else None
         self.load_from_module()
 
     # ------------------------------------------------------------ state sync
@@ -130,7 +153,7 @@ class FusedMLPProgram:
     @torch.no_grad()
     def flush(self) -> None:
         """Apply the pending SGD update (so P[parity] holds the current weights)."""
-        if not self.pending:
+        if self.persistent or not self.pending:
             return
         hp = self.hyper()
         c = self.parity
@@ -212,8 +235,9 @@ class FusedMLPProgram:
         assert self.host_step + S - R <= self.launched, "index ring overrun"
         self.loader.sampler.set_epoch(e)
         idx = self.loader.epoch_indices().to(torch.int32)
-        host = torch.zeros(S, B, dtype=torch.int32).pin_memory()
+        host = self._pinned_buffer(S, B)
         host.view(-1)[: idx.numel()] = idx
+        host.view(-1)[idx.numel():] = 0
         last = idx.numel() - (S - 1) * B
         r0 = self.host_step % R
         n1 = min(S, R - r0)
@@ -223,12 +247,25 @@ class FusedMLPProgram:
         ev = torch.cuda.Event()
         ev.record()
         self._staging.append((host, ev))
-        if len(self._staging) > 8:
-            self._staging = [(h, e2) for h, e2 in self._staging if not e2.query()]
         for j in range(S):
             self._batch_of[self.host_step + j] = B if j < S - 1 else last
         self.host_step += S
         self.next_epoch += 1
+
+    def _pinned_buffer(self, S: int, B: int) -> torch.Tensor:
+        """A pinned [S, B] int32 host buffer whose previous H2D copy has run
+        (pinned allocation costs ~ms: buffers are recycled, not re-allocated)."""
+        keep = []
+        free = None
+        for h, ev in self._staging:
+            if free is None and ev.query():
+                free = h
+            else:
+                keep.append((h, ev))
+        self._staging = keep
+        if free is None:
+            free = torch.empty(S, B, dtype=torch.int32).pin_memory()
+        return free
 
     def _ensure(self, upto: int) -> None:
         while self.host_step < upto:
@@ -236,8 +273,25 @@ class FusedMLPProgram:
 
     # ------------------------------------------------------------ stepping API
     @torch.no_grad()
+    def _run_persistent(self, n: int) -> None:
+        end = self.launched + n
+        hp = self.hyper()
+        while self.launched < end:
+            k = min(end - self.launched, self.R - self.steps_per_epoch)
+            self._ensure(self.launched + k)
+            mf.persistent_steps(self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor,
+                                self.mom_started_dev, self.P[0], self.M[0], self.layout, self.B, k, self.act,
+                                self.loss, 1.0 / self.ws, hp)
+            for j in range(k):
+                self._batch_of.pop(self.launched + j, None)
+            self.launched += k
+
+    @torch.no_grad()
     def run_steps(self, n: int) -> None:
         """Enqueue ``n`` training steps (crossing epochs as needed)."""
+        if self.persistent:
+            self._run_persistent(n)
+            return
         end = self.launched + n
         while self.launched < end:
             U = self.graph_steps

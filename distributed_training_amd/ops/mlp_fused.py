@@ -85,6 +85,37 @@ def supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool
     )
 
 
+def persistent_supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool = False) -> bool:
+    """Shapes served by the persistent single-workgroup loop (csrc/mlp_persistent.hip)."""
+    if not (1 <= in_dim and in_dim + 1 + out_dim <= 32 and out_dim == 1 and hidden % 32 == 0
+            and 32 <= hidden <= 512 and 1 <= batch <= 32):
+        return False
+    total = make_layout(in_dim, hidden, out_dim).total
+    return native().mlp_persistent_lds_bytes(total, hidden, out_dim, int(momentum)) <= LDS_LIMIT
+
+
+def pad_features(X: torch.Tensor) -> torch.Tensor:
+    """[N, in] -> bf16 [N, 32] = (X | 1 | 0): the persistent kernel's row format
+    (the ones column carries the bias gradient)."""
+    N, I = X.shape
+    Xp = torch.zeros(N, 32, dtype=torch.bfloat16, device=X.device)
+    Xp[:, :I] = X.to(torch.bfloat16)
+    Xp[:, I] = 1.0
+    return Xp
+
+
+def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout: MlpLayout,
+                     batch: int, nsteps: int, act: str, loss: str, grad_scale: float, sgd: Dict[str, float],
+                     stream=None, dbg=None, dbg_step: int = 0) -> None:
+    """``nsteps`` complete training steps (gather, forward, loss, backward, SGD) in ONE launch."""
+    native().mlp_persistent(
+        Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout.offsets, layout.total,
+        layout.in_dim, layout.hidden, layout.out_dim, int(batch), int(nsteps), ACTIVATIONS[act], LOSSES[loss],
+        float(grad_scale), float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)),
+        float(sgd.get("dampening", 0.0)), float(sgd.get("weight_decay", 0.0)), bool(sgd.get("nesterov", False)),
+        bool(sgd.get("maximize", False)), -1 if stream is None else int(stream.cuda_stream), dbg, int(dbg_step))
+
+
 STAGE_ROWS, STAGE_COLS = 128, 32
 
 

@@ -10,7 +10,7 @@ def _dev():
     return torch.device("cuda", 0)
 
 
-def _setup(hidden=512, size=256, batch=32, momentum=0.0, graph_steps=4):
+def _setup(hidden=512, size=256, batch=32, momentum=0.0, graph_steps=4, persistent=None):
     from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
     from distributed_training_amd.engine.fused_mlp import FusedMLPProgram
     from distributed_training_amd.models.mlp import MLP
@@ -29,15 +29,19 @@ def _setup(hidden=512, size=256, batch=32, momentum=0.0, graph_steps=4):
     ddp = DistributedDataParallel(model, comm=comm, device=dev)
     opt = FusedSGD(ddp.parameters(), lr=0.05, momentum=momentum)
     loader = DeviceDataLoader(ds, batch, sampler=DistributedSampler(ds, num_replicas=1, rank=0, seed=3), device=dev)
-    prog = FusedMLPProgram(model, opt, loader, comm, loss="mse", graph_steps=graph_steps)
+    prog = FusedMLPProgram(model, opt, loader, comm, loss="mse", graph_steps=graph_steps, persistent=persistent)
     return ds, model, ref, prog, loader
 
 
-@pytest.mark.parametrize("momentum,size,batch", [(0.0, 256, 32), (0.9, 200, 32), (0.0, 96, 64)])
-def test_fused_program_matches_torch_sgd(momentum, size, batch):
-    """Fused program (eager + hipGraph replays across epoch boundaries, partial
-    last batches) vs a plain fp32 torch training loop over the same batches."""
-    ds, model, ref, prog, loader = _setup(size=size, batch=batch, momentum=momentum)
+@pytest.mark.parametrize("momentum,size,batch,persistent", [(0.0, 256, 32, None), (0.9, 256, 32, None),
+                                                             (0.0, 256, 32, False), (0.9, 200, 32, None),
+                                                             (0.0, 96, 64, None)])
+def test_fused_program_matches_torch_sgd(momentum, size, batch, persistent):
+    """Fused program (persistent single-workgroup loop, or eager + hipGraph
+    replays across epoch boundaries with partial last batches) vs a plain fp32
+    torch training loop over the same batches."""
+    ds, model, ref, prog, loader = _setup(size=size, batch=batch, momentum=momentum, persistent=persistent)
+    assert prog.persistent == (persistent is None and size % batch == 0 and batch <= 32)
     opt_ref = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=momentum)
     n_epochs = 3
     ref_losses = []
@@ -63,12 +67,32 @@ def test_fused_program_matches_torch_sgd(momentum, size, batch):
 
 
 def test_fused_program_graph_used():
-    ds, model, ref, prog, loader = _setup(size=2048, batch=32, graph_steps=8)
+    ds, model, ref, prog, loader = _setup(size=2048, batch=32, graph_steps=8, persistent=False)
     prog.run_steps(100)
     torch.cuda.synchronize()
     assert 0 in prog._graphs or 1 in prog._graphs
     assert int(prog.cursor.item()) == 100
     assert torch.isfinite(prog.last_losses(100)).all()
+
+
+def test_persistent_program_long_run():
+    """Persistent launches of up to chunk_steps steps, crossing epochs and
+    index-ring wrap-around, match the per-step program bit-for-bit in loss
+    trajectory shape and end in the same place within bf16 tolerance."""
+    _, model_a, _, pa, _ = _setup(size=2048, batch=32)
+    _, model_b, _, pb, _ = _setup(size=2048, batch=32, persistent=False)
+    assert pa.persistent and not pb.persistent
+    pa.run_steps(2500)
+    pb.run_steps(2500)
+    pa.store_to_module()
+    pb.store_to_module()
+    torch.cuda.synchronize()
+    assert int(pa.cursor.item()) == 2500 % pa.R
+    la, lb = pa.last_losses(2500).cpu(), pb.last_losses(2500).cpu()
+    assert torch.isfinite(la).all()
+    torch.testing.assert_close(la[-200:].mean(), lb[-200:].mean(), rtol=5e-2, atol=1e-3)
+    for (n, p), (_, q) in zip(model_a.named_parameters(), model_b.named_parameters()):
+        assert (p - q).abs().max().item() < 3e-2 * max(1.0, q.abs().max().item()), n
 
 
 def test_trainer_end_to_end_gpu(tmp_path):
