@@ -55,6 +55,8 @@ hipError_t dta_p2p_allreduce(void*, float*, int64_t, float, int, hipStream_t);
 hipError_t dta_p2p_error(void*, int*);
 void dta_p2p_destroy(void*);
 void dta_p2p_set_ll(void*, int);
+hipError_t dta_p2p_ll_info(void*, unsigned long long*, unsigned long long*, int*, int*, long long*,
+                           unsigned long long*, unsigned long long*);
 
 namespace {
 
@@ -671,6 +673,15 @@ class PyP2PAllReduce {
   }
   int64_t max_elems() const { return max_elems_; }
   void set_ll(bool ll) { dta_p2p_set_ll(state_, ll ? 1 : 0); }
+  // (peer LL slot pointers, local LL pointer, rank, world, slot elems, err ptr, spare counter ptr)
+  py::tuple ll_info() const {
+    unsigned long long peers[8] = {}, local = 0, err = 0, ctr = 0;
+    int rank = 0, world = 0;
+    long long slot = 0;
+    hip_ok(dta_p2p_ll_info(state_, peers, &local, &rank, &world, &slot, &err, &ctr), "p2p ll_info");
+    std::vector<int64_t> pv(peers, peers + world);
+    return py::make_tuple(pv, (int64_t)local, rank, world, (int64_t)slot, (int64_t)err, (int64_t)ctr);
+  }
 
  private:
   void* state_ = nullptr;
@@ -685,7 +696,8 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
                     c10::optional<torch::Tensor> M, std::vector<int64_t> offsets, int64_t total, int64_t in_dim,
                     int64_t hidden, int64_t out_dim, int64_t B, int64_t nsteps, int64_t act, int64_t loss_type,
                     double grad_scale, double lr, double momentum, double dampening, double wd, bool nesterov,
-                    bool maximize, int64_t stream, c10::optional<torch::Tensor> dbg, int64_t dbg_step) {
+                    bool maximize, int64_t stream, c10::optional<torch::Tensor> dbg, int64_t dbg_step,
+                    std::vector<int64_t> xinfo) {
   check_gpu(Xp, "Xp");
   TORCH_CHECK(Xp.scalar_type() == torch::kBFloat16 && Xp.dim() == 2 && Xp.size(1) == 32 &&
                   reinterpret_cast<uintptr_t>(Xp.data_ptr()) % 16 == 0,
@@ -737,6 +749,22 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
   a.weight_decay = (float)wd;
   a.nesterov = nesterov;
   a.maximize = maximize;
+  // xinfo (DDP exchange, empty for one rank): world, rank, slot_elems, local_ll, xerr, xepoch,
+  // timeout_iters, peer_ll[0..world)
+  a.world = 1;
+  if (!xinfo.empty()) {
+    TORCH_CHECK(xinfo.size() >= 7 && (int64_t)xinfo.size() == 7 + xinfo[0] && xinfo[0] >= 1 && xinfo[0] <= 8,
+                "mlp_persistent: bad exchange info");
+    a.world = (int)xinfo[0];
+    a.rank = (int)xinfo[1];
+    a.slot_elems = xinfo[2];
+    TORCH_CHECK(a.slot_elems >= total, "mlp_persistent: p2p slots smaller than the parameter set");
+    a.local_ll = reinterpret_cast<const unsigned long long*>(xinfo[3]);
+    a.xerr = reinterpret_cast<int*>(xinfo[4]);
+    a.xepoch = reinterpret_cast<int*>(xinfo[5]);
+    a.timeout_iters = (int)xinfo[6];
+    for (int q = 0; q < a.world; ++q) a.peer_ll[q] = reinterpret_cast<unsigned long long*>(xinfo[7 + q]);
+  }
   if (dbg && dbg->defined()) {
     TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= 64, "dbg: int64 [64]");
     a.dbg = reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>());
@@ -767,7 +795,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("offsets"), py::arg("total"), py::arg("in_dim"), py::arg("hidden"), py::arg("out_dim"),
         py::arg("B"), py::arg("nsteps"), py::arg("act"), py::arg("loss_type"), py::arg("grad_scale"),
         py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
-        py::arg("maximize"), py::arg("stream") = -1, py::arg("dbg") = py::none(), py::arg("dbg_step") = 0);
+        py::arg("maximize"), py::arg("stream") = -1, py::arg("dbg") = py::none(), py::arg("dbg_step") = 0,
+        py::arg("xinfo") = std::vector<int64_t>{});
   m.def("mlp_persistent_lds_bytes", &dta_mlp_persistent_lds_bytes);
   m.def("attn_fwd", &attn_fwd);
   m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("rms"), py::arg("eps"),
@@ -805,6 +834,7 @@ PYBIND11_MODULE(_C, m) {
       .def("error", &PyP2PAllReduce::error)
       .def("destroy", &PyP2PAllReduce::destroy)
       .def("set_ll", &PyP2PAllReduce::set_ll)
+      .def("ll_info", &PyP2PAllReduce::ll_info)
       .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())

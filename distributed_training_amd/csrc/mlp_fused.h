@@ -58,6 +58,15 @@ struct MlpPArgs {
   int nesterov, maximize;
   unsigned long long* dbg;  // diagnostic s_memtime stamps [waves][8] of one step (nullptr = off)
   int dbg_step;
+  // DDP across ranks (world > 1): per-step gradient exchange through the LL
+  // slots of a dedicated p2p buffer set (csrc/p2p_allreduce.hip)
+  int rank, world;
+  unsigned long long* peer_ll[8];   // each rank's LL slot array [2][world][slot_elems]
+  const unsigned long long* local_ll;
+  long long slot_elems;
+  int* xepoch;                      // exchange epoch counter (device, advanced by nsteps)
+  int* xerr;                        // raised when a peer never delivered (bounded wait)
+  int timeout_iters;
 };
 
 }  // namespace dta

@@ -105,9 +105,95 @@ __device__ __forceinline__ void sgd_apply(float* p, float* m, float g, const Sgd
   *p = w - h.lr * g;
 }
 
+// ---- DDP across ranks: one-shot gradient exchange through LL slots ----
+// Every element travels as one 8-byte store {f32 bits, epoch} into slot
+// [epoch & 1][rank] of EVERY rank (itself included); each rank then sums the
+// `world` slots in rank order -- identical bits everywhere -- and applies SGD.
+// A slot is rewritten two epochs later only after its reader consumed it (each
+// element is pushed and read by the same lane mapping on every rank).
+__device__ __forceinline__ void xpush(const MlpPArgs& a, unsigned ep, int off, float g) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(g) | ((unsigned long long)ep << 32);
+  const long long slot = ((long long)(ep & 1) * a.world + a.rank) * a.slot_elems + off;
+  for (int q = 0; q < a.world; ++q)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.peer_ll[q]) + slot, v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// flat offset of the j-th real parameter (W1 | b1 | W2 | b2, padding skipped)
+__device__ __forceinline__ int xoff(const MlpPArgs& a, int j) {
+  const int n1 = a.hidden * a.in_dim;
+  if (j < n1) return a.o_w1 + j;
+  j -= n1;
+  if (j < a.hidden) return a.o_b1 + j;
+  j -= a.hidden;
+  if (j < a.hidden) return a.o_w2 + j;
+  return a.o_b2 + (j - a.hidden);
+}
+
+template <bool PLAIN>
+__device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf, bf16* Wb, SgdH hs, int first) {
+  constexpr int U = 8;  // elements per thread in flight (x world loads)
+  hs.first = first;
+  const int n = a.hidden * a.in_dim + 2 * a.hidden + a.out_dim;
+  const int W = a.world, par = ep & 1;
+  const unsigned long long* base = a.local_ll + (long long)par * W * a.slot_elems;
+  for (int j0 = threadIdx.x; j0 < n; j0 += kMpThreads * U) {
+    int off[U];
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * kMpThreads;
+      off[u] = xoff(a, j < n ? j : n - 1);
+      acc[u] = 0.f;
+    }
+    for (int q = 0; q < W; ++q) {  // rank order
+      unsigned long long v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = __hip_atomic_load(base + (long long)q * a.slot_elems + off[u], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int it = 0;
+        while ((unsigned)(v[u] >> 32) != ep) {
+          if (++it > a.timeout_iters) {
+            atomicOr(a.xerr, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          v[u] = __hip_atomic_load(base + (long long)q * a.slot_elems + off[u], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        acc[u] += __uint_as_float((unsigned)(v[u] & 0xffffffffu));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * kMpThreads;
+      if (j < n) {
+        const int o = off[u];
+        float g = acc[u];
+        float p = Pf[o];
+        if (!PLAIN) {
+          if (hs.maximize) g = -g;
+          if (hs.wd != 0.f) g += hs.wd * p;
+          if (hs.mom != 0.f) {
+            const float b = hs.first ? g : hs.mom * Mf[o] + (1.f - hs.damp) * g;
+            Mf[o] = b;
+            g = hs.nesterov ? g + hs.mom * b : b;
+          }
+        }
+        p -= hs.lr * g;
+        Pf[o] = p;
+        if (j < a.hidden * a.in_dim) Wb[(j / a.in_dim) * 32 + j % a.in_dim] = f2bf(p);
+      }
+    }
+  }
+}
+
 // OUT: output width, TPW: hidden tiles per wave (H <= 256 TPW), PLAIN: SGD
 // without momentum / weight decay / maximize (the update is p -= lr * g)
-template <int ACT, int OUT, int TPW, bool PLAIN>
+template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
 __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) {
   static_assert(OUT == 1, "the persistent loop serves single-output heads");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -147,6 +233,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   int c0 = *a.cursor;
   int lcur = *a.loss_cursor;
   int first = a.M ? (*a.mom_started == 0) : 0;
+  constexpr bool multi = MULTI;  // DDP across ranks (a.world > 1)
+  const unsigned xe0 = multi ? (unsigned)*a.xepoch : 0u;
 
   // ---- batch pipeline: idx two steps ahead, features one step ahead ----
   // threads [256, 256 + 32): idx of sample r for a step; feature loads: sample = tid-256 (r < B)
@@ -299,9 +387,13 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
       for (int o = 0; o < OUT; ++o) {
         const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
         if (lane == 0) {
-          SgdH hs = hbase;
-          hs.first = first;
-          sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hs);
+          if (multi) {
+            xpush(a, xe0 + s + 1, a.o_b2 + o, db);
+          } else {
+            SgdH hs = hbase;
+            hs.first = first;
+            sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hs);
+          }
         }
       }
       const float lsum = wave_sum(hh == 0 ? lossr : 0.f);
@@ -366,7 +458,13 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
         // SGD: all 16 parameters (and momenta) of this lane read first, then written
-        if (upd) {
+        if (upd && multi) {
+          // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
+          const unsigned ep = xe0 + s + 1;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, from_c2 ? c2[i] : c1[i]);
+        } else if (upd) {
 #pragma unroll
           for (int half = 0; half < 2; ++half) {  // 8 parameters at a time: all read, then all written
             float pv[8], mv[8];
@@ -403,11 +501,17 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         if (tt == 0) MP_STAMP(7);
       }
     }
+    if constexpr (MULTI) {
+      // all waves done reading the pre-update parameters before any update
+      lds_barrier();
+      xreduce_sgd<PLAIN>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
+      lds_barrier();
+    }
     MP_STAMP(5);
     first = 0;
-    // no barrier here: the next forward reads only this wave's own rows of
-    // W1 / b1 / W2 (updated above by this wave) and b2 / the next batch tile,
-    // both published before barrier 2 of this step
+    // one rank: no barrier here -- the next forward reads only this wave's own
+    // rows of W1 / b1 / W2 (updated above by this wave) and b2 / the next batch
+    // tile, both published before barrier 2 of this step
   }
   __syncthreads();
   for (int i = tid; i < a.total; i += kMpThreads) {
@@ -415,6 +519,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     if (a.M) a.M[i] = Mf[i];
   }
   if (tid == 0) {
+    if (multi) *a.xepoch = (int)(xe0 + (unsigned)a.nsteps);
     *a.cursor = (c0 + a.nsteps) % a.ring_steps;
     *a.loss_cursor = lcur;
     if (a.M && a.nsteps > 0) *a.mom_started = 1;
@@ -430,11 +535,11 @@ size_t dta_mlp_persistent_lds_bytes(int total, int hidden, int out_dim, int has_
          kMpWaves * out_dim * 32 * 4 + out_dim * 32 * 4 + 2 * 32 * out_dim * 4 + 16 + (size_t)hidden * 32 * 2;
 }
 
-template <int ACT, int OUT, int TPW, bool PLAIN>
+template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
 static hipError_t mp_launch(const MlpPArgs& a, size_t lds, hipStream_t st) {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_persistent_kernel<ACT, OUT, TPW, PLAIN>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((mlp_persistent_kernel<ACT, OUT, TPW, PLAIN>), dim3(1), dim3(kMpThreads), lds, st, a);
+  auto k = &mlp_persistent_kernel<ACT, OUT, TPW, PLAIN, MULTI>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k, dim3(1), dim3(kMpThreads), lds, st, a);
   return hipGetLastError();
 }
 
@@ -445,7 +550,9 @@ template <int ACT>
 static hipError_t mp_launch_out(const MlpPArgs& a, size_t lds, hipStream_t st) {
   if (a.out_dim != 1 || a.hidden > 512) return hipErrorInvalidValue;
   const bool plain = a.momentum == 0.f && a.weight_decay == 0.f && !a.maximize;
-  return plain ? mp_launch<ACT, 1, 2, true>(a, lds, st) : mp_launch<ACT, 1, 2, false>(a, lds, st);
+  if (a.world > 1)
+    return plain ? mp_launch<ACT, 1, 2, true, true>(a, lds, st) : mp_launch<ACT, 1, 2, false, true>(a, lds, st);
+  return plain ? mp_launch<ACT, 1, 2, true, false>(a, lds, st) : mp_launch<ACT, 1, 2, false, false>(a, lds, st);
 }
 
 hipError_t dta_mlp_persistent(const MlpPArgs* a, int act, hipStream_t st) {

@@ -243,6 +243,22 @@ hipError_t dta_p2p_open(void* state, const void* handles) {
   return hipSuccess;
 }
 
+// LL slot arrays of every rank (for kernels that exchange through them directly,
+// e.g. the persistent MLP loop), the error flag and a spare device counter.
+hipError_t dta_p2p_ll_info(void* state, unsigned long long* peer_ll, unsigned long long* local_ll, int* rank,
+                           int* world, long long* slot_elems, unsigned long long* err, unsigned long long* counter) {
+  auto* s = static_cast<P2PState*>(state);
+  if (!s->opened) return hipErrorInvalidValue;
+  for (int q = 0; q < s->world; ++q) peer_ll[q] = reinterpret_cast<unsigned long long>(s->peers[q] + s->ll_off);
+  *local_ll = reinterpret_cast<unsigned long long>(s->buf + s->ll_off);
+  *rank = s->rank;
+  *world = s->world;
+  *slot_elems = s->max_elems;
+  *err = reinterpret_cast<unsigned long long>(s->err);
+  *counter = reinterpret_cast<unsigned long long>(s->epoch + kP2PMaxWG + 1);  // after err: a free int
+  return hipSuccess;
+}
+
 int dta_p2p_num_wg(int64_t n) {
   // ~2048 elements (8 KiB) per workgroup: enough memory-level parallelism per
   // link without spreading a 45 KB bucket over more flag round trips

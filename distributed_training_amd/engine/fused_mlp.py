@@ -105,8 +105,13 @@ class FusedMLPProgram:
         full_batches = len(loader.sampler) % self.B == 0
         if persistent is None:
             persistent = os.environ.get("DTA_MLP_PERSISTENT", "1") != "0"
-        self.persistent = bool(persistent and self.ws == 1 and full_batches and mf.persistent_supported(
+        self.persistent = bool(persistent and full_batches and mf.persistent_supported(
             module.input_size, H, module.output_size, self.B, momentum=bool(self.hyper()["momentum"])))
+        self._p2p = None
+        self._xinfo = None
+        self.xepoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        if self.persistent and self.ws > 1:
+            self.persistent = self._setup_exchange()
         self.chunk_steps = 1024
         # index ring: whole epochs, at least one graph (or one persistent launch)
         # beyond an epoch, so uploads for epoch e+1 can be enqueued while epoch
@@ -132,6 +137,36 @@ class FusedMLPProgram:
         self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
         self.Xp = mf.pad_features(self.X) if self.persistent else None
         self.load_from_module()
+
+    def _setup_exchange(self) -> bool:
+        """DDP across ranks inside the persistent loop: a dedicated p2p buffer set
+        whose LL slots the kernel writes directly (collective; every rank agrees)."""
+        import torch.distributed as dist
+
+        from ..parallel.p2p import P2PAllReduce, intra_node
+
+        ok = 1
+        if not (dist.is_initialized() and intra_node() and self.ws <= 8):
+            ok = 0
+        p2p = None
+        if ok:
+            try:
+                p2p = P2PAllReduce(self.comm.rank, self.ws, self.device, dist.distributed_c10d._get_default_store(),
+                                   tag="fused_mlp", max_elems=self.layout.total)
+                self._xinfo = mf.exchange_info(p2p, self.xepoch)
+            except Exception as e:  # noqa: BLE001 - fall back to the per-step program
+                logger.warning("persistent DDP exchange unavailable (%s); per-step program used", e)
+                ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32,
+                            device=self.device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) != 1:
+            if p2p is not None:
+                p2p.destroy()
+            self._xinfo = None
+            return False
+        self._p2p = p2p
+        return True
 
     # ------------------------------------------------------------ state sync
     def hyper(self) -> Dict[str, float]:
@@ -168,6 +203,8 @@ class FusedMLPProgram:
         self.flush()
         if hasattr(self.comm, "check_errors"):
             self.comm.check_errors()  # a p2p all-reduce that timed out on a dead peer raises here
+        if self._p2p is not None:
+            self._p2p.check()
         v = self.layout.views(self.P[self.parity])
         for name, p in self.module.named_parameters():
             tag = getattr(p, "_dta_flat", None)
@@ -281,7 +318,7 @@ class FusedMLPProgram:
             self._ensure(self.launched + k)
             mf.persistent_steps(self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor,
                                 self.mom_started_dev, self.P[0], self.M[0], self.layout, self.B, k, self.act,
-                                self.loss, 1.0 / self.ws, hp)
+                                self.loss, 1.0 / self.ws, hp, xinfo=self._xinfo)
             for j in range(k):
                 self._batch_of.pop(self.launched + j, None)
             self.launched += k

@@ -106,14 +106,23 @@ def pad_features(X: torch.Tensor) -> torch.Tensor:
 
 def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout: MlpLayout,
                      batch: int, nsteps: int, act: str, loss: str, grad_scale: float, sgd: Dict[str, float],
-                     stream=None, dbg=None, dbg_step: int = 0) -> None:
-    """``nsteps`` complete training steps (gather, forward, loss, backward, SGD) in ONE launch."""
+                     stream=None, dbg=None, dbg_step: int = 0, xinfo=None) -> None:
+    """``nsteps`` complete training steps (gather, forward, loss, backward, SGD) in ONE launch.
+    ``xinfo`` (from :func:`exchange_info`): DDP gradient exchange across ranks inside the loop."""
     native().mlp_persistent(
         Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout.offsets, layout.total,
         layout.in_dim, layout.hidden, layout.out_dim, int(batch), int(nsteps), ACTIVATIONS[act], LOSSES[loss],
         float(grad_scale), float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)),
         float(sgd.get("dampening", 0.0)), float(sgd.get("weight_decay", 0.0)), bool(sgd.get("nesterov", False)),
-        bool(sgd.get("maximize", False)), -1 if stream is None else int(stream.cuda_stream), dbg, int(dbg_step))
+        bool(sgd.get("maximize", False)), -1 if stream is None else int(stream.cuda_stream), dbg, int(dbg_step),
+        list(xinfo) if xinfo else [])
+
+
+def exchange_info(p2p, xepoch: torch.Tensor, timeout_iters: int = 1 << 24):
+    """Flatten a :class:`~..parallel.p2p.P2PAllReduce` (dedicated to this loop) into the
+    kernel's exchange descriptor."""
+    peers, local, rank, world, slot, err, _ = p2p._h.ll_info()
+    return [world, rank, slot, local, err, xepoch.data_ptr(), int(timeout_iters)] + list(peers)
 
 
 STAGE_ROWS, STAGE_COLS = 128, 32
