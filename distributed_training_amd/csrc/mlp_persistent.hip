@@ -156,7 +156,9 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
       for (int u = 0; u < U; ++u) {
         int it = 0;
         while ((unsigned)(v[u] >> 32) != ep) {
-          if (++it > a.timeout_iters) {
+          // sticky error: after one timed-out wait the rest give up at once
+          if (++it > a.timeout_iters ||
+              ((it & 1023) == 1 && __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             atomicOr(a.xerr, 1);
             break;
           }

@@ -59,6 +59,10 @@ struct P2PArgs {
   const uint64_t* local_ll;
 };
 
+__device__ __forceinline__ bool peer_failed(int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
 // The epoch is global per call: every workgroup slot counter advances together
 // (workgroup 0 also advances the counters of workgroups this launch did not
 // use), so element i alternates parity on every call even when consecutive
@@ -98,7 +102,9 @@ __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_ll_kernel(P2PArgs a
       uint64_t v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       int it = 0;
       while ((unsigned)(v >> 32) != epoch) {
-        if (++it > a.timeout_iters) {
+        // bounded wait; once any wait timed out (sticky error flag) every later
+        // wait gives up at once, so a dead peer costs one timeout, not one per element
+        if (++it > a.timeout_iters || ((it & 1023) == 1 && peer_failed(a.err))) {
           atomicOr(a.err, 1);
           break;
         }
@@ -142,7 +148,7 @@ __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_kernel(P2PArgs a) {
     const int* f = a.local_flags + ((int64_t)par * kP2PMaxWG + w) * W + tid;
     int it = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-      if (++it > a.timeout_iters) {
+      if (++it > a.timeout_iters || ((it & 1023) == 1 && peer_failed(a.err))) {
         atomicOr(a.err, 1);
         break;
       }

@@ -153,6 +153,19 @@ class FusedMLPProgram:
             try:
                 p2p = P2PAllReduce(self.comm.rank, self.ws, self.device, dist.distributed_c10d._get_default_store(),
                                    tag="fused_mlp", max_elems=self.layout.total)
+                # the kernel pushes through the same peer mappings: prove them with
+                # one exchange of known values before any training step relies on them
+                n = self.layout.total
+                x = torch.arange(n, device=self.device, dtype=torch.float32) * (self.comm.rank + 1)
+                p2p.all_reduce(x, 1.0)
+                want = torch.arange(n, device=self.device, dtype=torch.float32) * (self.ws * (self.ws + 1) / 2)
+                torch.cuda.synchronize(self.device)
+                p2p.check()
+                if not torch.equal(x, want):
+                    raise RuntimeError("p2p self-test mismatch")
+                # the self-test left {value, tag 1} in the slots: the loop's first
+                # exchange epoch must be past it (epochs are xepoch + 1, + 2, ...)
+                self.xepoch.fill_(1)
                 self._xinfo = mf.exchange_info(p2p, self.xepoch)
             except Exception as e:  # noqa: BLE001 - fall back to the per-step program
                 logger.warning("persistent DDP exchange unavailable (%s); per-step program used", e)
