@@ -38,6 +38,8 @@
 #include "common.h"
 #include "attention.h"
 
+#include <cstdlib>
+
 namespace dta {
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -54,37 +56,65 @@ __device__ __forceinline__ bf16x4 lds_tr4(const bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// LDS images are unpadded [rows][D] bf16 tiles with the 16-byte chunks of each
+// row XOR-swizzled by a function of the row, chosen (scripts/lds_banks.py, the
+// lane-group / bank rules of MI355X_MICROARCH.md §LDS) so that all three
+// accesses are conflict-free on the same image: the row read of an MFMA
+// operand (ds_read_b128, lane = row, 16 B of the head dim), the transposed
+// read (ds_read_b64_tr_b16, 4 rows x 16 columns per 16-lane group) and the
+// register-staged 16-byte stores.  No padding keeps K+V double buffers at
+// 32 KB (D = 64) / 64 KB (D = 128) per workgroup, so two or more workgroups
+// share a CU.
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  static_assert(D == 64 || D == 128, "head dim");
+  if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 3) & 1) | (((row >> 4) & 1) << 1);
+  else return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+
+// element offset of (row, col) in a swizzled image (col % 4 == 0 for 8-byte reads)
+template <int D>
+__device__ __forceinline__ int lo(int row, int col) {
+  return row * D + ((((col >> 3) ^ swz<D>(row)) << 3) | (col & 7));
+}
+
 // A-operand fragment of X^T for a 32x32x16 MFMA whose B operand is an
 // accumulator tile used as it stands (its row index is the k index, in the
 // permuted order of cdna_hip_programming.md §3): lane (r32, hh) gets
 // X[row0 + 16s + 8(j>>2) + 4hh + (j&3)][col0 + r32], j = 0..7, from the
-// row-major LDS tile X (row stride ST elements) by two transposed reads.
-template <int ST>
+// swizzled LDS image X by two transposed reads.
+template <int D>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* X, int row0, int col0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int r = row0 + 16 * s + 4 * (g >> 1) + (i >> 2);
   const int c = col0 + 16 * (g & 1) + 4 * (i & 3);
-  const bf16x4 lo = lds_tr4(X + r * ST + c);
-  const bf16x4 hi = lds_tr4(X + (r + 8) * ST + c);
-  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  const bf16x4 lo4 = lds_tr4(X + lo<D>(r, c));
+  const bf16x4 hi4 = lds_tr4(X + lo<D>(r + 8, c));
+  return bf16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
 }
 
-// Cooperative register staging of an [R][D] bf16 tile (256 threads, 16-byte
-// loads), rows >= nrows zero-filled; then one store into an LDS tile of row
-// stride ST.
-template <int R, int D>
+// MFMA row-operand fragment: row `row`, head-dim columns 16 ks + 8 hh .. + 7
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag(const bf16* X, int row, int ks, int hh) {
+  return *reinterpret_cast<const bf16x8*>(X + lo<D>(row, ks * 16 + hh * 8));
+}
+
+// Cooperative register staging of an [R][D] bf16 tile (NT threads, 16-byte
+// loads), rows >= nrows zero-filled; then one store into a swizzled LDS image.
+template <int R, int D, int NT>
 struct TileRegs {
-  static constexpr int N = R * D / 8 / 256;
+  static constexpr int N = R * D / 8 / NT;
+  static_assert(N >= 1 && R * D == N * 8 * NT, "tile / thread count");
   bf16x8 v[N];
 };
 
-template <int R, int D>
-__device__ __forceinline__ void tile_load(TileRegs<R, D>& t, const bf16* base, int64_t rs, int row0, int nrows,
+template <int R, int D, int NT>
+__device__ __forceinline__ void tile_load(TileRegs<R, D, NT>& t, const bf16* base, int64_t rs, int row0, int nrows,
                                           int tid) {
   constexpr int CPR = D / 8;
 #pragma unroll
-  for (int l = 0; l < TileRegs<R, D>::N; ++l) {
-    const int e = tid + l * 256, r = e / CPR, c8 = (e % CPR) * 8;
+  for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
+    const int e = tid + l * NT, r = e / CPR, c8 = (e % CPR) * 8;
     if (row0 + r < nrows) {
       t.v[l] = *reinterpret_cast<const bf16x8*>(base + (int64_t)(row0 + r) * rs + c8);
     } else {
@@ -94,13 +124,13 @@ __device__ __forceinline__ void tile_load(TileRegs<R, D>& t, const bf16* base, i
   }
 }
 
-template <int R, int D, int ST>
-__device__ __forceinline__ void tile_store(const TileRegs<R, D>& t, bf16* lds, int tid) {
+template <int R, int D, int NT>
+__device__ __forceinline__ void tile_store(const TileRegs<R, D, NT>& t, bf16* lds, int tid) {
   constexpr int CPR = D / 8;
 #pragma unroll
-  for (int l = 0; l < TileRegs<R, D>::N; ++l) {
-    const int e = tid + l * 256, r = e / CPR, c8 = (e % CPR) * 8;
-    *reinterpret_cast<bf16x8*>(lds + r * ST + c8) = t.v[l];
+  for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
+    const int e = tid + l * NT, r = e / CPR, c8 = (e % CPR) * 8;
+    *reinterpret_cast<bf16x8*>(lds + lo<D>(r, c8)) = t.v[l];
   }
 }
 
@@ -109,21 +139,41 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 }
 
 // ------------------------------------------------------------------ forward
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+// Occupancy the register budget is fitted to (waves per SIMD): the K/V double
+// buffer is 32 KB (D = 64) / 64 KB (D = 128) per workgroup.
+template <int D>
+struct FwdCfg {
+  static constexpr int kWavesPerSimd = D == 64 ? 3 : 2;
+};
+
+// Block id -> (query block, batch, head).  Under the causal mask the work of a
+// query block grows with its index, so the heaviest blocks are dispatched
+// first and the light ones fill the tail.  Consecutive ids walk the heads, so
+// all query blocks of one head land on the same XCD (id % 8) whenever
+// B * H % 8 == 0 and share its L2 copy of K / V.
+__device__ __forceinline__ void fwd_block(int id, int BH, int nqb, bool causal, int& qb, int& bh) {
+  bh = id % BH;
+  qb = causal ? nqb - 1 - id / BH : id / BH;
+}
+
+template <int D, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 32;    // queries per workgroup
   constexpr int BN = 64;         // keys per block
-  constexpr int ST = D + 32;     // LDS row stride (elements)
   constexpr int NKS = D / 16;    // MFMA k-steps over D
   constexpr int NDT = D / 32;    // 32-wide output tiles over D
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * ST];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * ST];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * D];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * D];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int qb, bh;
+  fwd_block(blockIdx.x, a.B * a.H, (a.S + QB - 1) / QB, CAUSAL, qb, bh);
+  const int b = bh / a.H, h = bh % a.H;
   const int hk = h / (a.H / a.Hkv);
-  const int q0w = blockIdx.x * 128 + wave * 32;
+  const int q0w = qb * QB + wave * 32;
   const int qrow = q0w + r32;  // this lane's query row
   const bf16* qbase = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)h * D;
   const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
@@ -142,20 +192,20 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   f32x16 oacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) oacc[dt] = splat16(0.f);
-  float m = kNegBig, l = 0.f;
+  float m = kNegBig, l = 0.f;   // running max (scaled, log2 domain) and sum
   const float c = a.scale * kLog2e;
 
-  const int kv_end = CAUSAL ? min((int)blockIdx.x * 128 + 128, a.S) : a.S;
+  const int kv_end = CAUSAL ? min(qb * QB + QB, a.S) : a.S;
   const int nblk = (kv_end + BN - 1) / BN;
-  TileRegs<BN, D> kr, vr;
+  TileRegs<BN, D, NT> kr, vr;
   tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
   tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
   for (int j = 0; j < nblk; ++j) {
     const int buf = j & 1;
-    tile_store<BN, D, ST>(kr, Ks[buf], tid);
-    tile_store<BN, D, ST>(vr, Vs[buf], tid);
+    tile_store(kr, Ks[buf], tid);
+    tile_store(vr, Vs[buf], tid);
     __syncthreads();
-    if (j + 1 < nblk) {
+    if (j + 1 < nblk) {  // next tile's HBM latency hides behind this tile's MFMAs
       tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
       tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
     }
@@ -163,51 +213,52 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
     const bf16* Kb = Ks[buf];
     const bf16* Vb = Vs[buf];
-    // ---- S^T tiles: rows = keys k0 + t*32 + row, cols = this wave's queries ----
+    // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
     f32x16 st[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       st[t] = splat16(0.f);
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
-        st[t] = mfma32x32x16(kf, qf[ks], st[t]);
-      }
+      for (int ks = 0; ks < NKS; ++ks) st[t] = mfma32x32x16(row_frag<D>(Kb, t * 32 + r32, ks, hh), qf[ks], st[t]);
     }
-    // ---- scale, mask, online softmax (per-lane query row) ----
+    // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
     const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
-    float mblk = kNegBig;
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + t * 32 + mfma32_row(i, lane);
+          if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
+        }
+    }
+    float mblk = st[0][0];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float s = st[t][i] * c;
-        if (need_mask) {
-          const int key = k0 + t * 32 + mfma32_row(i, lane);
-          s = (key >= a.S || (CAUSAL && key > qrow)) ? kNegBig : s;
-        }
-        st[t][i] = s;
-        mblk = fmaxf(mblk, s);
-      }
+      for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
     mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
-    const float mnew = fmaxf(m, mblk);
-    const float alpha = fexp2(m - mnew);
+    const float mnew = fmaxf(m, mblk * c);
+    // rescale O and l only when some row's max moved (exact; no threshold)
+    if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+      const float alpha = fexp2(m - mnew);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      m = mnew;
+    }
     float lsum = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = fexp2(st[t][i] - mnew);
+        const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
         st[t][i] = p;
         lsum += p;
       }
-    lsum += __shfl_xor(lsum, 32, kWave);
-    l = l * alpha + lsum;
-    m = mnew;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+    l += lsum + __shfl_xor(lsum, 32, kWave);
     // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -217,7 +268,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<ST>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
+        for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
       }
   }
   // ---- epilogue: O = O^T^T / l ; LSE ----
@@ -264,11 +315,10 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a) {
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int BM = 32;        // query rows per slice
-  constexpr int ST = D + 32;    // LDS row stride (elements)
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * ST];
-  __shared__ __attribute__((aligned(16))) bf16 dOs[2][BM * ST];
+  __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * D];
+  __shared__ __attribute__((aligned(16))) bf16 dOs[2][BM * D];
   __shared__ __attribute__((aligned(16))) float rc[2][2][BM];  // [buf][-lse/scale | -delta][q]
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -301,7 +351,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   const int qstart = CAUSAL ? kblk0 : 0;
   const int nslice = (a.S - qstart + BM - 1) / BM;
   const int total = nslice * group;
-  TileRegs<BM, D> qr, dr;
+  TileRegs<BM, D, 256> qr, dr;
   float rcv = 0.f;
   auto load = [&](int it) {
     const int hq = hk * group + it / nslice;
@@ -318,8 +368,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   load(0);
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
-    tile_store<BM, D, ST>(qr, Qs[buf], tid);
-    tile_store<BM, D, ST>(dr, dOs[buf], tid);
+    tile_store(qr, Qs[buf], tid);
+    tile_store(dr, dOs[buf], tid);
     if (tid < 2 * BM) rc[buf][tid >> 5][tid & (BM - 1)] = rcv;
     __syncthreads();
     if (it + 1 < total) load(it + 1);
@@ -337,8 +387,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qb + r32 * ST + ks * 16 + hh * 8);
-      const bf16x8 da = *reinterpret_cast<const bf16x8*>(Db + r32 * ST + ks * 16 + hh * 8);
+      const bf16x8 qa = row_frag<D>(Qb, r32, ks, hh);
+      const bf16x8 da = row_frag<D>(Db, r32, ks, hh);
       s = mfma32x32x16(qa, kf[ks], s);
       dp = mfma32x32x16(da, vf[ks], dp);
     }
@@ -361,8 +411,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        dvacc[dt] = mfma32x32x16(tr_frag<ST>(Db, 0, dt * 32, st, lane), pb, dvacc[dt]);
-        dkacc[dt] = mfma32x32x16(tr_frag<ST>(Qb, 0, dt * 32, st, lane), db, dkacc[dt]);
+        dvacc[dt] = mfma32x32x16(tr_frag<D>(Db, 0, dt * 32, st, lane), pb, dvacc[dt]);
+        dkacc[dt] = mfma32x32x16(tr_frag<D>(Qb, 0, dt * 32, st, lane), db, dkacc[dt]);
       }
     }
   }
@@ -388,11 +438,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int BN = 64;
-  constexpr int ST = D + 32;
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * ST];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * ST];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * D];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * D];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -427,13 +476,13 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 
   const int kv_end = CAUSAL ? min((int)blockIdx.x * 128 + 128, a.S) : a.S;
   const int nblk = (kv_end + BN - 1) / BN;
-  TileRegs<BN, D> kr, vr;
+  TileRegs<BN, D, 256> kr, vr;
   tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
   tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
   for (int j = 0; j < nblk; ++j) {
     const int buf = j & 1;
-    tile_store<BN, D, ST>(kr, Ks[buf], tid);
-    tile_store<BN, D, ST>(vr, Vs[buf], tid);
+    tile_store(kr, Ks[buf], tid);
+    tile_store(vr, Vs[buf], tid);
     __syncthreads();
     if (j + 1 < nblk) {
       tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
@@ -451,8 +500,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       f32x16 s = splat16(s_init), dp = splat16(dp_init);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(Kb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
-        const bf16x8 va = *reinterpret_cast<const bf16x8*>(Vb + (t * 32 + r32) * ST + ks * 16 + hh * 8);
+        const bf16x8 ka = row_frag<D>(Kb, t * 32 + r32, ks, hh);
+        const bf16x8 va = row_frag<D>(Vb, t * 32 + r32, ks, hh);
         s = mfma32x32x16(ka, qf[ks], s);
         dp = mfma32x32x16(va, df[ks], dp);
       }
@@ -470,7 +519,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
         for (int jj = 0; jj < 8; ++jj) db[jj] = f2bf(dp[8 * s2 + jj]);
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
-          dqacc[dt] = mfma32x32x16(tr_frag<ST>(Kb, t * 32, dt * 32, s2, lane), db, dqacc[dt]);
+          dqacc[dt] = mfma32x32x16(tr_frag<D>(Kb, t * 32, dt * 32, s2, lane), db, dqacc[dt]);
       }
     }
   }
@@ -491,11 +540,23 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 
 using namespace dta;
 
+// 8 waves (256 queries) per workgroup share each K/V tile when the grid still
+// fills the chip several times over; 4 waves otherwise (GPT-2: S = 1024).
+template <int D, int NW>
+static void fwd_launch(const AttnArgs& a, bool causal, hipStream_t st) {
+  const int nqb = (a.S + NW * 32 - 1) / (NW * 32);
+  dim3 grid((unsigned)(nqb * a.B * a.H));
+  if (causal) hipLaunchKernelGGL((attn_fwd_kernel<D, true, NW>), grid, dim3(NW * 64), 0, st, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<D, false, NW>), grid, dim3(NW * 64), 0, st, a);
+}
+
 template <int D>
 static hipError_t fwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
-  dim3 grid((a.S + 127) / 128, a.B * a.H);
-  if (causal) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);
+  const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
+  const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
+  const bool eight = force ? atoi(force) == 8 : (D == 128 && wg8 >= 1024);
+  if (eight) fwd_launch<D, 8>(a, causal, st);
+  else fwd_launch<D, 4>(a, causal, st);
   return hipGetLastError();
 }
 
