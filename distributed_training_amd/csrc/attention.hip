@@ -312,9 +312,20 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a) {
   if ((tid & 7) == 0) a.delta[((int64_t)b * a.H + h) * a.S + q] = acc;
 }
 
+// Query rows per slice of the dK/dV kernel: at D = 128 the kernel runs one wave
+// per SIMD (K/V fragments + dK/dV accumulators fill the register file), so a
+// 64-row slice halves the barriers per MFMA and doubles the compute behind
+// each slice's prefetch; at D = 64 two waves per SIMD hide it with 32 rows.
+template <int D>
+struct DkdvCfg {
+  static constexpr int kBM = D == 128 ? 64 : 32;
+  static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
+};
+
 template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
-  constexpr int BM = 32;        // query rows per slice
+__global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_kernel(AttnArgs a) {
+  constexpr int BM = DkdvCfg<D>::kBM;  // query rows per slice
+  constexpr int NQT = BM / 32;         // 32-row query tiles per slice
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * D];
@@ -324,9 +335,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
-  const int bk = blockIdx.y, b = bk / a.Hkv, hk = bk % a.Hkv;
+  // key blocks in natural order = heaviest first under the causal mask;
+  // consecutive ids walk (batch, kv head)
+  const int BHk = a.B * a.Hkv;
+  const int bk = blockIdx.x % BHk, b = bk / a.Hkv, hk = bk % a.Hkv;
   const int group = a.H / a.Hkv;
-  const int kblk0 = blockIdx.x * 128;
+  const int kblk0 = (blockIdx.x / BHk) * 128;
   const int kw0 = kblk0 + wave * 32;  // this wave's first key
   const int key = kw0 + r32;          // this lane's key
   const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
@@ -359,7 +373,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
     tile_load(qr, static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, q0, a.S, tid);
     tile_load(dr, static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, q0, a.S, tid);
     if (tid < 2 * BM) {
-      const int qq = q0 + (tid & (BM - 1));
+      const int qq = q0 + tid % BM;
       const int64_t ri = ((int64_t)b * a.H + hq) * a.S + qq;
       if (tid < BM) rcv = qq < a.S ? -a.lse[ri] * inv_scale : kNegBig;  // q >= S: P = 0
       else rcv = qq < a.S ? -a.delta[ri] : 0.f;
@@ -370,49 +384,52 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
     const int buf = it & 1;
     tile_store(qr, Qs[buf], tid);
     tile_store(dr, dOs[buf], tid);
-    if (tid < 2 * BM) rc[buf][tid >> 5][tid & (BM - 1)] = rcv;
+    if (tid < 2 * BM) rc[buf][tid / BM][tid % BM] = rcv;
     __syncthreads();
     if (it + 1 < total) load(it + 1);
-    const int q0 = qstart + (it % nslice) * BM;
-    if (CAUSAL && q0 + BM - 1 < kw0) continue;  // all of this wave's keys are after the slice
+    const int q0s = qstart + (it % nslice) * BM;
+    if (CAUSAL && q0s + BM - 1 < kw0) continue;  // all of this wave's keys are after the slice
     const bf16* Qb = Qs[buf];
     const bf16* Db = dOs[buf];
-    // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
-    f32x16 s, dp;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qi = mfma32_row(i, lane);
-      s[i] = rc[buf][0][qi];
-      dp[i] = rc[buf][1][qi];
-    }
+    for (int qt = 0; qt < NQT; ++qt) {
+      const int q0 = q0s + qt * 32;
+      if (CAUSAL && NQT > 1 && q0 + 31 < kw0) continue;
+      // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
+      f32x16 s, dp;
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const bf16x8 qa = row_frag<D>(Qb, r32, ks, hh);
-      const bf16x8 da = row_frag<D>(Db, r32, ks, hh);
-      s = mfma32x32x16(qa, kf[ks], s);
-      dp = mfma32x32x16(da, vf[ks], dp);
-    }
-    const bool need_mask = CAUSAL && q0 < kw0 + 31;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float pv = fexp2(s[i] * c);
-      if (need_mask && key > q0 + mfma32_row(i, lane)) pv = 0.f;
-      s[i] = pv;             // P
-      dp[i] = pv * dp[i];    // dS (unscaled)
-    }
-    // dV^T += dO^T . P ;  dK^T += Q^T . dS
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      bf16x8 pb, db;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pb[j] = f2bf(s[8 * st + j]);
-        db[j] = f2bf(dp[8 * st + j]);
+      for (int i = 0; i < 16; ++i) {
+        const int qi = qt * 32 + mfma32_row(i, lane);
+        s[i] = rc[buf][0][qi];
+        dp[i] = rc[buf][1][qi];
       }
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        dvacc[dt] = mfma32x32x16(tr_frag<D>(Db, 0, dt * 32, st, lane), pb, dvacc[dt]);
-        dkacc[dt] = mfma32x32x16(tr_frag<D>(Qb, 0, dt * 32, st, lane), db, dkacc[dt]);
+      for (int ks = 0; ks < NKS; ++ks) {
+        s = mfma32x32x16(row_frag<D>(Qb, qt * 32 + r32, ks, hh), kf[ks], s);
+        dp = mfma32x32x16(row_frag<D>(Db, qt * 32 + r32, ks, hh), vf[ks], dp);
+      }
+      const bool need_mask = CAUSAL && q0 < kw0 + 31;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float pv = fexp2(s[i] * c);
+        if (need_mask && key > q0 + mfma32_row(i, lane)) pv = 0.f;
+        s[i] = pv;             // P
+        dp[i] = pv * dp[i];    // dS (unscaled)
+      }
+      // dV^T += dO^T . P ;  dK^T += Q^T . dS
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pb, db;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = f2bf(s[8 * st + j]);
+          db[j] = f2bf(dp[8 * st + j]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          dvacc[dt] = mfma32x32x16(tr_frag<D>(Db, qt * 32, dt * 32, st, lane), pb, dvacc[dt]);
+          dkacc[dt] = mfma32x32x16(tr_frag<D>(Qb, qt * 32, dt * 32, st, lane), db, dkacc[dt]);
+        }
       }
     }
   }
@@ -435,8 +452,16 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   }
 }
 
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
+// dQ keeps Q and dO fragments in registers: one wave per SIMD at D = 128.
+template <int D>
+struct DqCfg {
+  static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
+};
+
+template <int D, bool CAUSAL, int NW>
+__global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int QB = NW * 32;
   constexpr int BN = 64;
   constexpr int NKS = D / 16;
   constexpr int NDT = D / 32;
@@ -446,9 +471,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  int qb, bh;
+  fwd_block(blockIdx.x, a.B * a.H, (a.S + QB - 1) / QB, CAUSAL, qb, bh);
+  const int b = bh / a.H, h = bh % a.H;
   const int hk = h / (a.H / a.Hkv);
-  const int q0w = blockIdx.x * 128 + wave * 32;
+  const int q0w = qb * QB + wave * 32;
   const int qrow = q0w + r32;
   const bf16* qbase = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)h * D;
   const bf16* dobase = static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)h * D;
@@ -474,9 +501,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = splat16(0.f);
 
-  const int kv_end = CAUSAL ? min((int)blockIdx.x * 128 + 128, a.S) : a.S;
+  const int kv_end = CAUSAL ? min(qb * QB + QB, a.S) : a.S;
   const int nblk = (kv_end + BN - 1) / BN;
-  TileRegs<BN, D, 256> kr, vr;
+  TileRegs<BN, D, NT> kr, vr;
   tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
   tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
   for (int j = 0; j < nblk; ++j) {
@@ -550,28 +577,36 @@ static void fwd_launch(const AttnArgs& a, bool causal, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false, NW>), grid, dim3(NW * 64), 0, st, a);
 }
 
+static int fwd_waves(const AttnArgs& a, int D) {
+  const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
+  if (force) return atoi(force) == 8 ? 8 : 4;
+  const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
+  return D == 128 && wg8 >= 1024 ? 8 : 4;
+}
+
 template <int D>
 static hipError_t fwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
-  const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
-  const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
-  const bool eight = force ? atoi(force) == 8 : (D == 128 && wg8 >= 1024);
-  if (eight) fwd_launch<D, 8>(a, causal, st);
+  if (fwd_waves(a, D) == 8) fwd_launch<D, 8>(a, causal, st);
   else fwd_launch<D, 4>(a, causal, st);
   return hipGetLastError();
+}
+
+template <int D, int NW>
+static void dq_launch(const AttnArgs& a, bool causal, hipStream_t st) {
+  const int nqb = (a.S + NW * 32 - 1) / (NW * 32);
+  dim3 grid((unsigned)(nqb * a.B * a.H));
+  if (causal) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true, NW>), grid, dim3(NW * 64), 0, st, a);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false, NW>), grid, dim3(NW * 64), 0, st, a);
 }
 
 template <int D>
 static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.S * a.H;
   hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
-  dim3 gkv((a.S + 127) / 128, a.B * a.Hkv), gq((a.S + 127) / 128, a.B * a.H);
-  if (causal) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), gq, dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), gq, dim3(256), 0, st, a);
-  }
+  dim3 gkv((unsigned)(((a.S + 127) / 128) * a.B * a.Hkv));
+  if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
+  dq_launch<D, 4>(a, causal, st);
   return hipGetLastError();
 }
 
