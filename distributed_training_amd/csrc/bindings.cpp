@@ -750,10 +750,10 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
   a.nesterov = nesterov;
   a.maximize = maximize;
   // xinfo (DDP exchange, empty for one rank): world, rank, slot_elems, local_ll, xerr, xepoch,
-  // timeout_iters, peer_ll[0..world)
+  // timeout_iters, xmode, LL elements per rank buffer, peer_ll[0..world)
   a.world = 1;
   if (!xinfo.empty()) {
-    TORCH_CHECK(xinfo.size() >= 7 && (int64_t)xinfo.size() == 7 + xinfo[0] && xinfo[0] >= 1 && xinfo[0] <= 8,
+    TORCH_CHECK(xinfo.size() >= 9 && (int64_t)xinfo.size() == 9 + xinfo[0] && xinfo[0] >= 1 && xinfo[0] <= 8,
                 "mlp_persistent: bad exchange info");
     a.world = (int)xinfo[0];
     a.rank = (int)xinfo[1];
@@ -763,7 +763,12 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
     a.xerr = reinterpret_cast<int*>(xinfo[4]);
     a.xepoch = reinterpret_cast<int*>(xinfo[5]);
     a.timeout_iters = (int)xinfo[6];
-    for (int q = 0; q < a.world; ++q) a.peer_ll[q] = reinterpret_cast<unsigned long long*>(xinfo[7 + q]);
+    a.xmode = (int)xinfo[7];
+    TORCH_CHECK(a.xmode == 1 || a.xmode == 2, "mlp_persistent: exchange mode must be 1 (one-shot) or 2 (rs+ag)");
+    // the rs+ag form keeps its all-gather slots [2][slot] after the [2][world][slot] ones
+    TORCH_CHECK(xinfo[8] >= 2 * (a.world + (a.xmode == 2 ? 1 : 0)) * a.slot_elems,
+                "mlp_persistent: p2p buffer too small for the reduce-scatter + all-gather exchange");
+    for (int q = 0; q < a.world; ++q) a.peer_ll[q] = reinterpret_cast<unsigned long long*>(xinfo[9 + q]);
   }
   if (dbg && dbg->defined()) {
     TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= 64, "dbg: int64 [64]");

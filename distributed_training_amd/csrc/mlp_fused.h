@@ -67,6 +67,8 @@ struct MlpPArgs {
   int* xepoch;                      // exchange epoch counter (device, advanced by nsteps)
   int* xerr;                        // raised when a peer never delivered (bounded wait)
   int timeout_iters;
+  int xmode;                        // 1: one-shot (every gradient to every rank), 2: reduce-scatter to the
+                                    // owner rank (j % world) + all-gather of the summed gradient
 };
 
 }  // namespace dta

@@ -119,6 +119,71 @@ __device__ __forceinline__ void xpush(const MlpPArgs& a, unsigned ep, int off, f
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- reduce-scatter + all-gather form (xmode 2) ----
+// Pushing every gradient to every rank costs world stores per element from the
+// ONE workgroup that runs the loop -- at 8 ranks that single CU's store issue,
+// not the xGMI links, bounds the step.  In this form each gradient goes once,
+// to its owner rank (dense index j % world), into RS slot [par][src][j]; the
+// owner sums its elements in rank order (the same bits as the one-shot form)
+// and pushes the sum to every rank's AG slot [par][j]: 2 stores per element
+// per rank instead of `world`, for one more one-way hop of latency.  Slot
+// reuse is safe two epochs later for the same reason as the one-shot form.
+__device__ __forceinline__ unsigned long long ll_pack(float g, unsigned ep) {
+  return (unsigned long long)__float_as_uint(g) | ((unsigned long long)ep << 32);
+}
+
+__device__ __forceinline__ void xpush_owner(const MlpPArgs& a, unsigned ep, int j, float g) {
+  const long long slot = ((long long)(ep & 1) * a.world + a.rank) * a.slot_elems + j;
+  __hip_atomic_store(a.peer_ll[j % a.world] + slot, ll_pack(g, ep), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// bounded poll of one LL slot for tag `ep` (sticky error: see xreduce_sgd)
+__device__ __forceinline__ float ll_wait(const MlpPArgs& a, const unsigned long long* p, unsigned ep) {
+  unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  int it = 0;
+  while ((unsigned)(v >> 32) != ep) {
+    if (++it > a.timeout_iters ||
+        ((it & 1023) == 1 && __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      atomicOr(a.xerr, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  return __uint_as_float((unsigned)(v & 0xffffffffu));
+}
+
+// owner: sum the elements j = rank, rank + world, ... over the RS slots (rank
+// order) and push each sum to every rank's AG slot
+__device__ void xowner_reduce(const MlpPArgs& a, unsigned ep, int n) {
+  constexpr int U = 4;
+  const int W = a.world, par = ep & 1;
+  const unsigned long long* rs = a.local_ll + (long long)par * W * a.slot_elems;
+  const long long ag = 2LL * W * a.slot_elems + (long long)par * a.slot_elems;
+  const int nown = (n - a.rank + W - 1) / W;
+  for (int k0 = threadIdx.x; k0 < nown; k0 += kMpThreads * U) {
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    for (int q = 0; q < W; ++q)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * kMpThreads;
+        if (k < nown) acc[u] += ll_wait(a, rs + (long long)q * a.slot_elems + a.rank + (long long)k * W, ep);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * kMpThreads;
+      if (k < nown) {
+        const unsigned long long v = ll_pack(acc[u], ep);
+        for (int q = 0; q < W; ++q)
+          __hip_atomic_store(a.peer_ll[q] + ag + a.rank + (long long)k * W, v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
 // flat offset of the j-th real parameter (W1 | b1 | W2 | b2, padding skipped)
 __device__ __forceinline__ int xoff(const MlpPArgs& a, int j) {
   const int n1 = a.hidden * a.in_dim;
@@ -130,13 +195,16 @@ __device__ __forceinline__ int xoff(const MlpPArgs& a, int j) {
   return a.o_b2 + (j - a.hidden);
 }
 
-template <bool PLAIN>
+// AG: read the summed gradient of dense element j from this rank's AG slot
+// (xmode 2); otherwise sum the one-shot slots [par][q][offset] in rank order.
+template <bool PLAIN, bool AG>
 __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf, bf16* Wb, SgdH hs, int first) {
   constexpr int U = 8;  // elements per thread in flight (x world loads)
   hs.first = first;
   const int n = a.hidden * a.in_dim + 2 * a.hidden + a.out_dim;
-  const int W = a.world, par = ep & 1;
-  const unsigned long long* base = a.local_ll + (long long)par * W * a.slot_elems;
+  const int W = AG ? 1 : a.world, par = ep & 1;
+  const unsigned long long* base = AG ? a.local_ll + 2LL * a.world * a.slot_elems + (long long)par * a.slot_elems
+                                      : a.local_ll + (long long)par * W * a.slot_elems;
   for (int j0 = threadIdx.x; j0 < n; j0 += kMpThreads * U) {
     int off[U];
     float acc[U];
@@ -149,9 +217,11 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
     for (int q = 0; q < W; ++q) {  // rank order
       unsigned long long v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = __hip_atomic_load(base + (long long)q * a.slot_elems + off[u], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * kMpThreads;
+        const long long idx = AG ? (long long)(j < n ? j : n - 1) : (long long)q * a.slot_elems + off[u];
+        v[u] = __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         int it = 0;
@@ -163,8 +233,9 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
             break;
           }
           __builtin_amdgcn_s_sleep(1);
-          v[u] = __hip_atomic_load(base + (long long)q * a.slot_elems + off[u], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+          const int j = j0 + u * kMpThreads;
+          const long long idx = AG ? (long long)(j < n ? j : n - 1) : (long long)q * a.slot_elems + off[u];
+          v[u] = __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         acc[u] += __uint_as_float((unsigned)(v[u] & 0xffffffffu));
       }
@@ -390,7 +461,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
         if (lane == 0) {
           if (multi) {
-            xpush(a, xe0 + s + 1, a.o_b2 + o, db);
+            if (a.xmode == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
+            else xpush(a, xe0 + s + 1, a.o_b2 + o, db);
           } else {
             SgdH hs = hbase;
             hs.first = first;
@@ -463,9 +535,18 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         if (upd && multi) {
           // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
           const unsigned ep = xe0 + s + 1;
+          if (a.xmode == 2) {
+            // dense index: W1[h][c] = h * IN + c, b1[h] = H IN + h, W2[h] = H IN + H + h
+            const int jb = c < IN ? c : H * IN + (c - IN) * H;
+            const int js = c < IN ? IN : 1;
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, from_c2 ? c2[i] : c1[i]);
+            for (int i = 0; i < 16; ++i)
+              xpush_owner(a, ep, jb + (h0 + mfma32_row(i, lane)) * js, from_c2 ? c2[i] : c1[i]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, from_c2 ? c2[i] : c1[i]);
+          }
         } else if (upd) {
 #pragma unroll
           for (int half = 0; half < 2; ++half) {  // 8 parameters at a time: all read, then all written
@@ -505,8 +586,15 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     }
     if constexpr (MULTI) {
       // all waves done reading the pre-update parameters before any update
-      lds_barrier();
-      xreduce_sgd<PLAIN>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
+      if (a.xmode == 2) {
+        // the owner sums need no LDS: start them before the barrier
+        xowner_reduce(a, xe0 + s + 1, H * IN + 2 * H + a.out_dim);
+        lds_barrier();
+        xreduce_sgd<PLAIN, true>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
+      } else {
+        lds_barrier();
+        xreduce_sgd<PLAIN, false>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
+      }
       lds_barrier();
     }
     MP_STAMP(5);

@@ -20,6 +20,7 @@ device ring and a device-side cursor walks it.
 from __future__ import annotations
 
 import logging
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -62,11 +63,16 @@ def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torc
 class FusedMLPProgram:
     """Two execution modes:
 
-    * persistent (one rank, full batches, shapes within the persistent kernel's
-      limits): ``csrc/mlp_persistent.hip`` runs up to ~1000 complete steps per
-      launch in one workgroup with the parameters resident in LDS;
-    * per-step (otherwise, and for DDP across ranks): the multi-workgroup fused
-      step kernel + gradient all-reduce, hipGraph-replayed.
+    * persistent (full batches, shapes within the persistent kernel's limits):
+      ``csrc/mlp_persistent.hip`` runs up to ~1000 complete steps per launch in
+      one workgroup with the parameters resident in LDS; across ranks the
+      gradients are exchanged inside the loop through IPC-mapped LL slots
+      (one-shot, or reduce-scatter + all-gather);
+    * per-step (otherwise): the multi-workgroup fused step kernel + gradient
+      all-reduce, hipGraph-replayed.
+
+    With several ranks the form is chosen by timing all of them on the node
+    (``DTA_MLP_XMODE=auto``, the default; or force oneshot / rsag / step).
     """
 
     def __init__(self, module, optimizer, loader, comm, loss: str = "mse", graph_steps: int = 32,
@@ -100,8 +106,6 @@ class FusedMLPProgram:
         self.X = self.X.float().contiguous()
         self.Y = self.Y.float().contiguous()
         self.steps_per_epoch = S = max(1, len(loader))
-        import os
-
         full_batches = len(loader.sampler) % self.B == 0
         if persistent is None:
             persistent = os.environ.get("DTA_MLP_PERSISTENT", "1") != "0"
@@ -109,21 +113,54 @@ class FusedMLPProgram:
             module.input_size, H, module.output_size, self.B, momentum=bool(self.hyper()["momentum"])))
         self._p2p = None
         self._xinfo = None
+        self._xinfos = {}
         self.xepoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        # DDP across ranks: the persistent loop's in-kernel exchange ("oneshot" |
+        # "rsag"), the per-step program ("step": multi-workgroup step kernel +
+        # all-reduce), or "auto": all are timed on this node at construction and
+        # every rank takes the fastest (xGMI latency and the store rate of the
+        # loop's single CU decide it; neither is knowable off the target node)
+        self.xmode = os.environ.get("DTA_MLP_XMODE", "auto")
+        if self.xmode not in ("auto", "step", *mf.XMODES):
+            raise ValueError(f"DTA_MLP_XMODE={self.xmode!r}")
+        if self.xmode == "step" and self.ws > 1:
+            self.persistent = False
+        auto_x = self.xmode == "auto"
+        if auto_x:
+            self.xmode = "oneshot"
         if self.persistent and self.ws > 1:
             self.persistent = self._setup_exchange()
         self.chunk_steps = 1024
         # index ring: whole epochs, at least one graph (or one persistent launch)
         # beyond an epoch, so uploads for epoch e+1 can be enqueued while epoch
         # e's steps are still queued
-        ahead = self.chunk_steps if self.persistent else 2 * self.graph_steps
+        ahead = self.chunk_steps if self.persistent else 2 * self.graph_steps  # (covers both modes)
         k = max(2, -(-ahead // S) + 1)
         self.R = S * k
         self.ring = torch.zeros(self.R, self.B, dtype=torch.int32, device=dev)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.stage = mf.make_stage(dev)
-        self.staged = False        # staging slot `parity` holds the batch of step `launched`
         self.loss_ring = torch.zeros(loss_len, device=dev)
+        self._staging: List = []   # (pinned tensor, event) kept alive until the copy ran
+        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.loss_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
+        self.Xp = mf.pad_features(self.X) if self.persistent else None
+        self._reset_state()
+        if auto_x and self.persistent and self.ws > 1:
+            self._calibrate_exchange()
+
+    def _reset_state(self) -> None:
+        """Training state back to step 0 with the module's weights (the module
+        itself is only written by :meth:`store_to_module`)."""
+        for t in (*self.P, *self.G, *(m for m in self.M if m is not None)):
+            t.zero_()
+        self.ring.zero_()
+        self.cursor.zero_()
+        self.loss_ring.zero_()
+        self.loss_cursor.zero_()
+        self.mom_started_dev.zero_()
+        self.staged = False        # staging slot `parity` holds the batch of step `launched`
         self.parity = 0
         self.pending = False
         self.mom_started = False
@@ -131,12 +168,46 @@ class FusedMLPProgram:
         self.host_step = 0         # global steps whose indices are uploaded
         self.next_epoch = 0        # next epoch to upload
         self._batch_of: Dict[int, int] = {}
-        self._staging: List = []   # (pinned tensor, event) kept alive until the copy ran
-        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
-        self.loss_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
-        self.Xp = mf.pad_features(self.X) if self.persistent else None
         self.load_from_module()
+
+    def _calibrate_exchange(self, steps: int = 256) -> None:
+        """Time both exchange forms of the persistent loop on this node (xGMI
+        topology, store issue rate of one CU) and keep the faster; every rank
+        takes the same decision (MAX over ranks of each time).  The probe steps
+        are discarded: the state is reset to step 0 afterwards."""
+        import torch.distributed as dist
+
+        times = {}
+        can_step = hasattr(self.comm, "all_reduce_inline") or hasattr(self.comm, "all_reduce")
+        for mode in (*mf.XMODES, *(("step",) if can_step else ())):
+            self.persistent = mode != "step"
+            if self.persistent:
+                self.xmode = mode
+                self._xinfo = self._xinfos[mode]
+            self._reset_state()
+            self.run_steps(2 * self.graph_steps + 8)  # warm (first touch of the slots, graph capture)
+            torch.cuda.synchronize(self.device)
+            dist.barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.run_steps(steps)
+            e1.record()
+            torch.cuda.synchronize(self.device)
+            t = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64,
+                             device=self.device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            times[mode] = float(t.item())
+        self._p2p.check()
+        best = min(times, key=times.get)
+        self.persistent = best != "step"
+        self.xmode = best
+        if self.persistent:
+            self._xinfo = self._xinfos[best]
+        self.exchange_times_ms = times
+        logger.info("MLP DDP step form: %s (%s)", self.xmode,
+                    ", ".join(f"{m} {v / steps * 1e3:.2f} us/step" for m, v in times.items()))
+        torch.cuda.synchronize(self.device)
+        self._reset_state()
 
     def _setup_exchange(self) -> bool:
         """DDP across ranks inside the persistent loop: a dedicated p2p buffer set
@@ -151,8 +222,10 @@ class FusedMLPProgram:
         p2p = None
         if ok:
             try:
+                # [2][world][total] one-shot / reduce-scatter slots + [2][total] all-gather slots
+                T = self.layout.total
                 p2p = P2PAllReduce(self.comm.rank, self.ws, self.device, dist.distributed_c10d._get_default_store(),
-                                   tag="fused_mlp", max_elems=self.layout.total)
+                                   tag="fused_mlp", max_elems=T + -(-T // self.ws) + 64)
                 # the kernel pushes through the same peer mappings: prove them with
                 # one exchange of known values before any training step relies on them
                 n = self.layout.total
@@ -166,7 +239,8 @@ class FusedMLPProgram:
                 # the self-test left {value, tag 1} in the slots: the loop's first
                 # exchange epoch must be past it (epochs are xepoch + 1, + 2, ...)
                 self.xepoch.fill_(1)
-                self._xinfo = mf.exchange_info(p2p, self.xepoch)
+                self._xinfos = {m: mf.exchange_info(p2p, self.xepoch, T, m) for m in mf.XMODES}
+                self._xinfo = self._xinfos[self.xmode]
             except Exception as e:  # noqa: BLE001 - fall back to the per-step program
                 logger.warning("persistent DDP exchange unavailable (%s); per-step program used", e)
                 ok = 0

@@ -118,11 +118,19 @@ def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_starte
         list(xinfo) if xinfo else [])
 
 
-def exchange_info(p2p, xepoch: torch.Tensor, timeout_iters: int = 1 << 24):
+XMODES = {"oneshot": 1, "rsag": 2}
+
+
+def exchange_info(p2p, xepoch: torch.Tensor, slot_elems: int, mode: str = "oneshot",
+                  timeout_iters: int = 1 << 24):
     """Flatten a :class:`~..parallel.p2p.P2PAllReduce` (dedicated to this loop) into the
-    kernel's exchange descriptor."""
+    kernel's exchange descriptor.  ``slot_elems``: slot stride (>= the parameter count);
+    ``mode``: "oneshot" (every gradient to every rank) or "rsag" (reduce-scatter to an
+    owner rank + all-gather of the sums; needs 2 (world + 1) slots per rank)."""
     peers, local, rank, world, slot, err, _ = p2p._h.ll_info()
-    return [world, rank, slot, local, err, xepoch.data_ptr(), int(timeout_iters)] + list(peers)
+    cap = 2 * world * slot  # LL elements per rank's buffer
+    return [world, rank, int(slot_elems), local, err, xepoch.data_ptr(), int(timeout_iters), XMODES[mode],
+            cap] + list(peers)
 
 
 STAGE_ROWS, STAGE_COLS = 128, 32

@@ -26,6 +26,8 @@ class P2PAllReduce:
     store (an empty value if allocation failed) before anything can raise, so
     no rank is left waiting on a key that never appears."""
 
+    _seq: dict = {}
+
     def __init__(self, rank: int, world_size: int, device: torch.device, store, tag: str = "default",
                  max_elems: int = DEFAULT_MAX_ELEMS, timeout_iters: int = DEFAULT_TIMEOUT_ITERS,
                  protocol: str = "ll"):
@@ -33,7 +35,12 @@ class P2PAllReduce:
 
         self.rank, self.world_size, self.device = rank, world_size, device
         self.timeout_iters = int(timeout_iters)
-        key = f"dta_p2p/{tag}"
+        # one store key per construction: every rank builds its buffers in the same
+        # order, so the n-th construction with a tag agrees across ranks (a reused
+        # key could hand a peer the previous buffer's handle)
+        seq = P2PAllReduce._seq.get(tag, 0)
+        P2PAllReduce._seq[tag] = seq + 1
+        key = f"dta_p2p/{tag}/{seq}"
         self._h = None
         err = None
         try:

@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 
-def worker(rank, ws, port, steps, q):
+def worker(rank, ws, port, steps, with_comm, q):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": str(ws),
                        "LOCAL_WORLD_SIZE": str(ws)})
     dist.init_process_group("gloo", rank=rank, world_size=ws)
@@ -34,7 +34,17 @@ def worker(rank, ws, port, steps, q):
     model = MLP(20, 512, 1).to(dev)
     opt = FusedSGD(model.parameters(), lr=1e-3)
     loader = DeviceDataLoader(ds, 32, sampler=DistributedSampler(ds, num_replicas=ws, rank=rank), device=dev)
-    prog = FusedMLPProgram(model, opt, loader, types.SimpleNamespace(world_size=ws, rank=rank), loss="mse")
+    comm = types.SimpleNamespace(world_size=ws, rank=rank)
+    if with_comm:
+        # the per-step program's all-reduce: the one-shot p2p kernel the RCCL
+        # communicator routes small fp32 buckets to (RCCL itself refuses two
+        # ranks on one GPU)
+        from distributed_training_amd.parallel.p2p import P2PAllReduce
+
+        p2p = P2PAllReduce(rank, ws, dev, dist.distributed_c10d._get_default_store(), tag="bench_comm")
+        comm.all_reduce_inline = lambda t, op="sum", stream=None: p2p.all_reduce(t, 1.0, stream=stream)
+        comm.check_errors = p2p.check
+    prog = FusedMLPProgram(model, opt, loader, comm, loss="mse")
     prog.run_steps(256)
     torch.cuda.synchronize()
     dist.barrier()
@@ -45,7 +55,8 @@ def worker(rank, ws, port, steps, q):
     dist.barrier()
     prog.store_to_module()
     if rank == 0:
-        q.put({"procs": ws, "persistent": prog.persistent, "us_per_step": dt / steps * 1e6})
+        q.put({"procs": ws, "persistent": prog.persistent, "xmode": prog.xmode, "us_per_step": dt / steps * 1e6,
+               "calibration_ms": getattr(prog, "exchange_times_ms", None)})
     dist.destroy_process_group()
 
 
@@ -53,6 +64,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=2)
     ap.add_argument("--steps", type=int, default=4096)
+    ap.add_argument("--comm", action="store_true", help="give the program an all-reduce (enables the per-step form)")
     a = ap.parse_args()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -60,7 +72,7 @@ def main():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    ps = [ctx.Process(target=worker, args=(r, a.procs, port, a.steps, q)) for r in range(a.procs)]
+    ps = [ctx.Process(target=worker, args=(r, a.procs, port, a.steps, a.comm, q)) for r in range(a.procs)]
     for p in ps:
         p.start()
     for p in ps:

@@ -22,26 +22,38 @@ def _worker(rank, ws, steps, momentum):
     from distributed_training_amd.ops.optim import FusedSGD
     from distributed_training_amd.parallel.sampler import DistributedSampler
 
+    import os
+
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    torch.manual_seed(0)
     ds = MyTrainDataset(256 * ws, 20, 1, seed=0)
-    model = MLP(20, 512, 1).to(dev)
-    init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    opt = FusedSGD(model.parameters(), lr=0.05, momentum=momentum)
     sampler = DistributedSampler(ds, num_replicas=ws, rank=rank, seed=5)
-    loader = DeviceDataLoader(ds, 32, sampler=sampler, device=dev)
-    comm = types.SimpleNamespace(world_size=ws, rank=rank)
-    prog = FusedMLPProgram(model, opt, loader, comm, loss="mse")
-    assert prog.persistent and prog._xinfo is not None
-    prog.run_steps(steps)
-    prog.store_to_module()
-    torch.cuda.synchronize()
-    final = torch.cat([p.detach().float().reshape(-1).cpu() for p in model.parameters()])
-    gathered = [torch.empty_like(final) for _ in range(ws)]
-    dist.all_gather(gathered, final)
-    for g in gathered[1:]:
-        assert torch.equal(g, gathered[0]), "replicas diverged"
+    finals = {}
+    for mode in ("oneshot", "rsag", "auto"):
+        os.environ["DTA_MLP_XMODE"] = mode
+        torch.manual_seed(0)
+        model = MLP(20, 512, 1).to(dev)
+        init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        opt = FusedSGD(model.parameters(), lr=0.05, momentum=momentum)
+        loader = DeviceDataLoader(ds, 32, sampler=sampler, device=dev)
+        comm = types.SimpleNamespace(world_size=ws, rank=rank)
+        prog = FusedMLPProgram(model, opt, loader, comm, loss="mse")
+        assert prog.persistent and prog._xinfo is not None
+        assert mode == "auto" or prog.xmode == mode
+        prog.run_steps(steps)
+        prog.store_to_module()
+        torch.cuda.synchronize()
+        final = torch.cat([p.detach().float().reshape(-1).cpu() for p in model.parameters()])
+        gathered = [torch.empty_like(final) for _ in range(ws)]
+        dist.all_gather(gathered, final)
+        for g in gathered[1:]:
+            assert torch.equal(g, gathered[0]), f"replicas diverged ({mode})"
+        finals[mode] = final
+    # both exchange forms sum in rank order: bit-identical training; auto (after
+    # its discarded calibration steps) restarts from step 0 and matches too
+    assert torch.equal(finals["oneshot"], finals["rsag"])
+    assert torch.equal(finals["auto"], finals["oneshot"])
+    final = finals["oneshot"]
     if rank == 0:
         # fp32 DDP reference over the same per-rank batches
         ref = MLP(20, 512, 1)
@@ -64,6 +76,6 @@ def _worker(rank, ws, steps, momentum):
         assert err < 2e-2 * max(1.0, want.abs().max().item()), err
 
 
-@pytest.mark.parametrize("ws,momentum", [(2, 0.0), (2, 0.9), (4, 0.0)])
+@pytest.mark.parametrize("ws,momentum", [(2, 0.0), (2, 0.9), (3, 0.0), (4, 0.9)])
 def test_persistent_ddp_exchange_multi_process(ws, momentum):
     run_gloo(_worker, ws, 40, momentum)
