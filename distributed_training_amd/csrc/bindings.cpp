@@ -57,6 +57,7 @@ void dta_p2p_destroy(void*);
 void dta_p2p_set_ll(void*, int);
 hipError_t dta_p2p_ll_info(void*, unsigned long long*, unsigned long long*, int*, int*, long long*,
                            unsigned long long*, unsigned long long*);
+hipError_t dta_p2p_regions(void*, unsigned long long*, long long*, unsigned long long*, long long*);
 
 namespace {
 
@@ -674,6 +675,13 @@ class PyP2PAllReduce {
   int64_t max_elems() const { return max_elems_; }
   void set_ll(bool ll) { dta_p2p_set_ll(state_, ll ? 1 : 0); }
   // (peer LL slot pointers, local LL pointer, rank, world, slot elems, err ptr, spare counter ptr)
+  py::tuple regions() const {
+    unsigned long long data = 0, flags = 0;
+    long long db = 0, fb = 0;
+    hip_ok(dta_p2p_regions(state_, &data, &db, &flags, &fb), "p2p regions");
+    return py::make_tuple((int64_t)data, (int64_t)db, (int64_t)flags, (int64_t)fb);
+  }
+
   py::tuple ll_info() const {
     unsigned long long peers[8] = {}, local = 0, err = 0, ctr = 0;
     int rank = 0, world = 0;
@@ -753,7 +761,8 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
   // timeout_iters, xmode, LL elements per rank buffer, peer_ll[0..world)
   a.world = 1;
   if (!xinfo.empty()) {
-    TORCH_CHECK(xinfo.size() >= 9 && (int64_t)xinfo.size() == 9 + xinfo[0] && xinfo[0] >= 1 && xinfo[0] <= 8,
+    TORCH_CHECK(xinfo.size() >= 9 && xinfo[0] >= 1 && xinfo[0] <= 8 &&
+                    (int64_t)xinfo.size() == 9 + xinfo[0] + (xinfo[7] == 3 ? 6 : 0),
                 "mlp_persistent: bad exchange info");
     a.world = (int)xinfo[0];
     a.rank = (int)xinfo[1];
@@ -764,11 +773,26 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
     a.xepoch = reinterpret_cast<int*>(xinfo[5]);
     a.timeout_iters = (int)xinfo[6];
     a.xmode = (int)xinfo[7];
-    TORCH_CHECK(a.xmode == 1 || a.xmode == 2, "mlp_persistent: exchange mode must be 1 (one-shot) or 2 (rs+ag)");
+    TORCH_CHECK(a.xmode >= 1 && a.xmode <= 3, "mlp_persistent: exchange mode 1 (one-shot), 2 (rs+ag), 3 (helpers)");
     // the rs+ag form keeps its all-gather slots [2][slot] after the [2][world][slot] ones
     TORCH_CHECK(xinfo[8] >= 2 * (a.world + (a.xmode == 2 ? 1 : 0)) * a.slot_elems,
                 "mlp_persistent: p2p buffer too small for the reduce-scatter + all-gather exchange");
     for (int q = 0; q < a.world; ++q) a.peer_ll[q] = reinterpret_cast<unsigned long long*>(xinfo[9 + q]);
+    if (a.xmode == 3) {
+      // helpers: xg_out, xg_red ([2][xe] fp32), xready [2], xdone [nh] (int32), nh, xe
+      const size_t o = 9 + a.world;
+      a.xg_out = reinterpret_cast<float*>(xinfo[o]);
+      a.xg_red = reinterpret_cast<float*>(xinfo[o + 1]);
+      a.xready = reinterpret_cast<int*>(xinfo[o + 2]);
+      a.xdone = reinterpret_cast<int*>(xinfo[o + 3]);
+      a.nh = (int)xinfo[o + 4];
+      a.xe = (int)xinfo[o + 5];
+      const int nt = (int)(hidden / 32);
+      TORCH_CHECK(a.nh >= 1 && a.nh <= 255 && a.xe >= nt * 1024 + out_dim && a.slot_elems >= a.xe &&
+                      (a.xe + a.nh - 1) / a.nh <= 4 * 512,
+                  "mlp_persistent: helper exchange geometry (nh in [1, 255], xe >= hidden * 32 + out, "
+                  "slots >= xe, <= 2048 elements per helper)");
+    }
   }
   if (dbg && dbg->defined()) {
     TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= 64, "dbg: int64 [64]");
@@ -840,6 +864,7 @@ PYBIND11_MODULE(_C, m) {
       .def("destroy", &PyP2PAllReduce::destroy)
       .def("set_ll", &PyP2PAllReduce::set_ll)
       .def("ll_info", &PyP2PAllReduce::ll_info)
+      .def("regions", &PyP2PAllReduce::regions)
       .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())

@@ -68,7 +68,15 @@ struct MlpPArgs {
   int* xerr;                        // raised when a peer never delivered (bounded wait)
   int timeout_iters;
   int xmode;                        // 1: one-shot (every gradient to every rank), 2: reduce-scatter to the
-                                    // owner rank (j % world) + all-gather of the summed gradient
+                                    // owner rank (j % world) + all-gather of the summed gradient,
+                                    // 3: helper workgroups run the one-shot exchange (grid 1 + nh)
+  // xmode 3: gradients leave the loop's CU once (xg_out, fragment order), nh helper
+  // workgroups push / reduce them across ranks on their own CUs, sums come back in xg_red
+  float* xg_out;                    // [2][xe]
+  float* xg_red;                    // [2][xe]
+  int* xready;                      // [2] epoch of the gradients in xg_out[parity]
+  int* xdone;                       // [nh] epoch each helper finished
+  int nh, xe;
 };
 
 }  // namespace dta

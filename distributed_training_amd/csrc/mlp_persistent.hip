@@ -264,6 +264,89 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
   }
 }
 
+// ---- helper-workgroup exchange (xmode 3) ----
+// The loop's single CU issues every global access of the exchange itself in
+// the other forms, and one CU's load/store rate (not xGMI) then sets the step
+// time.  Here the loop writes its gradients ONCE (fp32, fragment order: tile,
+// accumulator register, lane -- 256 contiguous bytes per wave-instruction)
+// and releases them with a flag; nh helper workgroups on other CUs each take a
+// slice, push it to every rank's LL slots, sum the world slices in rank order
+// and hand the sums back through xg_red + a per-helper flag.  Gradient bytes
+// through the loop's CU per step: 2 x 64 KB, whatever the world size.
+// Visibility: every access to the hand-off bytes and flags is a system-scope
+// (sc1) load / store -- the per-XCD L2s are not coherent with each other, and
+// the loop and a helper may sit on different XCDs -- in the p2p buffer's
+// uncached regions: writer waves drain vmcnt, barrier, then the flag store;
+// the reader issues its loads only after the poll returned.  No L2 write-back
+// or invalidate per step (an acquire in the poll loop would invalidate L2 on
+// every iteration).
+__device__ __forceinline__ float ld_sc(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sc(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool flag_wait(const MlpPArgs& a, const int* f, int ep) {
+  int it = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != ep) {
+    if (++it > a.timeout_iters ||
+        ((it & 1023) == 1 && __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      atomicOr(a.xerr, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+__device__ void helper_loop(const MlpPArgs& a, unsigned xe0) {
+  const int h = blockIdx.x - 1, tid = threadIdx.x;
+  const int chunk = (a.xe + a.nh - 1) / a.nh;
+  const int e0 = h * chunk, e1 = min(a.xe, e0 + chunk);
+  const int W = a.world;
+  constexpr int U = 4;  // elements per thread (the host keeps chunk <= U * kMpThreads)
+  for (int s = 0; s < a.nsteps; ++s) {
+    const unsigned ep = xe0 + s + 1;
+    const int par = ep & 1;
+    if (tid == 0) flag_wait(a, a.xready + par, (int)ep);
+    __syncthreads();
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + tid + u * kMpThreads;
+      v[u] = e < e1 ? ld_sc(a.xg_out + (long long)par * a.xe + e) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + tid + u * kMpThreads;
+      if (e < e1) {
+        const unsigned long long pv = ll_pack(v[u], ep);
+        const long long slot = ((long long)par * W + a.rank) * a.slot_elems + e;
+        for (int q = 0; q < W; ++q)
+          __hip_atomic_store(a.peer_ll[q] + slot, pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    const unsigned long long* base = a.local_ll + (long long)par * W * a.slot_elems;
+    for (int q = 0; q < W; ++q)  // rank order: the same bits on every rank
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + tid + u * kMpThreads;
+        if (e < e1) acc[u] += ll_wait(a, base + (long long)q * a.slot_elems + e, ep);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + tid + u * kMpThreads;
+      if (e < e1) st_sc(a.xg_red + (long long)par * a.xe + e, acc[u]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.xdone + h, (int)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // OUT: output width, TPW: hidden tiles per wave (H <= 256 TPW), PLAIN: SGD
 // without momentum / weight decay / maximize (the update is p -= lr * g)
 template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
@@ -275,6 +358,10 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   const int r32 = lane & 31, hh = lane >> 5;
   const int IN = a.in_dim, H = a.hidden, B = a.B, NT = H / 32;
   const int IMG = H + kMpImgPad;  // activation image row stride (elements)
+  if (MULTI && blockIdx.x > 0) {  // xmode 3: helper workgroups (the loop is workgroup 0)
+    helper_loop(a, (unsigned)*a.xepoch);
+    return;
+  }
 
   // ---- LDS carve ----
   float* Pf = reinterpret_cast<float*>(smem);                       // [total]
@@ -461,7 +548,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
         if (lane == 0) {
           if (multi) {
-            if (a.xmode == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
+            if (a.xmode == 3) st_sc(a.xg_out + (long long)((xe0 + s + 1) & 1) * a.xe + NT * 1024 + o, db);
+            else if (a.xmode == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
             else xpush(a, xe0 + s + 1, a.o_b2 + o, db);
           } else {
             SgdH hs = hbase;
@@ -532,10 +620,15 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
         // SGD: all 16 parameters (and momenta) of this lane read first, then written
-        if (upd && multi) {
+        if (multi && (upd || a.xmode == 3)) {
           // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
           const unsigned ep = xe0 + s + 1;
-          if (a.xmode == 2) {
+          if (a.xmode == 3) {
+            // fragment order: [tile][register][lane]; lanes past the parameter columns write 0
+            float* go = a.xg_out + (long long)(ep & 1) * a.xe + (long long)t * 1024 + lane;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) st_sc(go + i * 64, upd ? (from_c2 ? c2[i] : c1[i]) : 0.f);
+          } else if (a.xmode == 2) {
             // dense index: W1[h][c] = h * IN + c, b1[h] = H IN + h, W2[h] = H IN + H + h
             const int jb = c < IN ? c : H * IN + (c - IN) * H;
             const int js = c < IN ? IN : 1;
@@ -586,7 +679,61 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     }
     if constexpr (MULTI) {
       // all waves done reading the pre-update parameters before any update
-      if (a.xmode == 2) {
+      if (a.xmode == 3) {
+        const unsigned ep = xe0 + s + 1;
+        const int par = ep & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gradient stores landed
+        lds_barrier();                                     // ... and every other wave's
+        if (tid == 0) __hip_atomic_store(a.xready + par, (int)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid < a.nh) flag_wait(a, a.xdone + tid, (int)ep);
+        __syncthreads();
+        // SGD from the summed gradients (same lane <-> parameter map as one rank)
+        const float* gr = a.xg_red + (long long)par * a.xe;
+        SgdH hs2 = hbase;
+        hs2.first = first;
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt) {
+          const int t = wave + kMpWaves * tt;
+          if (t < NT && upd) {
+            const int h0 = t * 32;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              float pv[8], mv[8], gv[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int i = 8 * half + u;
+                const int off = pbase + (h0 + mfma32_row(i, lane)) * pstride;
+                gv[u] = ld_sc(gr + (long long)t * 1024 + i * 64 + lane);
+                pv[u] = Pf[off];
+                mv[u] = PLAIN ? 0.f : Mf[off];
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                float g = gv[u];
+                if (!PLAIN) {
+                  if (hs2.maximize) g = -g;
+                  if (hs2.wd != 0.f) g += hs2.wd * pv[u];
+                  if (hs2.mom != 0.f) {
+                    mv[u] = hs2.first ? g : hs2.mom * mv[u] + (1.f - hs2.damp) * g;
+                    g = hs2.nesterov ? g + hs2.mom * mv[u] : mv[u];
+                  }
+                }
+                pv[u] -= hs2.lr * g;
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int hrow = h0 + mfma32_row(8 * half + u, lane);
+                const int off = pbase + hrow * pstride;
+                Pf[off] = pv[u];
+                if (!PLAIN && hs2.mom != 0.f) Mf[off] = mv[u];
+                if (c < IN) Wb[hrow * 32 + c] = f2bf(pv[u]);
+              }
+            }
+          }
+        }
+        if (tid < a.out_dim) sgd_apply(Pf + a.o_b2 + tid, Mf + a.o_b2 + tid, ld_sc(gr + NT * 1024 + tid), hs2);
+        lds_barrier();
+      } else if (a.xmode == 2) {
         // the owner sums need no LDS: start them before the barrier
         xowner_reduce(a, xe0 + s + 1, H * IN + 2 * H + a.out_dim);
         lds_barrier();
@@ -595,7 +742,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         lds_barrier();
         xreduce_sgd<PLAIN, false>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
       }
-      lds_barrier();
+      if (a.xmode != 3) lds_barrier();
     }
     MP_STAMP(5);
     first = 0;
@@ -629,7 +776,8 @@ template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
 static hipError_t mp_launch(const MlpPArgs& a, size_t lds, hipStream_t st) {
   auto k = &mlp_persistent_kernel<ACT, OUT, TPW, PLAIN, MULTI>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k, dim3(1), dim3(kMpThreads), lds, st, a);
+  const int grid = (MULTI && a.xmode == 3) ? 1 + a.nh : 1;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMpThreads), lds, st, a);
   return hipGetLastError();
 }
 

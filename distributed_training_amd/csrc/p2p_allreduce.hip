@@ -265,6 +265,20 @@ hipError_t dta_p2p_ll_info(void* state, unsigned long long* peer_ll, unsigned lo
   return hipSuccess;
 }
 
+// This rank's uncached (fine-grained, MTYPE UC) data and flag regions, for
+// kernels that hand data between workgroups of one GPU through them with plain
+// stores + s_waitcnt + relaxed flag atomics (no L2 write-back / invalidate):
+// the persistent MLP loop's helper exchange.  Unused by the LL protocol.
+hipError_t dta_p2p_regions(void* state, unsigned long long* data, long long* data_bytes, unsigned long long* flags,
+                           long long* flags_bytes) {
+  auto* s = static_cast<P2PState*>(state);
+  *data = reinterpret_cast<unsigned long long>(s->buf);
+  *data_bytes = (long long)2 * s->world * s->max_elems * (long long)sizeof(float);
+  *flags = reinterpret_cast<unsigned long long>(s->buf + s->flags_off);
+  *flags_bytes = (long long)2 * kP2PMaxWG * s->world * (long long)sizeof(int);
+  return hipSuccess;
+}
+
 int dta_p2p_num_wg(int64_t n) {
   // ~2048 elements (8 KiB) per workgroup: enough memory-level parallelism per
   // link without spreading a 45 KB bucket over more flag round trips

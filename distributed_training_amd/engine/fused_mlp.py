@@ -116,7 +116,7 @@ class FusedMLPProgram:
         self._xinfos = {}
         self.xepoch = torch.zeros(1, dtype=torch.int32, device=dev)
         # DDP across ranks: the persistent loop's in-kernel exchange ("oneshot" |
-        # "rsag"), the per-step program ("step": multi-workgroup step kernel +
+        # "rsag" | "helpers"), the per-step program ("step": multi-workgroup step kernel +
         # all-reduce), or "auto": all are timed on this node at construction and
         # every rank takes the fastest (xGMI latency and the store rate of the
         # loop's single CU decide it; neither is knowable off the target node)
@@ -179,7 +179,7 @@ class FusedMLPProgram:
 
         times = {}
         can_step = hasattr(self.comm, "all_reduce_inline") or hasattr(self.comm, "all_reduce")
-        for mode in (*mf.XMODES, *(("step",) if can_step else ())):
+        for mode in (*self._xinfos, *(("step",) if can_step else ())):
             self.persistent = mode != "step"
             if self.persistent:
                 self.xmode = mode
@@ -222,8 +222,11 @@ class FusedMLPProgram:
         p2p = None
         if ok:
             try:
-                # [2][world][total] one-shot / reduce-scatter slots + [2][total] all-gather slots
-                T = self.layout.total
+                # [2][world][slot] one-shot / reduce-scatter slots + [2][slot] all-gather slots;
+                # the slot covers the parameters and the helper form's fragment-order array
+                L = self.layout
+                XE = mf.helper_elems(L.hidden, L.out_dim)
+                T = max(L.total, XE)
                 p2p = P2PAllReduce(self.comm.rank, self.ws, self.device, dist.distributed_c10d._get_default_store(),
                                    tag="fused_mlp", max_elems=T + -(-T // self.ws) + 64)
                 # the kernel pushes through the same peer mappings: prove them with
@@ -239,7 +242,11 @@ class FusedMLPProgram:
                 # the self-test left {value, tag 1} in the slots: the loop's first
                 # exchange epoch must be past it (epochs are xepoch + 1, + 2, ...)
                 self.xepoch.fill_(1)
-                self._xinfos = {m: mf.exchange_info(p2p, self.xepoch, T, m) for m in mf.XMODES}
+                hb = mf.helper_buffers(p2p, L.hidden, L.out_dim)
+                self._xinfos = {m: mf.exchange_info(p2p, self.xepoch, T, m, helper=hb)
+                                for m in mf.XMODES if m != "helpers" or hb is not None}
+                if self.xmode not in self._xinfos:
+                    raise RuntimeError(f"exchange form {self.xmode} unavailable")
                 self._xinfo = self._xinfos[self.xmode]
             except Exception as e:  # noqa: BLE001 - fall back to the per-step program
                 logger.warning("persistent DDP exchange unavailable (%s); per-step program used", e)

@@ -118,19 +118,42 @@ def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_starte
         list(xinfo) if xinfo else [])
 
 
-XMODES = {"oneshot": 1, "rsag": 2}
+XMODES = {"oneshot": 1, "rsag": 2, "helpers": 3}
+
+
+def helper_elems(hidden: int, out_dim: int) -> int:
+    """Exchange array of the helper form: fragment order [hidden/32 tiles][16][64] + the b2 gradients."""
+    return (hidden // 32) * 1024 + 64 * (-(-out_dim // 64))
 
 
 def exchange_info(p2p, xepoch: torch.Tensor, slot_elems: int, mode: str = "oneshot",
-                  timeout_iters: int = 1 << 24):
+                  timeout_iters: int = 1 << 24, helper=None):
     """Flatten a :class:`~..parallel.p2p.P2PAllReduce` (dedicated to this loop) into the
-    kernel's exchange descriptor.  ``slot_elems``: slot stride (>= the parameter count);
-    ``mode``: "oneshot" (every gradient to every rank) or "rsag" (reduce-scatter to an
-    owner rank + all-gather of the sums; needs 2 (world + 1) slots per rank)."""
+    kernel's exchange descriptor.  ``slot_elems``: slot stride (>= the parameter count,
+    >= the helper exchange array); ``mode``: "oneshot" (every gradient to every rank),
+    "rsag" (reduce-scatter to an owner rank + all-gather of the sums; needs 2 (world + 1)
+    slots per rank) or "helpers" (``helper`` = (xg_out, xg_red, xready, xdone, nh, xe):
+    helper workgroups run the one-shot exchange off the loop's CU)."""
     peers, local, rank, world, slot, err, _ = p2p._h.ll_info()
     cap = 2 * world * slot  # LL elements per rank's buffer
-    return [world, rank, int(slot_elems), local, err, xepoch.data_ptr(), int(timeout_iters), XMODES[mode],
+    info = [world, rank, int(slot_elems), local, err, xepoch.data_ptr(), int(timeout_iters), XMODES[mode],
             cap] + list(peers)
+    if mode == "helpers":
+        info += [int(v) for v in helper]  # xg_out, xg_red, xready, xdone (device addresses), nh, xe
+    return info
+
+
+def helper_buffers(p2p, hidden: int, out_dim: int):
+    """The helper form's hand-off buffers, carved from the p2p buffer's uncached data
+    and flag regions (unused by the LL protocol): plain stores there reach memory
+    before an s_waitcnt returns, so a relaxed flag suffices -- no L2 write-back or
+    invalidate per step.  Returns (xg_out, xg_red, xready, xdone, nh, xe)."""
+    xe = helper_elems(hidden, out_dim)
+    nh = max(1, min(64, -(-xe // 512)))  # ~512 elements (one per thread) per helper
+    data, dbytes, flags, fbytes = p2p._h.regions()
+    if 4 * xe * 4 > dbytes or (2 + nh) * 4 > fbytes:
+        return None
+    return (data, data + 2 * xe * 4, flags, flags + 2 * 4, nh, xe)
 
 
 STAGE_ROWS, STAGE_COLS = 128, 32

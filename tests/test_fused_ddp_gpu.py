@@ -29,7 +29,7 @@ def _worker(rank, ws, steps, momentum):
     ds = MyTrainDataset(256 * ws, 20, 1, seed=0)
     sampler = DistributedSampler(ds, num_replicas=ws, rank=rank, seed=5)
     finals = {}
-    for mode in ("oneshot", "rsag", "auto"):
+    for mode in ("oneshot", "rsag", "helpers", "auto"):
         os.environ["DTA_MLP_XMODE"] = mode
         torch.manual_seed(0)
         model = MLP(20, 512, 1).to(dev)
@@ -52,6 +52,7 @@ def _worker(rank, ws, steps, momentum):
     # both exchange forms sum in rank order: bit-identical training; auto (after
     # its discarded calibration steps) restarts from step 0 and matches too
     assert torch.equal(finals["oneshot"], finals["rsag"])
+    assert torch.equal(finals["oneshot"], finals["helpers"])
     assert torch.equal(finals["auto"], finals["oneshot"])
     final = finals["oneshot"]
     if rank == 0:
