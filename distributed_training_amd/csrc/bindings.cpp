@@ -22,7 +22,7 @@ hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float
                         void*, void*, int64_t, int, int, int, const void*, hipStream_t);
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 int dta_gemm_tn_split(int, int, int);
-hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int,
+hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*, void*,
                        hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
@@ -449,7 +449,9 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
 // C[M, N] = A^T B for A [K, M], B [K, N] bf16 row-major (the weight gradient dY^T X); split = 0: auto
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) { return dta_gemm_tn_split((int)M, (int)N, (int)K) > 0; }
 
-torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream) {
+// C = A^T B (and, with_colsum, the column sums of A: the bias gradient of the same Linear)
+std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream,
+                                        bool with_colsum) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
               "gemm_tn: bf16 GPU operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0), "gemm_tn: A [K, M], B [K, N]");
@@ -461,12 +463,28 @@ torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t sp
   const int sp = split > 0 ? (int)split : dta_gemm_tn_split((int)M, (int)N, (int)K);
   TORCH_CHECK(sp > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
   auto c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
-  torch::Tensor slab;
+  torch::Tensor slab, cs, db;
   if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
+  if (with_colsum) {
+    cs = torch::empty({sp, M}, a.options().dtype(torch::kFloat32));
+    db = torch::empty({M}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  }
   hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,
-                     sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, pick_stream(stream)),
+                     sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0,
+                     with_colsum ? cs.data_ptr<float>() : nullptr, with_colsum ? db.data_ptr() : nullptr,
+                     pick_stream(stream)),
          "gemm_tn");
-  return c;
+  if (with_colsum) return {c, db};
+  return {c};
+}
+
+torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream) {
+  return gemm_tn_impl(a, b, out_f32, split, stream, false)[0];
+}
+
+std::vector<torch::Tensor> gemm_tn_colsum(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split,
+                                          int64_t stream) {
+  return gemm_tn_impl(a, b, out_f32, split, stream, true);
 }
 
 // bias gradient = column sums of dy [N, C] (bf16), returned in `dtype`'s float type (bf16 or f32)
@@ -840,6 +858,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out_f32") = false, py::arg("split") = 0,
         py::arg("stream") = -1);
+  m.def("gemm_tn_colsum", &gemm_tn_colsum, py::arg("a"), py::arg("b"), py::arg("out_f32") = false,
+        py::arg("split") = 0, py::arg("stream") = -1);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_split", &dta_gemm_tn_split);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);

@@ -56,6 +56,9 @@ struct GemmTnArgs {
   int M, N, K, split, k_per_split;
   int tiles_m, tiles_n;
   int out_f32;
+  // fused column sums of A (the bias gradient sum_k dY[k, m] of the same Linear):
+  // f32 [split][M] partials, summed over splits by splitk_reduce_kernel (nullptr: off)
+  float* colsum;
 };
 
 template <bool SLAB>
@@ -79,6 +82,13 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
 
   // staging: 4 chunks of A and 4 of B per thread per stage (chunk e: row e>>4, 16-B chunk e&15)
   bf16x8 ra[4], rb[4];
+  // fused bias gradient (workgroups of output column 0 only): this thread's 4 A
+  // chunks per stage share the 16-B chunk tid & 15, so it keeps the 8 column
+  // partial sums of those columns in registers -- 32 VALU adds per stage
+  const bool do_cs = g.colsum != nullptr && tn == 0;
+  float cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
   auto gload = [&](int k0) {
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
@@ -90,6 +100,12 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
   auto lstore = [&](int buf) {
     char* ta = lds + buf * 2 * kGtTileBytes;
     char* tb = ta + kGtTileBytes;
+    if (do_cs) {
+#pragma unroll
+      for (int l = 0; l < 4; ++l)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] += bf2f(ra[l][j]);
+    }
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       const int e = tid + 256 * l, row = e >> 4, ch = e & 15;
@@ -132,6 +148,25 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
     __syncthreads();
   }
 
+  if (do_cs) {
+    // sum the 16 threads of each 16-B chunk: lanes ch + 16x of every wave (shuffles), then the 4 waves (LDS)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, kWave);
+      cs[j] += __shfl_xor(cs[j], 32, kWave);
+    }
+    float* red = reinterpret_cast<float*>(lds);  // [4 waves][16 chunks][8]; every stage's reads are done
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(wave * 16 + lane) * 8 + j] = cs[j];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const float v = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
+      g.colsum[(int64_t)sp * g.M + m0 + tid] = v;  // tid = 8 * chunk + j = column offset in the tile
+    }
+  }
+
   // epilogue: acc[i][j] rows m = m0 + wm*64 + 32i + mfma32_row(e), cols n = n0 + wn*64 + 32j + (lane & 31)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -152,9 +187,22 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
     }
 }
 
-// out[M, N] = sum_s slab[s][M][N]   (bf16 or f32 out, 4 elements per thread)
+// out[M, N] = sum_s slab[s][M][N]   (bf16 or f32 out, 4 elements per thread);
+// blocks past the matrix sum the fused column-sum partials: cout[m] = sum_s cs[s][m]
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int split, int64_t mn,
-                                                            void* out, int out_f32) {
+                                                            void* out, int out_f32, const float* __restrict__ cs,
+                                                            int M, void* cout, int cout_f32) {
+  const int64_t mblocks = (mn / 4 + 255) / 256;
+  if ((int64_t)blockIdx.x >= mblocks) {
+    const int m = (int)(((int64_t)blockIdx.x - mblocks) * 256 + threadIdx.x);
+    if (m < M) {
+      float v = 0.f;
+      for (int s = 0; s < split; ++s) v += cs[(int64_t)s * M + m];
+      if (cout_f32) static_cast<float*>(cout)[m] = v;
+      else static_cast<bf16*>(cout)[m] = f2bf(v);
+    }
+    return;
+  }
   const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i4 * 4 >= mn) return;
   float4 acc = reinterpret_cast<const float4*>(slab)[i4];
@@ -188,8 +236,9 @@ int dta_gemm_tn_split(int M, int N, int K) {
 }
 
 // c: [M, N] (bf16 or f32, row stride ldc); slab: f32 [split * M * N] when split > 1
+// colsum (optional): f32 [split][M] scratch; cout: the bias gradient [M] (bf16 / f32 as out_f32)
 hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int M, int N,
-                       int K, int split, float* slab, int out_f32, hipStream_t st) {
+                       int K, int split, float* slab, int out_f32, float* colsum, void* cout, hipStream_t st) {
   if (M % kGtBM || N % kGtBN || K % kGtBK || split < 1 || (K / kGtBK) % split) return hipErrorInvalidValue;
   GemmTnArgs g{};
   g.a = static_cast<const bf16*>(a);
@@ -205,17 +254,23 @@ hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, v
   g.tiles_m = M / kGtBM;
   g.tiles_n = N / kGtBN;
   g.out_f32 = out_f32;
+  g.colsum = cout ? colsum : nullptr;
+  if (cout && !colsum) return hipErrorInvalidValue;
   const int grid = g.tiles_m * g.tiles_n * split;
+  const unsigned cblocks = cout ? (unsigned)((M + 255) / 256) : 0u;
   if (split == 1) {
     g.c = c;
     hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(grid), dim3(256), 0, st, g);
+    if (cout)  // column sums only (mn = 0): one pass over the [1][M] partials
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks), dim3(256), 0, st, static_cast<const float*>(nullptr), 1,
+                         (int64_t)0, static_cast<void*>(nullptr), out_f32, colsum, M, cout, out_f32);
   } else {
     if (ldc != N) return hipErrorInvalidValue;
     g.c = slab;
     hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(grid), dim3(256), 0, st, g);
     const int64_t mn = (int64_t)M * N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256)), dim3(256), 0, st, slab, split, mn,
-                       c, out_f32);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256) + cblocks), dim3(256), 0, st, slab,
+                       split, mn, c, out_f32, colsum, M, cout, out_f32);
   }
   return hipGetLastError();
 }

@@ -210,23 +210,32 @@ def rms_norm(x, w, eps: float = 1e-5):
 _WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this hipBLASLt fills the chip by itself
 
 
-def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    """dW = dy^T x.  Small outputs with a long token reduction (GPT-2: 768 x 768 ..
-    3072 x 768 over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip),
-    which fills 256 CUs where a library GEMM tiling only the output does not
-    (measured 1.4-1.8x on the attention projections); large outputs stay on
-    hipBLASLt."""
+def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False):
+    """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
+    Small outputs with a long token reduction (GPT-2: 768 x 768 .. 3072 x 768
+    over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip), which fills
+    256 CUs where a library GEMM tiling only the output does not (measured
+    1.4-1.8x on the attention projections) and sums the bias gradient from the
+    dy tiles it already stages (no separate pass over dy); large outputs stay
+    on hipBLASLt."""
     K, M = dy2.shape
     N = x2.shape[1]
     if (M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and (M // 128) * (N // 128) <= _WGRAD_NATIVE_MAX_TILES
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
-        return native().gemm_tn(dy2, x2.contiguous() if x2.stride(0) % 8 else x2, False, 0, -1)
-    return torch.mm(dy2.t(), x2)
+        x2 = x2.contiguous() if x2.stride(0) % 8 else x2
+        if with_bias:
+            dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1)
+            return dw, db
+        return native().gemm_tn(dy2, x2, False, 0, -1)
+    dw = torch.mm(dy2.t(), x2)
+    if with_bias:
+        return dw, native().bias_grad(dy2, False, -1)
+    return dw
 
 
 class _Linear(Function):
-    """y = x W^T + b: GEMMs on hipBLASLt, bias gradient on the native
-    column-sum kernel (one 16-byte-load pass over dy)."""
+    """y = x W^T + b: forward / input-gradient GEMMs on hipBLASLt, weight and
+    bias gradients from one native split-K kernel (see _weight_grad)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -243,9 +252,11 @@ class _Linear(Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w).view(*x.shape[:-1], w.shape[1])
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            dw = _weight_grad(dy2, x.reshape(-1, x.shape[-1]))
-        if ctx.has_b and ctx.needs_input_grad[2]:
+            r = _weight_grad(dy2, x.reshape(-1, x.shape[-1]), with_bias=want_b)
+            dw, db = r if want_b else (r, None)
+        elif want_b:
             db = native().bias_grad(dy2, False, -1)
         return dx, dw, db
 

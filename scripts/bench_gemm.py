@@ -29,7 +29,22 @@ def timeit(fn, reps=20):
     return s.elapsed_time(e) / reps * 1e3  # us
 
 
+def linear_shapes():
+    """Forward (y = x W^T) and input-gradient (dx = dy W) GEMMs of GPT-2 small on hipBLASLt."""
+    for T, out_f, in_f in [(8192, 2304, 768), (8192, 768, 768), (8192, 3072, 768), (8192, 768, 3072),
+                           (8192, 50304, 768)]:
+        x = torch.randn(T, in_f, device="cuda").bfloat16()
+        w = torch.randn(out_f, in_f, device="cuda").bfloat16()
+        dy = torch.randn(T, out_f, device="cuda").bfloat16()
+        fl = 2.0 * T * out_f * in_f
+        tf = timeit(lambda: torch.mm(x, w.t()))
+        tb = timeit(lambda: torch.mm(dy, w))
+        print(json.dumps({"T": T, "out": out_f, "in": in_f, "fwd_us": round(tf, 1), "fwd_TF": round(fl / tf / 1e6, 1),
+                          "dgrad_us": round(tb, 1), "dgrad_TF": round(fl / tb / 1e6, 1)}), flush=True)
+
+
 def main():
+    linear_shapes()
     C = native()
     for K, M, N in SHAPES:
         a = torch.randn(K, M, device="cuda").bfloat16()

@@ -297,3 +297,20 @@ def test_gemm_tn_weight_gradient(K, M, N, split):
     wide = torch.randn(K, M + 128, device=DEV).bfloat16()
     c2 = native().gemm_tn(wide[:, 64:64 + M], b, True, split)
     assert _rel(c2, wide[:, 64:64 + M].float().t() @ b.float()) < 1e-3
+
+
+@pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
+                                         (4096, 2304, 768, 0)])
+def test_gemm_tn_fused_bias_gradient(K, M, N, split):
+    """dW = dY^T X and db = column sums of dY from one split-K launch vs fp32 torch."""
+    from distributed_training_amd.ops import native
+
+    torch.manual_seed(9)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    c, db = native().gemm_tn_colsum(a, b, True, split)
+    assert _rel(c, a.float().t() @ b.float()) < 1e-3
+    assert db.shape == (M,) and db.dtype == torch.float32
+    assert _rel(db, a.float().sum(0)) < 1e-4
+    c16, db16 = native().gemm_tn_colsum(a, b, False, split)
+    assert db16.dtype == torch.bfloat16 and _rel(db16, a.float().sum(0)) < 1e-2
