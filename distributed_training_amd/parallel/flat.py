@@ -20,7 +20,7 @@ Trainer wraps the model) -- keeps working.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -66,6 +66,10 @@ class FlatParamGroup:
         # set by an engine whose backward hooks move fresh gradients into the
         # flat buffer (DDP): zero_grad(set_to_none=True) may then drop the views
         self.steal_ok = False
+        # set by an engine that writes every gradient slice itself in the next
+        # backward (FSDP reduce-scatters into the slices): zero_grad(set_to_none)
+        # then drops the gradients and calls it instead of zero-filling the buffer
+        self.fresh_hook: Optional[Callable[[], None]] = None
         for i, p in enumerate(self.params):
             p.data = self.param_view(i)
             p.grad = self.grad_view(i)
@@ -113,9 +117,11 @@ class FlatParamGroup:
         tensors over without an accumulate kernel; the DDP engine moves them
         into the flat buffer in one batched copy per bucket).  Otherwise zero
         the flat buffer and keep the views."""
-        if set_to_none and self.steal_ok:
+        if set_to_none and (self.steal_ok or self.fresh_hook is not None):
             for p in self.params:
                 p.grad = None
+            if self.fresh_hook is not None:
+                self.fresh_hook()
             return
         self.grad.zero_()
         for i, p in enumerate(self.params):

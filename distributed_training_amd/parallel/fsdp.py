@@ -156,7 +156,14 @@ class _Unit:
         if own.world_size == 1:  # the whole gradient is this rank's shard: no collective, no copy
             own._pending_rs.append((self, CommWork(), g, g))
         else:
-            out = torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
+            # after zero_grad(set_to_none) the flat gradient holds nothing worth
+            # keeping: reduce-scatter straight into this unit's slice of it
+            fg = own.shards
+            i = fg.index_of(self.shard_param)
+            direct = own._grad_fresh and fg.grad_dtype == g.dtype and self.index not in own._written
+            out = fg.grad_view(i) if direct else torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
+            if direct:
+                own._written.add(self.index)
             op = "avg" if own.comm.supports_avg() else "sum"
             if op == "sum":
                 g.div_(own.world_size)
@@ -257,6 +264,7 @@ class FullyShardedDataParallel(nn.Module):
                     p.data = torch.empty(0, dtype=p.dtype, device=p.device)
                 u.entries = [(m, a, n, None) for m, a, n, _ in u.entries]
         self.shards = FlatParamGroup(shard_params, self.device, param_dtype=param_dtype, names=names)
+        self.shards.fresh_hook = self._mark_grads_fresh
         self.shard_params = nn.ParameterList(shard_params)
         if sync_module_states and self.world_size > 1:
             for b in module.buffers():
@@ -272,6 +280,11 @@ class FullyShardedDataParallel(nn.Module):
         self._record_order = True
         self._pending_rs: List = []
         self._cb_queued = False
+        # zero_grad(set_to_none=True) leaves the flat gradient stale instead of
+        # zero-filling it; the first backward then writes (reduce-scatters /
+        # copies) each unit's gradient in place of accumulating into zeros
+        self._grad_fresh = False
+        self._written: Set[int] = set()
         logger.debug("FSDP: %d unit(s), shard sizes %s", len(self.units), [u.shard_size for u in self.units])
 
     # ------------------------------------------------------------ forward
@@ -355,14 +368,34 @@ class FullyShardedDataParallel(nn.Module):
 
     def _finalize_backward(self) -> None:
         fg = self.shards
+        fresh = self._grad_fresh
+        done: Set[int] = set()
         for u, work, out, g in self._pending_rs:
             work.wait()
             i = fg.index_of(u.shard_param)
             gv = fg.grad_view(i)
-            if not fg.grad_is_view(i):
-                fg.rebind_grad(i)
-            gv.add_(out.to(gv.dtype))
+            if fresh and u.index not in done:  # first gradient of this unit since zero_grad
+                if fg.params[i].grad is None or not fg.grad_is_view(i):
+                    fg.params[i].grad = gv
+                if out.data_ptr() != gv.data_ptr():  # (reduce-scattered in place otherwise)
+                    gv.copy_(out)
+                done.add(u.index)
+                self._written.add(u.index)
+            elif fresh:
+                gv.add_(out.to(gv.dtype))
+            else:
+                if not fg.grad_is_view(i):
+                    fg.rebind_grad(i)
+                gv.add_(out.to(gv.dtype))
             del g
+        if fresh:
+            for u in self.units:  # units without a gradient this backward: zeros, as torch would accumulate
+                if u.index not in self._written:
+                    i = fg.index_of(u.shard_param)
+                    fg.grad_view(i).zero_()
+                    fg.params[i].grad = fg.grad_view(i)
+            self._grad_fresh = False
+            self._written = set()
         self._pending_rs = []
         self._cb_queued = False
         for u in self.units:  # any unit not used in backward: drop its gathered copy
@@ -370,8 +403,17 @@ class FullyShardedDataParallel(nn.Module):
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):
                 u.free()
 
-    def zero_grad(self, set_to_none: bool = True) -> None:  # noqa: ARG002
-        self.shards.zero_grad()
+    def _mark_grads_fresh(self) -> None:
+        self._grad_fresh = True
+        self._written = set()
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """``set_to_none`` (default): no fill pass -- the next backward writes every
+        unit's gradient slice (see _finalize_backward); otherwise zero the flat
+        gradient (later backwards accumulate into it)."""
+        if not set_to_none:
+            self._grad_fresh = False
+        self.shards.zero_grad(set_to_none)
 
     # ------------------------------------------------------------ state dict
     @torch.no_grad()

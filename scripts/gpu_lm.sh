@@ -13,3 +13,4 @@ cat gpurun_out/lm_llama8b_fsdp.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gpt2 -o run -- \
   python3 bench_lm.py --model gpt2 --strategy ddp --steps 10 --warmup 3 > gpurun_out/prof_gpt2/bench.log 2>&1
 python scripts/kstats.py gpurun_out/prof_gpt2/run_kernel_stats.csv 13 30 > gpurun_out/prof_gpt2/summary.txt
+timeout -k 10 300 python -u -m pytest tests/test_lm_ops_gpu.py tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_lm2.log 2>&1

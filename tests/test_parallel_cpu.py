@@ -90,7 +90,7 @@ def test_native_ddp_matches_torch_ddp(bucket_mb, unused, accum):
     run_gloo(_ddp_parity, 2, bucket_mb, unused, accum)
 
 
-def _fsdp_parity(rank, ws, wrap, opt_name):
+def _fsdp_parity(rank, ws, wrap, opt_name, accum=False):
     from distributed_training_amd.ops.optim import FusedAdamW, FusedSGD
     from distributed_training_amd.parallel.comm import TorchComm
     from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
@@ -112,11 +112,18 @@ def _fsdp_parity(rank, ws, wrap, opt_name):
         g = torch.Generator().manual_seed(100 + it)
         X = torch.randn(8 * ws, 20, generator=g)
         Y = torch.randn(8 * ws, 1, generator=g)
-        o1.zero_grad()
-        F.mse_loss(ref(X), Y).backward()
+        # accum: two micro-batches per step, alternating zero_grad(set_to_none) forms
+        # (set_to_none writes the first micro-batch's gradient in place, later ones accumulate)
+        none = it % 2 == 0 or not accum
+        o1.zero_grad(set_to_none=none)
+        o2.zero_grad(set_to_none=none)
+        for mb in range(2 if accum else 1):
+            lo, hi = (mb * 4, mb * 4 + 4) if accum else (0, 8)
+            xs = torch.cat([X[r * 8 + lo:r * 8 + hi] for r in range(ws)])
+            ys = torch.cat([Y[r * 8 + lo:r * 8 + hi] for r in range(ws)])
+            F.mse_loss(ref(xs), ys).backward()
+            F.mse_loss(fs(X[rank * 8 + lo:rank * 8 + hi]), Y[rank * 8 + lo:rank * 8 + hi]).backward()
         o1.step()
-        o2.zero_grad()
-        F.mse_loss(fs(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
         o2.step()
     sd = fs.full_state_dict(rank0_only=False)
     rs = ref.state_dict()
@@ -137,17 +144,21 @@ def _fsdp_parity(rank, ws, wrap, opt_name):
         torch.testing.assert_close(fs(x), ref(x), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("wrap,opt_name", [(True, "adamw"), (False, "sgd"), (True, "sgd")])
-def test_native_fsdp_matches_single_process(wrap, opt_name):
-    run_gloo(_fsdp_parity, 2, wrap, opt_name)
+@pytest.mark.parametrize("wrap,opt_name,accum", [(True, "adamw", False), (False, "sgd", False), (True, "sgd", False),
+                                                (True, "sgd", True), (False, "adamw", True)])
+def test_native_fsdp_matches_single_process(wrap, opt_name, accum):
+    run_gloo(_fsdp_parity, 2, wrap, opt_name, accum)
 
 
-def _fsdp_ws4(rank, ws):
-    _fsdp_parity(rank, ws, True, "adamw")
+def _fsdp_ws(rank, ws):
+    _fsdp_parity(rank, ws, True, "adamw", False)
 
 
-def test_native_fsdp_world4():
-    run_gloo(_fsdp_ws4, 4)
+@pytest.mark.parametrize("ws", [4, 8])
+def test_native_fsdp_world(ws):
+    """4 and 8 ranks (the 8-GPU node's rank count) over gloo: shard padding, gathers,
+    reduce-scatters and the full state dict at every world size the bench runs."""
+    run_gloo(_fsdp_ws, ws)
 
 
 def _comm_ops(rank, ws):
