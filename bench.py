@@ -112,6 +112,11 @@ def run_fused(args, dev, ws):
         prog.store_to_module()
         return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
 
+    # which DDP step form ran (persistent loop + in-kernel exchange, or per-step
+    # kernel + all-reduce), and the per-form calibration times when ranks > 1
+    form = ("persistent" + (f"/{prog.xmode}" if ws > 1 else "")) if prog.persistent else "per-step"
+    finish.info = {"step_form": form,
+                   "calibration_ms": getattr(prog, "exchange_times_ms", None)}
     return step_fn, finish, comm
 
 
@@ -269,6 +274,7 @@ def main():
                    "impl": args.impl},
         "final_loss": last_loss,
     }
+    out.update(getattr(finish, "info", {}))
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -22,6 +22,32 @@ def test_kernels_are_gfx950_code_objects():
     assert b"mlp2_fused_step_kernel" in data
 
 
+def test_rccl_loader_under_host_sanitizers(tmp_path):
+    """The host C++ comm layer (csrc/rccl_comm.cpp) built with AddressSanitizer +
+    UBSan and driven through its load / error paths (no GPU needed)."""
+    import shutil
+
+    import pytest
+    import torch
+
+    cxx = shutil.which("g++")
+    rccl = Path(torch.__file__).resolve().parent / "lib" / "librccl.so"
+    if cxx is None or not rccl.exists():
+        pytest.skip("g++ or librccl.so not available")
+    csrc = ROOT / "distributed_training_amd" / "csrc"
+    exe = tmp_path / "rccl_loader_check"
+    b = subprocess.run([cxx, "-std=c++17", "-g", "-O1", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                        "-fno-sanitize-recover=undefined", "-D__HIP_PLATFORM_AMD__=1", f"-I{csrc}",
+                        "-I/opt/rocm/include", str(ROOT / "tests" / "native" / "rccl_loader_check.cpp"),
+                        str(csrc / "rccl_comm.cpp"), "-L/opt/rocm/lib", "-lamdhip64", "-ldl",
+                        "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)], capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-3000:]
+    env = {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1", "PATH": "/usr/bin:/bin",
+           "HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""}
+    r = subprocess.run([str(exe), str(rccl)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "ok rccl" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
 def test_native_entrypoints_present():
     from distributed_training_amd.ops import native
 
