@@ -57,11 +57,22 @@ def main():
         t_tf = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt, is_causal=True))
         ot = F.scaled_dot_product_attention(qt, kt, vt, is_causal=True)
         t_tb = timeit(lambda: torch.autograd.grad(ot, (qt, kt, vt), dot, retain_graph=True))
+        # the models' path: strided q/k/v views of one packed QKV projection output
+        # (row stride (H + 2 Hkv) D), RoPE applied, packed dQKV written by backward
+        from distributed_training_amd.ops import lm
+
+        qkv = torch.randn(B, S, (H + 2 * Hkv) * D, device=dev, dtype=torch.bfloat16, generator=g)
+        qkv.requires_grad_()
+        cos, sin = lm.rope_tables(S, D, 500000.0, device=dev)
+        t_pf = timeit(lambda: lm.attention_packed(qkv, H, Hkv, True, rope=(cos, sin)))
+        op = lm.attention_packed(qkv, H, Hkv, True, rope=(cos, sin))
+        t_pb = timeit(lambda: torch.autograd.grad(op, qkv, do, retain_graph=True))
         err = (o.float() - ot.detach().transpose(1, 2).float()).abs().max().item()
         print(json.dumps({"shape": name, "B": B, "S": S, "H": H, "Hkv": Hkv, "D": D,
                           "fwd_us": round(t_fwd * 1e6, 1), "bwd_us": round(t_bwd * 1e6, 1),
                           "fwd_tflops": round(fl / t_fwd / 1e12, 1), "bwd_tflops": round(2.5 * fl / t_bwd / 1e12, 1),
                           "sdpa_fwd_us": round(t_tf * 1e6, 1), "sdpa_bwd_us": round(t_tb * 1e6, 1),
+                          "packed_rope_fwd_us": round(t_pf * 1e6, 1), "packed_rope_bwd_us": round(t_pb * 1e6, 1),
                           "max_abs_err_vs_sdpa": err}), flush=True)
 
 
