@@ -807,9 +807,9 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
       a.xe = (int)xinfo[o + 5];
       const int nt = (int)(hidden / 32);
       TORCH_CHECK(a.nh >= 1 && a.nh <= 255 && a.xe >= nt * 1024 + out_dim && a.slot_elems >= a.xe &&
-                      (a.xe + a.nh - 1) / a.nh <= 4 * 512,
+                      (int64_t)a.nh * 512 >= a.xe && out_dim <= 64,
                   "mlp_persistent: helper exchange geometry (nh in [1, 255], xe >= hidden * 32 + out, "
-                  "slots >= xe, <= 2048 elements per helper)");
+                  "slots >= xe, 512 elements per helper, out <= 64)");
     }
   }
   if (dbg && dbg->defined()) {

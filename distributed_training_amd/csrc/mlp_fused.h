@@ -74,8 +74,8 @@ struct MlpPArgs {
   // workgroups push / reduce them across ranks on their own CUs, sums come back in xg_red
   float* xg_out;                    // [2][xe]
   float* xg_red;                    // [2][xe]
-  int* xready;                      // [2] epoch of the gradients in xg_out[parity]
-  int* xdone;                       // [nh] epoch each helper finished
+  int* xready;                      // [2][8 waves] epoch of each loop wave's gradients in xg_out[parity]
+  int* xdone;                       // [nh] epoch each helper finished (helper h: elements [512 h, 512 h + 512))
   int nh, xe;
 };
 

@@ -36,7 +36,8 @@ namespace dta {
 constexpr int kMpWaves = 8;
 constexpr int kMpThreads = kMpWaves * 64;
 constexpr int kMpXs = 32;            // batch tile columns (bf16): X | 1 | dY | 0
-constexpr int kMpImgPad = 32;        // bf16 pad per activation-image row (rows 64 B apart mod 256 B)
+constexpr int kMpImgPad = 32;
+constexpr int kP2PRanks = 8;         // most ranks of an in-kernel exchange (one node)        // bf16 pad per activation-image row (rows 64 B apart mod 256 B)
 
 
 __device__ __forceinline__ bf16x4 mp_tr4(const bf16* p) {
@@ -153,6 +154,36 @@ __device__ __forceinline__ float ll_wait(const MlpPArgs& a, const unsigned long 
   return __uint_as_float((unsigned)(v & 0xffffffffu));
 }
 
+// Sum one batch of U elements over the `W` ranks' LL slots (rank order, the
+// same bits on every rank).  Every load of the batch -- R x U uncached
+// system-scope reads -- is issued before any tag is checked, so a batch costs
+// one memory latency instead of one per rank; a slot whose tag is not yet `ep`
+// is re-polled.  Unused (rank, element) pairs load a valid duplicate address
+// (no branch around a load) and are left out of the sum.
+template <int R, int U>
+__device__ __forceinline__ void ll_sum_ranks(const MlpPArgs& a, const unsigned long long* base, long long stride,
+                                             const long long (&idx)[U], const bool (&live)[U], int W, unsigned ep,
+                                             float (&acc)[U]) {
+  unsigned long long v[R][U];
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[q][u] = __hip_atomic_load(base + (long long)(q < W ? q : 0) * stride + idx[u], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.f;
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q < W && live[u]) {
+        float x = __uint_as_float((unsigned)(v[q][u] & 0xffffffffu));
+        if ((unsigned)(v[q][u] >> 32) != ep) x = ll_wait(a, base + (long long)q * stride + idx[u], ep);
+        acc[u] += x;
+      }
+}
+
 // owner: sum the elements j = rank, rank + world, ... over the RS slots (rank
 // order) and push each sum to every rank's AG slot
 __device__ void xowner_reduce(const MlpPArgs& a, unsigned ep, int n) {
@@ -163,14 +194,15 @@ __device__ void xowner_reduce(const MlpPArgs& a, unsigned ep, int n) {
   const int nown = (n - a.rank + W - 1) / W;
   for (int k0 = threadIdx.x; k0 < nown; k0 += kMpThreads * U) {
     float acc[U];
+    long long idx[U];
+    bool live[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = 0.f;
-    for (int q = 0; q < W; ++q)
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * kMpThreads;
-        if (k < nown) acc[u] += ll_wait(a, rs + (long long)q * a.slot_elems + a.rank + (long long)k * W, ep);
-      }
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * kMpThreads;
+      live[u] = k < nown;
+      idx[u] = a.rank + (long long)(live[u] ? k : 0) * W;
+    }
+    ll_sum_ranks<kP2PRanks, U>(a, rs, a.slot_elems, idx, live, W, ep, acc);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + u * kMpThreads;
@@ -199,7 +231,7 @@ __device__ __forceinline__ int xoff(const MlpPArgs& a, int j) {
 // (xmode 2); otherwise sum the one-shot slots [par][q][offset] in rank order.
 template <bool PLAIN, bool AG>
 __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf, bf16* Wb, SgdH hs, int first) {
-  constexpr int U = 8;  // elements per thread in flight (x world loads)
+  constexpr int U = AG ? 8 : 4;  // elements per thread per batch (x ranks loads in flight)
   hs.first = first;
   const int n = a.hidden * a.in_dim + 2 * a.hidden + a.out_dim;
   const int W = AG ? 1 : a.world, par = ep & 1;
@@ -214,31 +246,16 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
       off[u] = xoff(a, j < n ? j : n - 1);
       acc[u] = 0.f;
     }
-    for (int q = 0; q < W; ++q) {  // rank order
-      unsigned long long v[U];
+    {
+      long long idx[U];
+      bool live[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = j0 + u * kMpThreads;
-        const long long idx = AG ? (long long)(j < n ? j : n - 1) : (long long)q * a.slot_elems + off[u];
-        v[u] = __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        live[u] = true;  // j >= n duplicates element n-1 and is not applied below
+        idx[u] = AG ? (long long)(j < n ? j : n - 1) : (long long)off[u];
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        int it = 0;
-        while ((unsigned)(v[u] >> 32) != ep) {
-          // sticky error: after one timed-out wait the rest give up at once
-          if (++it > a.timeout_iters ||
-              ((it & 1023) == 1 && __hip_atomic_load(a.xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-            atomicOr(a.xerr, 1);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          const int j = j0 + u * kMpThreads;
-          const long long idx = AG ? (long long)(j < n ? j : n - 1) : (long long)q * a.slot_elems + off[u];
-          v[u] = __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        acc[u] += __uint_as_float((unsigned)(v[u] & 0xffffffffu));
-      }
+      ll_sum_ranks<AG ? 1 : kP2PRanks, U>(a, base, a.slot_elems, idx, live, W, ep, acc);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -300,15 +317,18 @@ __device__ __forceinline__ bool flag_wait(const MlpPArgs& a, const int* f, int e
 }
 
 __device__ void helper_loop(const MlpPArgs& a, unsigned xe0) {
+  // helper h owns elements [512 h, 512 h + 512): half of tile h / 2, written by
+  // loop wave (h / 2) % 8 -- or the output-bias gradients (last helper, wave 0)
   const int h = blockIdx.x - 1, tid = threadIdx.x;
-  const int chunk = (a.xe + a.nh - 1) / a.nh;
-  const int e0 = h * chunk, e1 = min(a.xe, e0 + chunk);
+  const int e0 = h * kMpThreads, e1 = min(a.xe, e0 + kMpThreads);
+  const int NT = a.hidden / 32;
+  const int owner = h < 2 * NT ? (h >> 1) % kMpWaves : 0;
   const int W = a.world;
-  constexpr int U = 4;  // elements per thread (the host keeps chunk <= U * kMpThreads)
+  constexpr int U = 1;  // one element per thread
   for (int s = 0; s < a.nsteps; ++s) {
     const unsigned ep = xe0 + s + 1;
     const int par = ep & 1;
-    if (tid == 0) flag_wait(a, a.xready + par, (int)ep);
+    if (tid == 0) flag_wait(a, a.xready + par * kMpWaves + owner, (int)ep);
     __syncthreads();
     float v[U];
 #pragma unroll
@@ -327,15 +347,16 @@ __device__ void helper_loop(const MlpPArgs& a, unsigned xe0) {
       }
     }
     float acc[U];
+    long long idx[U];
+    bool live[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + tid + u * kMpThreads;
+      live[u] = e < e1;
+      idx[u] = live[u] ? e : e0;
+    }
     const unsigned long long* base = a.local_ll + (long long)par * W * a.slot_elems;
-    for (int q = 0; q < W; ++q)  // rank order: the same bits on every rank
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + tid + u * kMpThreads;
-        if (e < e1) acc[u] += ll_wait(a, base + (long long)q * a.slot_elems + e, ep);
-      }
+    ll_sum_ranks<kP2PRanks, U>(a, base, a.slot_elems, idx, live, W, ep, acc);  // rank order
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = e0 + tid + u * kMpThreads;
@@ -349,7 +370,9 @@ __device__ void helper_loop(const MlpPArgs& a, unsigned xe0) {
 
 // OUT: output width, TPW: hidden tiles per wave (H <= 256 TPW), PLAIN: SGD
 // without momentum / weight decay / maximize (the update is p -= lr * g)
-template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
+// XM: 0 one rank, else the exchange form (1 one-shot, 2 rs+ag, 3 helpers) -- one
+// instantiation per form keeps the other forms' live ranges out of its registers
+template <int ACT, int OUT, int TPW, bool PLAIN, int XM>
 __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) {
   static_assert(OUT == 1, "the persistent loop serves single-output heads");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -358,7 +381,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   const int r32 = lane & 31, hh = lane >> 5;
   const int IN = a.in_dim, H = a.hidden, B = a.B, NT = H / 32;
   const int IMG = H + kMpImgPad;  // activation image row stride (elements)
-  if (MULTI && blockIdx.x > 0) {  // xmode 3: helper workgroups (the loop is workgroup 0)
+  if (XM == 3 && blockIdx.x > 0) {  // xmode 3: helper workgroups (the loop is workgroup 0)
     helper_loop(a, (unsigned)*a.xepoch);
     return;
   }
@@ -393,7 +416,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   int c0 = *a.cursor;
   int lcur = *a.loss_cursor;
   int first = a.M ? (*a.mom_started == 0) : 0;
-  constexpr bool multi = MULTI;  // DDP across ranks (a.world > 1)
+  constexpr bool multi = XM != 0;  // DDP across ranks (a.world > 1)
   const unsigned xe0 = multi ? (unsigned)*a.xepoch : 0u;
 
   // ---- batch pipeline: idx two steps ahead, features one step ahead ----
@@ -548,8 +571,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
         if (lane == 0) {
           if (multi) {
-            if (a.xmode == 3) st_sc(a.xg_out + (long long)((xe0 + s + 1) & 1) * a.xe + NT * 1024 + o, db);
-            else if (a.xmode == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
+            if (XM == 3) st_sc(a.xg_out + (long long)((xe0 + s + 1) & 1) * a.xe + NT * 1024 + o, db);
+            else if (XM == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
             else xpush(a, xe0 + s + 1, a.o_b2 + o, db);
           } else {
             SgdH hs = hbase;
@@ -620,15 +643,15 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
         // SGD: all 16 parameters (and momenta) of this lane read first, then written
-        if (multi && (upd || a.xmode == 3)) {
+        if (multi && (upd || XM == 3)) {
           // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
           const unsigned ep = xe0 + s + 1;
-          if (a.xmode == 3) {
+          if (XM == 3) {
             // fragment order: [tile][register][lane]; lanes past the parameter columns write 0
             float* go = a.xg_out + (long long)(ep & 1) * a.xe + (long long)t * 1024 + lane;
 #pragma unroll
             for (int i = 0; i < 16; ++i) st_sc(go + i * 64, upd ? (from_c2 ? c2[i] : c1[i]) : 0.f);
-          } else if (a.xmode == 2) {
+          } else if (XM == 2) {
             // dense index: W1[h][c] = h * IN + c, b1[h] = H IN + h, W2[h] = H IN + H + h
             const int jb = c < IN ? c : H * IN + (c - IN) * H;
             const int js = c < IN ? IN : 1;
@@ -677,20 +700,36 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         if (tt == 0) MP_STAMP(7);
       }
     }
-    if constexpr (MULTI) {
+    if constexpr (XM != 0) {
       // all waves done reading the pre-update parameters before any update
-      if (a.xmode == 3) {
+      if (XM == 3) {
+        // per-wave hand-off, no workgroup barrier: a wave's tiles (and wave 0's
+        // output-bias gradient) go to their own helpers and come back from them,
+        // and the wave updates only parameters it alone reads next step (as on
+        // one rank), so fast waves run ahead
         const unsigned ep = xe0 + s + 1;
         const int par = ep & 1;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gradient stores landed
-        lds_barrier();                                     // ... and every other wave's
-        if (tid == 0) __hip_atomic_store(a.xready + par, (int)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (tid < a.nh) flag_wait(a, a.xdone + tid, (int)ep);
-        __syncthreads();
+        if (lane == 0)
+          __hip_atomic_store(a.xready + par * kMpWaves + wave, (int)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane < 2 * TPW) {
+          const int t = wave + kMpWaves * (lane >> 1);
+          if (t < NT) flag_wait(a, a.xdone + 2 * t + (lane & 1), (int)ep);
+        } else if (lane == 2 * TPW && wave == 0) {
+          flag_wait(a, a.xdone + 2 * NT, (int)ep);
+        }
         // SGD from the summed gradients (same lane <-> parameter map as one rank)
         const float* gr = a.xg_red + (long long)par * a.xe;
         SgdH hs2 = hbase;
         hs2.first = first;
+        // all of this lane's summed gradients in flight at once (one latency)
+        float gall[TPW][16];
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt) {
+          const int t = wave + kMpWaves * tt;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) gall[tt][i] = t < NT ? ld_sc(gr + (long long)t * 1024 + i * 64 + lane) : 0.f;
+        }
 #pragma unroll
         for (int tt = 0; tt < TPW; ++tt) {
           const int t = wave + kMpWaves * tt;
@@ -703,7 +742,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
               for (int u = 0; u < 8; ++u) {
                 const int i = 8 * half + u;
                 const int off = pbase + (h0 + mfma32_row(i, lane)) * pstride;
-                gv[u] = ld_sc(gr + (long long)t * 1024 + i * 64 + lane);
+                gv[u] = gall[tt][i];
                 pv[u] = Pf[off];
                 mv[u] = PLAIN ? 0.f : Mf[off];
               }
@@ -732,8 +771,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           }
         }
         if (tid < a.out_dim) sgd_apply(Pf + a.o_b2 + tid, Mf + a.o_b2 + tid, ld_sc(gr + NT * 1024 + tid), hs2);
-        lds_barrier();
-      } else if (a.xmode == 2) {
+      } else if (XM == 2) {
         // the owner sums need no LDS: start them before the barrier
         xowner_reduce(a, xe0 + s + 1, H * IN + 2 * H + a.out_dim);
         lds_barrier();
@@ -742,7 +780,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         lds_barrier();
         xreduce_sgd<PLAIN, false>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
       }
-      if (a.xmode != 3) lds_barrier();
+      if (XM != 3) lds_barrier();
     }
     MP_STAMP(5);
     first = 0;
@@ -772,11 +810,11 @@ size_t dta_mlp_persistent_lds_bytes(int total, int hidden, int out_dim, int has_
          kMpWaves * out_dim * 32 * 4 + out_dim * 32 * 4 + 2 * 32 * out_dim * 4 + 16 + (size_t)hidden * 32 * 2;
 }
 
-template <int ACT, int OUT, int TPW, bool PLAIN, bool MULTI>
+template <int ACT, int OUT, int TPW, bool PLAIN, int XM>
 static hipError_t mp_launch(const MlpPArgs& a, size_t lds, hipStream_t st) {
-  auto k = &mlp_persistent_kernel<ACT, OUT, TPW, PLAIN, MULTI>;
+  auto k = &mlp_persistent_kernel<ACT, OUT, TPW, PLAIN, XM>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int grid = (MULTI && a.xmode == 3) ? 1 + a.nh : 1;
+  const int grid = XM == 3 ? 1 + a.nh : 1;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kMpThreads), lds, st, a);
   return hipGetLastError();
 }
@@ -788,9 +826,15 @@ template <int ACT>
 static hipError_t mp_launch_out(const MlpPArgs& a, size_t lds, hipStream_t st) {
   if (a.out_dim != 1 || a.hidden > 512) return hipErrorInvalidValue;
   const bool plain = a.momentum == 0.f && a.weight_decay == 0.f && !a.maximize;
-  if (a.world > 1)
-    return plain ? mp_launch<ACT, 1, 2, true, true>(a, lds, st) : mp_launch<ACT, 1, 2, false, true>(a, lds, st);
-  return plain ? mp_launch<ACT, 1, 2, true, false>(a, lds, st) : mp_launch<ACT, 1, 2, false, false>(a, lds, st);
+  if (a.world > 1) {
+    switch (a.xmode) {
+      case 1: return plain ? mp_launch<ACT, 1, 2, true, 1>(a, lds, st) : mp_launch<ACT, 1, 2, false, 1>(a, lds, st);
+      case 2: return plain ? mp_launch<ACT, 1, 2, true, 2>(a, lds, st) : mp_launch<ACT, 1, 2, false, 2>(a, lds, st);
+      case 3: return plain ? mp_launch<ACT, 1, 2, true, 3>(a, lds, st) : mp_launch<ACT, 1, 2, false, 3>(a, lds, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return plain ? mp_launch<ACT, 1, 2, true, 0>(a, lds, st) : mp_launch<ACT, 1, 2, false, 0>(a, lds, st);
 }
 
 hipError_t dta_mlp_persistent(const MlpPArgs* a, int act, hipStream_t st) {

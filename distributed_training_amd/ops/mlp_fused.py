@@ -149,11 +149,11 @@ def helper_buffers(p2p, hidden: int, out_dim: int):
     before an s_waitcnt returns, so a relaxed flag suffices -- no L2 write-back or
     invalidate per step.  Returns (xg_out, xg_red, xready, xdone, nh, xe)."""
     xe = helper_elems(hidden, out_dim)
-    nh = max(1, min(64, -(-xe // 512)))  # ~512 elements (one per thread) per helper
+    nh = -(-xe // 512)  # 512 elements (one per thread) per helper: two per 32-unit hidden tile + the output bias
     data, dbytes, flags, fbytes = p2p._h.regions()
-    if 4 * xe * 4 > dbytes or (2 + nh) * 4 > fbytes:
+    if 4 * xe * 4 > dbytes or (16 + nh) * 4 > fbytes or nh > 255 or out_dim > 64:
         return None
-    return (data, data + 2 * xe * 4, flags, flags + 2 * 4, nh, xe)
+    return (data, data + 2 * xe * 4, flags, flags + 16 * 4, nh, xe)  # xready [2][8 waves], xdone [nh]
 
 
 STAGE_ROWS, STAGE_COLS = 128, 32
