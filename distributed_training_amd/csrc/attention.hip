@@ -577,11 +577,22 @@ static void fwd_launch(const AttnArgs& a, bool causal, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false, NW>), grid, dim3(NW * 64), 0, st, a);
 }
 
+// 8 waves (256 queries) per workgroup share each K/V tile: measured faster
+// whenever the grid still holds >= 256 (D = 64; GPT-2: 43.6 -> 37.4 us) or
+// >= 1024 (D = 128) such workgroups.
 static int fwd_waves(const AttnArgs& a, int D) {
   const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
   if (force) return atoi(force) == 8 ? 8 : 4;
   const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
-  return D == 128 && wg8 >= 1024 ? 8 : 4;
+  return wg8 >= (D == 128 ? 1024 : 256) ? 8 : 4;
+}
+
+static int dq_waves(const AttnArgs& a, int D) {
+  const char* force = getenv("DTA_ATTN_DQ_WAVES");
+  if (force) return atoi(force) == 8 ? 8 : 4;
+  (void)a;
+  (void)D;
+  return 4;
 }
 
 template <int D>
@@ -606,6 +617,12 @@ static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
   dim3 gkv((unsigned)(((a.S + 127) / 128) * a.B * a.Hkv));
   if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
+  if constexpr (D == 64) {
+    if (dq_waves(a, D) == 8) {
+      dq_launch<D, 8>(a, causal, st);
+      return hipGetLastError();
+    }
+  }
   dq_launch<D, 4>(a, causal, st);
   return hipGetLastError();
 }
