@@ -22,6 +22,7 @@ hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float
                         void*, void*, int64_t, int, int, int, const void*, hipStream_t);
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 int dta_gemm_tn_split(int, int, int);
+int dta_gemm_tn_cs_workers(int);
 hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*, void*,
                        hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
@@ -466,7 +467,7 @@ std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool o
   torch::Tensor slab, cs, db;
   if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
   if (with_colsum) {
-    cs = torch::empty({sp, M}, a.options().dtype(torch::kFloat32));
+    cs = torch::empty({dta_gemm_tn_cs_workers((int)K), M}, a.options().dtype(torch::kFloat32));
     db = torch::empty({M}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   }
   hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,

@@ -56,20 +56,58 @@ struct GemmTnArgs {
   int M, N, K, split, k_per_split;
   int tiles_m, tiles_n;
   int out_f32;
-  // fused column sums of A (the bias gradient sum_k dY[k, m] of the same Linear):
-  // f32 [split][M] partials, summed over splits by splitk_reduce_kernel (nullptr: off)
+  // column sums of A (the bias gradient sum_k dY[k, m] of the same Linear) by
+  // `cs_workers` extra workgroups of the same launch: f32 [cs_workers][M]
+  // partials, summed by splitk_reduce_kernel (nullptr: off)
   float* colsum;
+  int cs_workers, gemm_wgs;
 };
+
+// Extra workgroup of a gemm_tn launch: column sums of A over its share of the
+// K rows.  The GEMM grid leaves most CUs' second workgroup slot idle at these
+// shapes (e.g. 288 GEMM workgroups on 256 CUs x 2 slots), and these run there,
+// so the bias gradient costs neither a separate pass nor GEMM-workgroup time.
+__device__ void gemm_tn_colsum_worker(const GemmTnArgs& g, int w) {
+  const int rows = (g.K + g.cs_workers - 1) / g.cs_workers;
+  const int k0 = w * rows, k1 = min(g.K, k0 + rows);
+  for (int c8 = threadIdx.x * 8; c8 < g.M; c8 += 256 * 8) {  // 8 columns per thread
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {  // 8 rows in flight
+      bf16x8 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const bf16x8*>(g.a + (int64_t)(k + u) * g.lda + c8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[u][j]);
+    }
+    for (; k < k1; ++k) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(g.a + (int64_t)k * g.lda + c8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+    }
+    float* out = g.colsum + (int64_t)w * g.M + c8;
+    reinterpret_cast<float4*>(out)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    reinterpret_cast<float4*>(out)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
 
 template <bool SLAB>
 __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 2 * kGtTileBytes];  // [buf][A|B][64][256 B]
+  if ((int)blockIdx.x >= g.gemm_wgs) {  // column-sum workers (after every GEMM workgroup)
+    gemm_tn_colsum_worker(g, blockIdx.x - g.gemm_wgs);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   // bijective XCD remap: consecutive logical tiles (same split, neighbouring
   // output tiles -> shared A/B panels) land on the same XCD's L2
-  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int nwg = g.gemm_wgs, orig = blockIdx.x;
   const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   const int tiles = g.tiles_m * g.tiles_n;
@@ -82,13 +120,6 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
 
   // staging: 4 chunks of A and 4 of B per thread per stage (chunk e: row e>>4, 16-B chunk e&15)
   bf16x8 ra[4], rb[4];
-  // fused bias gradient (workgroups of output column 0 only): this thread's 4 A
-  // chunks per stage share the 16-B chunk tid & 15, so it keeps the 8 column
-  // partial sums of those columns in registers -- 32 VALU adds per stage
-  const bool do_cs = g.colsum != nullptr && tn == 0;
-  float cs[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
   auto gload = [&](int k0) {
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
@@ -100,12 +131,6 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
   auto lstore = [&](int buf) {
     char* ta = lds + buf * 2 * kGtTileBytes;
     char* tb = ta + kGtTileBytes;
-    if (do_cs) {
-#pragma unroll
-      for (int l = 0; l < 4; ++l)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) cs[j] += bf2f(ra[l][j]);
-    }
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       const int e = tid + 256 * l, row = e >> 4, ch = e & 15;
@@ -148,25 +173,6 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
     __syncthreads();
   }
 
-  if (do_cs) {
-    // sum the 16 threads of each 16-B chunk: lanes ch + 16x of every wave (shuffles), then the 4 waves (LDS)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16, kWave);
-      cs[j] += __shfl_xor(cs[j], 32, kWave);
-    }
-    float* red = reinterpret_cast<float*>(lds);  // [4 waves][16 chunks][8]; every stage's reads are done
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[(wave * 16 + lane) * 8 + j] = cs[j];
-    }
-    __syncthreads();
-    if (tid < 128) {
-      const float v = red[tid] + red[128 + tid] + red[256 + tid] + red[384 + tid];
-      g.colsum[(int64_t)sp * g.M + m0 + tid] = v;  // tid = 8 * chunk + j = column offset in the tile
-    }
-  }
-
   // epilogue: acc[i][j] rows m = m0 + wm*64 + 32i + mfma32_row(e), cols n = n0 + wn*64 + 32j + (lane & 31)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -188,16 +194,16 @@ __global__ void __launch_bounds__(256) gemm_tn_kernel(GemmTnArgs g) {
 }
 
 // out[M, N] = sum_s slab[s][M][N]   (bf16 or f32 out, 4 elements per thread);
-// blocks past the matrix sum the fused column-sum partials: cout[m] = sum_s cs[s][m]
+// blocks past the matrix sum the column-sum partials: cout[m] = sum_w cs[w][m]
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int split, int64_t mn,
                                                             void* out, int out_f32, const float* __restrict__ cs,
-                                                            int M, void* cout, int cout_f32) {
+                                                            int M, void* cout, int cout_f32, int ncs) {
   const int64_t mblocks = (mn / 4 + 255) / 256;
   if ((int64_t)blockIdx.x >= mblocks) {
     const int m = (int)(((int64_t)blockIdx.x - mblocks) * 256 + threadIdx.x);
     if (m < M) {
       float v = 0.f;
-      for (int s = 0; s < split; ++s) v += cs[(int64_t)s * M + m];
+      for (int s = 0; s < ncs; ++s) v += cs[(int64_t)s * M + m];
       if (cout_f32) static_cast<float*>(cout)[m] = v;
       else static_cast<bf16*>(cout)[m] = f2bf(v);
     }
@@ -236,7 +242,12 @@ int dta_gemm_tn_split(int M, int N, int K) {
 }
 
 // c: [M, N] (bf16 or f32, row stride ldc); slab: f32 [split * M * N] when split > 1
-// colsum (optional): f32 [split][M] scratch; cout: the bias gradient [M] (bf16 / f32 as out_f32)
+// colsum (optional): f32 [dta_gemm_tn_cs_workers(K)][M] scratch; cout: the bias gradient [M] (bf16 / f32 as out_f32)
+// 64 rows per worker: 8 row loads in flight per thread, and enough workers to
+// fill the CU slots the GEMM grid leaves idle (partials summed by colsum_kernel)
+int dta_gemm_tn_cs_workers(int K) { return (K + 63) / 64; }
+hipError_t dta_colsum_partials(const float* part, int nrows, int C, void* out, int out_f32, hipStream_t st);
+
 hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int M, int N,
                        int K, int split, float* slab, int out_f32, float* colsum, void* cout, hipStream_t st) {
   if (M % kGtBM || N % kGtBN || K % kGtBK || split < 1 || (K / kGtBK) % split) return hipErrorInvalidValue;
@@ -256,21 +267,21 @@ hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, v
   g.out_f32 = out_f32;
   g.colsum = cout ? colsum : nullptr;
   if (cout && !colsum) return hipErrorInvalidValue;
-  const int grid = g.tiles_m * g.tiles_n * split;
-  const unsigned cblocks = cout ? (unsigned)((M + 255) / 256) : 0u;
+  if (cout && M % 8) return hipErrorInvalidValue;
+  g.gemm_wgs = g.tiles_m * g.tiles_n * split;
+  g.cs_workers = cout ? dta_gemm_tn_cs_workers(K) : 0;
+  const int grid = g.gemm_wgs + g.cs_workers;
   if (split == 1) {
     g.c = c;
     hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(grid), dim3(256), 0, st, g);
-    if (cout)  // column sums only (mn = 0): one pass over the [1][M] partials
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cblocks), dim3(256), 0, st, static_cast<const float*>(nullptr), 1,
-                         (int64_t)0, static_cast<void*>(nullptr), out_f32, colsum, M, cout, out_f32);
   } else {
     if (ldc != N) return hipErrorInvalidValue;
     g.c = slab;
     hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(grid), dim3(256), 0, st, g);
     const int64_t mn = (int64_t)M * N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256) + cblocks), dim3(256), 0, st, slab,
-                       split, mn, c, out_f32, colsum, M, cout, out_f32);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256)), dim3(256), 0, st, slab, split, mn,
+                       c, out_f32, static_cast<const float*>(nullptr), 0, static_cast<void*>(nullptr), 0, 0);
   }
+  if (cout) DTA_HIP_CHECK(dta_colsum_partials(colsum, g.cs_workers, M, cout, out_f32, st));
   return hipGetLastError();
 }

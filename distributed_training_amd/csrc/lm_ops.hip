@@ -490,6 +490,13 @@ hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, 
   return hipGetLastError();
 }
 
+// out[c] = sum_r part[r][c] (fp32 [nrows][C] partials -> bf16 / f32)
+hipError_t dta_colsum_partials(const float* part, int nrows, int C, void* out, int out_f32, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, nrows, C,
+                     out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr);
+  return hipGetLastError();
+}
+
 hipError_t dta_bias_grad(const void* dy, int64_t N, int C, float* part, int nsplit, void* out, int out_f32,
                          hipStream_t st) {
   if (C % 8) return hipErrorInvalidValue;
