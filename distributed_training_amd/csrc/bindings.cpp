@@ -54,6 +54,7 @@ hipError_t dta_p2p_open(void*, const void*);
 int dta_p2p_num_wg(int64_t);
 hipError_t dta_p2p_allreduce(void*, float*, int64_t, float, int, hipStream_t);
 hipError_t dta_p2p_error(void*, int*);
+hipError_t dta_p2p_clear_error(void*);
 void dta_p2p_destroy(void*);
 void dta_p2p_set_ll(void*, int);
 hipError_t dta_p2p_ll_info(void*, unsigned long long*, unsigned long long*, int*, int*, long long*,
@@ -687,6 +688,7 @@ class PyP2PAllReduce {
     hip_ok(dta_p2p_error(state_, &e), "p2p error");
     return e;
   }
+  void clear_error() { hip_ok(dta_p2p_clear_error(state_), "p2p clear_error"); }
   void destroy() {
     if (state_) dta_p2p_destroy(state_);
     state_ = nullptr;
@@ -886,6 +888,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_ll", &PyP2PAllReduce::set_ll)
       .def("ll_info", &PyP2PAllReduce::ll_info)
       .def("regions", &PyP2PAllReduce::regions)
+      .def("clear_error", &PyP2PAllReduce::clear_error)
       .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())

@@ -96,27 +96,52 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwacc[i][j] = dbacc[i][j] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  for (int64_t row = r0 + wave; row < min(r0 + rows_per_block, N); row += 4) {
-    const float mu = RMS ? 0.f : mean[row];
-    const float rs = rstd[row];
+  const int64_t rend = min(r0 + rows_per_block, N);
+  // one row ahead in flight: the next row's x / dy / dres (raw bf16) and stats
+  // are loaded before this row's reductions, so a wave's rows do not serialise
+  // on load latency (the kernel is latency-, not bandwidth-bound at C = 768)
+  bf16x8 xn[NV], dn[NV], rn[NV];
+  float mun = 0.f, rsn = 0.f;
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = min((i * 64 + lane) * 8, C - 8);  // clamped: lanes past C re-read a valid chunk, unused
+      xn[i] = *reinterpret_cast<const bf16x8*>(x + row * C + c);
+      dn[i] = *reinterpret_cast<const bf16x8*>(dy + row * C + c);
+      if (dres) rn[i] = *reinterpret_cast<const bf16x8*>(dres + row * C + c);
+    }
+    mun = RMS ? 0.f : mean[row];
+    rsn = rstd[row];
+  };
+  float wv[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) load8(w + min((i * 64 + lane) * 8, C - 8), wv[i]);
+  if (r0 + wave < rend) fetch(r0 + wave);
+  for (int64_t row = r0 + wave; row < rend; row += 4) {
+    const float mu = mun, rs = rsn;
+    bf16x8 xc[NV], dc[NV], rc[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      xc[i] = xn[i];
+      dc[i] = dn[i];
+      if (dres) rc[i] = rn[i];
+    }
+    if (row + 4 < rend) fetch(row + 4);
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 8;
       if (c < C) {
-        float xv[8], dv[8], wv[8];
-        load8(x + row * C + c, xv);
-        load8(dy + row * C + c, dv);
-        load8(w + c, wv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[i][j] = (xv[j] - mu) * rs;
-          g[i][j] = dv[j] * wv[j];
+          const float xv = bf2f(xc[i][j]), dv = bf2f(dc[i][j]);
+          xh[i][j] = (xv - mu) * rs;
+          g[i][j] = dv * wv[i][j];
           s1 += g[i][j];
           s2 += g[i][j] * xh[i][j];
-          dwacc[i][j] += dv[j] * xh[i][j];
-          dbacc[i][j] += dv[j];
+          dwacc[i][j] += dv * xh[i][j];
+          dbacc[i][j] += dv;
         }
       }
     }
@@ -130,10 +155,8 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - m1 - xh[i][j] * m2);
         if (dres) {  // gradient arriving on the residual stream (fused accumulate)
-          float r[8];
-          load8(dres + row * C + c, r);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) o[j] += bf2f(rc[i][j]);
         }
         store8(dx + row * C + c, o);
       }

@@ -322,6 +322,13 @@ hipError_t dta_p2p_error(void* state, int* out) {
   return hipMemcpy(out, s->err, sizeof(int), hipMemcpyDeviceToHost);
 }
 
+// Re-arm after a timed-out exchange that was expected to be survivable (e.g. a
+// probe of an exchange form during calibration); every rank clears together.
+hipError_t dta_p2p_clear_error(void* state) {
+  auto* s = static_cast<P2PState*>(state);
+  return hipMemset(s->err, 0, sizeof(int));
+}
+
 void dta_p2p_destroy(void* state) {
   auto* s = static_cast<P2PState*>(state);
   if (!s) return;

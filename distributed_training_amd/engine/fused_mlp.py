@@ -193,11 +193,27 @@ class FusedMLPProgram:
             self.run_steps(steps)
             e1.record()
             torch.cuda.synchronize(self.device)
-            t = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64,
+            ms = e0.elapsed_time(e1)
+            # a form whose exchange timed out anywhere is ruled out (inf), not fatal:
+            # the error flag is re-armed on every rank and the next form is probed
+            if self._p2p._h.error() or (hasattr(self.comm, "_p2p") and self.comm._p2p is not None
+                                        and self.comm._p2p._h.error()):
+                logger.warning("MLP DDP step form %s timed out during calibration; excluded", mode)
+                ms = float("inf")
+            t = torch.tensor([ms], dtype=torch.float64,
                              device=self.device if dist.get_backend() == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             times[mode] = float(t.item())
-        self._p2p.check()
+            if times[mode] == float("inf"):
+                torch.cuda.synchronize(self.device)
+                dist.barrier()
+                self._p2p._h.clear_error()
+                if hasattr(self.comm, "_p2p") and self.comm._p2p is not None:
+                    self.comm._p2p._h.clear_error()
+                torch.cuda.synchronize(self.device)
+                dist.barrier()
+        if all(v == float("inf") for v in times.values()):
+            raise RuntimeError("no MLP DDP step form completed its calibration exchange")
         best = min(times, key=times.get)
         self.persistent = best != "step"
         self.xmode = best
