@@ -7,6 +7,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -23,6 +24,9 @@ hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 int dta_gemm_tn_split(int, int, int);
 int dta_gemm_tn_cs_workers(int);
+int dta_gemm_tn_gd_split(int, int, int);
+hipError_t dta_gemm_tn_gd(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*,
+                          void*, hipStream_t);
 hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*, void*,
                        hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
@@ -448,7 +452,9 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   return {dx, dw, db};
 }
 
-// C[M, N] = A^T B for A [K, M], B [K, N] bf16 row-major (the weight gradient dY^T X); split = 0: auto
+// C[M, N] = A^T B for A [K, M], B [K, N] bf16 row-major (the weight gradient dY^T X);
+// split = 0: LDS-DMA split-K kernel with its own split choice, > 0: that kernel with `split`,
+// < 0: the register-staged split-K kernel over -split slabs
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) { return dta_gemm_tn_split((int)M, (int)N, (int)K) > 0; }
 
 // C = A^T B (and, with_colsum, the column sums of A: the bias gradient of the same Linear)
@@ -462,20 +468,30 @@ std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool o
                   reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
               "gemm_tn: 16-byte aligned rows required");
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  const int sp = split > 0 ? (int)split : dta_gemm_tn_split((int)M, (int)N, (int)K);
-  TORCH_CHECK(sp > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
+  TORCH_CHECK(dta_gemm_tn_split((int)M, (int)N, (int)K) > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
   auto c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   torch::Tensor slab, cs, db;
-  if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
   if (with_colsum) {
     cs = torch::empty({dta_gemm_tn_cs_workers((int)K), M}, a.options().dtype(torch::kFloat32));
     db = torch::empty({M}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   }
-  hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,
-                     sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0,
-                     with_colsum ? cs.data_ptr<float>() : nullptr, with_colsum ? db.data_ptr() : nullptr,
-                     pick_stream(stream)),
-         "gemm_tn");
+  float* csp = with_colsum ? cs.data_ptr<float>() : nullptr;
+  void* dbp = with_colsum ? db.data_ptr() : nullptr;
+  if (split >= 0) {  // LDS-DMA split-K kernel (default)
+    const int sp = split > 0 ? (int)split : dta_gemm_tn_gd_split((int)M, (int)N, (int)K);
+    TORCH_CHECK(sp >= 1 && sp <= K / 32, "gemm_tn: split must be in [1, K / 32]");
+    if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
+    hip_ok(dta_gemm_tn_gd(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K,
+                          sp, sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, csp, dbp, pick_stream(stream)),
+           "gemm_tn");
+  } else {  // register-staged split-K kernel over -split slabs (kept for A/B measurements)
+    const int sp = (int)-split;
+    TORCH_CHECK((K / 64) % sp == 0, "gemm_tn: register-staged split must divide K / 64");
+    if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
+    hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,
+                       sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, csp, dbp, pick_stream(stream)),
+           "gemm_tn");
+  }
   if (with_colsum) return {c, db};
   return {c};
 }
@@ -864,7 +880,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_colsum", &gemm_tn_colsum, py::arg("a"), py::arg("b"), py::arg("out_f32") = false,
         py::arg("split") = 0, py::arg("stream") = -1);
   m.def("gemm_tn_supported", &gemm_tn_supported);
-  m.def("gemm_tn_split", &dta_gemm_tn_split);
+  m.def("gemm_tn_split", &dta_gemm_tn_gd_split);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),

@@ -77,6 +77,37 @@ __device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Column sums of fp32 [nrows, C] partials for columns c0 .. c0+31, by one
+// 256-thread workgroup: 32 columns x 8 row groups, 8 independent loads in
+// flight per thread, LDS reduce.  out: bf16 and/or f32 (nullptr: skip).
+__device__ __forceinline__ void colsum_block(const float* __restrict__ part, int nrows, int C, int c0,
+                                             bf16* __restrict__ out_bf16, float* __restrict__ out_f32) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = c0 + cl;
+  float s = 0.f;
+  if (c < C) {
+    int r = rg;
+    for (; r + 56 < nrows; r += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(r + 8 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < nrows; r += 8) s += part[(int64_t)r * C + c];
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][cl];
+    if (out_bf16) out_bf16[c] = f2bf(t);
+    if (out_f32) out_f32[c] = t;
+  }
+}
+
 // XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): blocks that land on one XCD (b % 8 equal)
 // get a contiguous chunk of the logical tile space so they share L2 panels.

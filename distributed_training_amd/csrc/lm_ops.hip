@@ -184,34 +184,14 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
-// Column sums of the [nrows, C] partials: 32 columns x 8 row groups per
-// workgroup, 8 independent loads in flight per thread, LDS reduce.
-__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int nrows, int C,
-                                                     bf16* __restrict__ out_bf16, float* __restrict__ out_f32) {
-  __shared__ float red[8][33];
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  float s = 0.f;
-  if (c < C) {
-    int r = rg;
-    for (; r + 56 < nrows; r += 64) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(r + 8 * u) * C + c];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; r < nrows; r += 8) s += part[(int64_t)r * C + c];
-  }
-  red[rg][cl] = s;
-  __syncthreads();
-  if (rg == 0 && c < C) {
-    float t = 0.f;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) t += red[g][cl];
-    if (out_bf16) out_bf16[c] = f2bf(t);
-    if (out_f32) out_f32[c] = t;
-  }
+// Column sums of one or two [nrows, C] partial sets (colsum_block): blocks
+// [0, ceil(C/32)) finish set 0, the rest set 1 (e.g. a norm's dw and db in one launch).
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part0, const float* __restrict__ part1,
+                                                     int nrows, int C, bf16* __restrict__ ob0, float* __restrict__ of0,
+                                                     bf16* __restrict__ ob1, float* __restrict__ of1) {
+  const int nb = (C + 31) / 32;
+  if ((int)blockIdx.x < nb) colsum_block(part0, nrows, C, blockIdx.x * 32, ob0, of0);
+  else colsum_block(part1, nrows, C, (blockIdx.x - nb) * 32, ob1, of1);
 }
 
 // Partial column sums of a bf16 [N, C] matrix (bias gradients): a workgroup
@@ -504,19 +484,21 @@ hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, 
                                     dw_part, db_part, N, C, rows_per_block, (const bf16*)dres, st);
   if (r != hipSuccess) return r;
   const int nblk = (int)((N + rows_per_block - 1) / rows_per_block);
-  dim3 g((C + 31) / 32);
-  hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, dw_part, nblk, C, grads_f32 ? nullptr : (bf16*)dw,
-                     grads_f32 ? (float*)dw : nullptr);
-  if (!rms)
-    hipLaunchKernelGGL(colsum_kernel, g, dim3(256), 0, st, db_part, nblk, C, grads_f32 ? nullptr : (bf16*)db,
-                       grads_f32 ? (float*)db : nullptr);
+  const int nb = (C + 31) / 32;
+  bf16* w16 = grads_f32 ? nullptr : (bf16*)dw;
+  float* w32 = grads_f32 ? (float*)dw : nullptr;
+  bf16* b16 = grads_f32 ? nullptr : (bf16*)db;
+  float* b32 = grads_f32 ? (float*)db : nullptr;
+  hipLaunchKernelGGL(colsum_kernel, dim3(rms ? nb : 2 * nb), dim3(256), 0, st, dw_part, db_part, nblk, C, w16, w32, b16,
+                     b32);
   return hipGetLastError();
 }
 
 // out[c] = sum_r part[r][c] (fp32 [nrows][C] partials -> bf16 / f32)
 hipError_t dta_colsum_partials(const float* part, int nrows, int C, void* out, int out_f32, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, nrows, C,
-                     out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, static_cast<const float*>(nullptr),
+                     nrows, C, out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr,
+                     static_cast<bf16*>(nullptr), static_cast<float*>(nullptr));
   return hipGetLastError();
 }
 
@@ -526,8 +508,9 @@ hipError_t dta_bias_grad(const void* dy, int64_t N, int C, float* part, int nspl
   const int rps = (int)((N + nsplit - 1) / nsplit);
   hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3((C + 511) / 512, nsplit), dim3(256), 0, st, (const bf16*)dy, N,
                      C, rps, part);
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, nsplit, C,
-                     out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, static_cast<const float*>(nullptr),
+                     nsplit, C, out_f32 ? nullptr : (bf16*)out, out_f32 ? (float*)out : nullptr,
+                     static_cast<bf16*>(nullptr), static_cast<float*>(nullptr));
   return hipGetLastError();
 }
 

@@ -44,7 +44,8 @@ def linear_shapes():
 
 
 def main():
-    linear_shapes()
+    if "--no-linear" not in sys.argv:
+        linear_shapes()
     C = native()
     for K, M, N in SHAPES:
         a = torch.randn(K, M, device="cuda").bfloat16()
@@ -52,13 +53,23 @@ def main():
         fl = 2.0 * K * M * N
         t_ref = timeit(lambda: torch.mm(a.t(), b))
         row = {"K": K, "M": M, "N": N, "torch_us": round(t_ref, 1), "torch_TF": round(fl / t_ref / 1e6, 1)}
-        for sp in (1, 2, 4, 8, 0):
-            if (K // 64) % max(sp, 1):
+        for sp in (1, 2, 4, 8):  # register-staged split-K kernel
+            if (K // 64) % sp:
+                continue
+            t = timeit(lambda: C.gemm_tn(a, b, False, -sp))
+            row[f"reg_s{sp}_us"] = round(t, 1)
+        tiles = (M // 128) * (N // 128)
+        for sp in sorted({1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32}):  # LDS-DMA kernel
+            if sp > 1 and tiles * sp > 4096:
                 continue
             t = timeit(lambda: C.gemm_tn(a, b, False, sp))
-            row[f"native_s{sp}_us"] = round(t, 1)
-        row["auto_split"] = C.gemm_tn_split(M, N, K)
-        best = min(v for k, v in row.items() if k.startswith("native_"))
+            row[f"gd_s{sp}_us"] = round(t, 1)
+        row["gd_auto_split"] = C.gemm_tn_split(M, N, K)
+        t = timeit(lambda: C.gemm_tn(a, b, False, 0))
+        row["gd_auto_us"] = round(t, 1)
+        t = timeit(lambda: C.gemm_tn_colsum(a, b, False, 0))
+        row["gd_auto_colsum_us"] = round(t, 1)
+        best = min(v for k, v in row.items() if k.endswith("_us") and not k.startswith("torch") and "colsum" not in k)
         row["native_best_TF"] = round(fl / best / 1e6, 1)
         print(json.dumps(row), flush=True)
 

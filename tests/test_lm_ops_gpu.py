@@ -279,9 +279,13 @@ def test_fused_model_matches_fp32_reference(arch):
 
 
 @pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
-                                         (4096, 2304, 768, 0)])
+                                         (4096, 2304, 768, 0), (4096, 2304, 768, -2), (1024, 384, 256, 7),
+                                         (512, 256, 128, 0), (2048, 512, 384, 64), (2048, 512, 384, 22),
+                                         (2048, 512, 384, 32), (1024, 384, 256, -1)])
 def test_gemm_tn_weight_gradient(K, M, N, split):
-    """C = A^T B (dW = dY^T X) on the split-K MFMA kernel vs fp32 torch."""
+    """C = A^T B (dW = dY^T X) vs fp32 torch: the LDS-DMA split-K kernel (split 0: its own choice; splits that
+    do not divide K; 1-3 stages per split, i.e. the ring's prologue/tail counts) and the register-staged
+    kernel (split < 0)."""
     from distributed_training_amd.ops import native
 
     torch.manual_seed(8)
@@ -300,7 +304,7 @@ def test_gemm_tn_weight_gradient(K, M, N, split):
 
 
 @pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
-                                         (4096, 2304, 768, 0)])
+                                         (4096, 2304, 768, 0), (1024, 384, 256, 7), (1024, 384, 256, -4)])
 def test_gemm_tn_fused_bias_gradient(K, M, N, split):
     """dW = dY^T X and db = column sums of dY from one split-K launch vs fp32 torch."""
     from distributed_training_amd.ops import native
