@@ -458,8 +458,11 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) { return dta_gemm_tn_split((int)M, (int)N, (int)K) > 0; }
 
 // C = A^T B (and, with_colsum, the column sums of A: the bias gradient of the same Linear)
+// c_out / db_out (optional): write the results there (e.g. the parameter's
+// slice of a flat gradient buffer) instead of fresh tensors
 std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream,
-                                        bool with_colsum) {
+                                        bool with_colsum, c10::optional<torch::Tensor> c_out = c10::nullopt,
+                                        c10::optional<torch::Tensor> db_out = c10::nullopt) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
               "gemm_tn: bf16 GPU operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0), "gemm_tn: A [K, M], B [K, N]");
@@ -469,11 +472,26 @@ std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool o
               "gemm_tn: 16-byte aligned rows required");
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
   TORCH_CHECK(dta_gemm_tn_split((int)M, (int)N, (int)K) > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
-  auto c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  const auto odt = out_f32 ? torch::kFloat32 : torch::kBFloat16;
+  torch::Tensor c;
+  if (c_out.has_value()) {
+    c = *c_out;
+    TORCH_CHECK(c.is_cuda() && c.scalar_type() == odt && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
+                    c.is_contiguous(),
+                "gemm_tn: c_out must be a contiguous [M, N] tensor of the output dtype");
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(odt));
+  }
   torch::Tensor slab, cs, db;
   if (with_colsum) {
     cs = torch::empty({dta_gemm_tn_cs_workers((int)K), M}, a.options().dtype(torch::kFloat32));
-    db = torch::empty({M}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+    if (db_out.has_value()) {
+      db = *db_out;
+      TORCH_CHECK(db.is_cuda() && db.scalar_type() == odt && db.numel() == M && db.is_contiguous(),
+                  "gemm_tn: db_out must be a contiguous [M] tensor of the output dtype");
+    } else {
+      db = torch::empty({M}, a.options().dtype(odt));
+    }
   }
   float* csp = with_colsum ? cs.data_ptr<float>() : nullptr;
   void* dbp = with_colsum ? db.data_ptr() : nullptr;
@@ -496,13 +514,15 @@ std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool o
   return {c};
 }
 
-torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream) {
-  return gemm_tn_impl(a, b, out_f32, split, stream, false)[0];
+torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream,
+                      c10::optional<torch::Tensor> c_out) {
+  return gemm_tn_impl(a, b, out_f32, split, stream, false, c_out)[0];
 }
 
 std::vector<torch::Tensor> gemm_tn_colsum(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split,
-                                          int64_t stream) {
-  return gemm_tn_impl(a, b, out_f32, split, stream, true);
+                                          int64_t stream, c10::optional<torch::Tensor> c_out,
+                                          c10::optional<torch::Tensor> db_out) {
+  return gemm_tn_impl(a, b, out_f32, split, stream, true, c_out, db_out);
 }
 
 // bias gradient = column sums of dy [N, C] (bf16), returned in `dtype`'s float type (bf16 or f32)
@@ -876,9 +896,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_", &rope_);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out_f32") = false, py::arg("split") = 0,
-        py::arg("stream") = -1);
+        py::arg("stream") = -1, py::arg("c_out") = py::none());
   m.def("gemm_tn_colsum", &gemm_tn_colsum, py::arg("a"), py::arg("b"), py::arg("out_f32") = false,
-        py::arg("split") = 0, py::arg("stream") = -1);
+        py::arg("split") = 0, py::arg("stream") = -1, py::arg("c_out") = py::none(), py::arg("db_out") = py::none());
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_split", &dta_gemm_tn_gd_split);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);

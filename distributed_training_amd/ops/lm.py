@@ -210,23 +210,45 @@ def rms_norm(x, w, eps: float = 1e-5):
 _WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this hipBLASLt fills the chip by itself
 
 
-def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False):
+def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The slice of the DDP engine's flat gradient buffer that ``p``'s gradient
+    goes to, when this backward may write it there directly: the engine hands
+    fresh gradients over (``zero_grad(set_to_none=True)``), ``p.grad`` is unset
+    and no other use of ``p`` in this backward has claimed the slice (a second
+    use would overwrite it before autograd sums the two).  Autograd then adopts
+    the returned view as ``p.grad`` and the engine's per-bucket copy kernel has
+    nothing to move (parallel/ddp.py)."""
+    tag = getattr(p, "_dta_flat", None) if p is not None else None
+    if tag is None or p.grad is not None:
+        return None
+    group, i = tag
+    if not group.steal_ok or not group.grad.is_cuda or group.grad.dtype != p.dtype or i in group.direct_claimed:
+        return None
+    group.direct_claimed.add(i)
+    return group.grad_view(i)
+
+
+def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
+                 b: Optional[torch.Tensor] = None):
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
     Small outputs with a long token reduction (GPT-2: 768 x 768 .. 3072 x 768
     over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip), which fills
     256 CUs where a library GEMM tiling only the output does not (measured
-    1.4-1.8x on the attention projections) and sums the bias gradient from the
-    dy tiles it already stages (no separate pass over dy); large outputs stay
-    on hipBLASLt."""
+    1.3-2.0x on the four GPT-2 shapes) and sums the bias gradient in extra
+    workgroups of the same launch; large outputs stay on hipBLASLt.  With the
+    parameters ``w`` / ``b`` given, the results go straight into their flat
+    gradient slices when :func:`_grad_dest` allows it."""
     K, M = dy2.shape
     N = x2.shape[1]
     if (M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and (M // 128) * (N // 128) <= _WGRAD_NATIVE_MAX_TILES
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
         x2 = x2.contiguous() if x2.stride(0) % 8 else x2
+        cw = _grad_dest(w)
         if with_bias:
-            dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1)
+            cb = _grad_dest(b)
+            dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
             return dw, db
-        return native().gemm_tn(dy2, x2, False, 0, -1)
+        return native().gemm_tn(dy2, x2, False, 0, -1, cw)
     dw = torch.mm(dy2.t(), x2)
     if with_bias:
         return dw, native().bias_grad(dy2, False, -1)
@@ -241,11 +263,13 @@ class _Linear(Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.params = (w, b)  # the Parameters themselves (their .grad decides a direct write)
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        pw, pb = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
@@ -254,7 +278,7 @@ class _Linear(Function):
             dx = torch.mm(dy2, w).view(*x.shape[:-1], w.shape[1])
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            r = _weight_grad(dy2, x.reshape(-1, x.shape[-1]), with_bias=want_b)
+            r = _weight_grad(dy2, x.reshape(-1, x.shape[-1]), with_bias=want_b, w=pw, b=pb if want_b else None)
             dw, db = r if want_b else (r, None)
         elif want_b:
             db = native().bias_grad(dy2, False, -1)

@@ -15,9 +15,10 @@ MI355X-first design:
   enough to amortise RCCL launch latency, small enough for >= 4-8 buckets of
   overlap on GPT-2-sized models);
 * ``zero_grad(set_to_none=True)`` drops the views so autograd hands each
-  gradient over without an accumulate-add kernel; when a bucket is ready all
-  its gradients are moved into the bucket slice by ONE multi-tensor copy
-  kernel (with the 1/world_size pre-scale fused when the backend has no
+  gradient over without an accumulate-add kernel; the native Linear backward
+  writes weight / bias gradients straight into their slices (ops/lm.py
+  ``_grad_dest``), and what else arrives as a fresh tensor is moved into the
+  bucket slice by ONE multi-tensor copy kernel (with the 1/world_size pre-scale fused when the backend has no
   ``avg``) -- instead of one ``grad += new`` kernel per parameter;
 * a post-accumulate-grad hook per parameter counts readiness; ready buckets
   are launched strictly in bucket order (identical collective order on every
@@ -108,6 +109,7 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------ per step
     def _reset_iteration(self) -> None:
+        self.flat.direct_claimed.clear()
         self._ready = [0] * len(self.buckets)
         self._next = 0
         self._works = []

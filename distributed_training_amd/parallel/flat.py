@@ -70,6 +70,9 @@ class FlatParamGroup:
         # backward (FSDP reduce-scatters into the slices): zero_grad(set_to_none)
         # then drops the gradients and calls it instead of zero-filling the buffer
         self.fresh_hook: Optional[Callable[[], None]] = None
+        # parameters whose gradient a backward already wrote straight into its
+        # slice since the last zero_grad(set_to_none) (ops/lm.py _grad_dest)
+        self.direct_claimed: set = set()
         for i, p in enumerate(self.params):
             p.data = self.param_view(i)
             p.grad = self.grad_view(i)
@@ -118,6 +121,7 @@ class FlatParamGroup:
         into the flat buffer in one batched copy per bucket).  Otherwise zero
         the flat buffer and keep the views."""
         if set_to_none and (self.steal_ok or self.fresh_hook is not None):
+            self.direct_claimed.clear()
             for p in self.params:
                 p.grad = None
             if self.fresh_hook is not None:

@@ -142,6 +142,54 @@ def test_gpt2_tiny_trains_on_gpu():
     assert losses[-1] < losses[0] * 0.5, losses
 
 
+def test_ddp_linear_gradients_written_into_flat_buffer():
+    """Native Linear backward writes dW / db straight into the DDP engine's flat
+    gradient slices (no bucket copy), a Linear used twice in one backward still
+    gets the sum of both uses, and gradients match an un-wrapped copy."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = lm.Linear(128, 256)
+            self.b = lm.Linear(256, 128)
+            self.shared = lm.Linear(128, 128)
+
+        def forward(self, x):
+            h = self.shared(self.b(lm.gelu(self.a(x))))
+            return self.shared(h)  # second use of the same weight in this backward
+
+    torch.manual_seed(3)
+    dev = torch.device(DEV, 0)
+    net = Net().to(dev).bfloat16()
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    copied = []
+    orig = ddp._gather_into_bucket
+
+    def spy(b, scale):
+        copied.extend(ddp.flat.names[i] for i in ddp._pending[b])
+        return orig(b, scale)
+
+    ddp._gather_into_bucket = spy
+    x = torch.randn(512, 128, device=dev).bfloat16()
+    for it in range(2):
+        ddp.zero_grad(set_to_none=True)
+        copied.clear()
+        ddp(x).float().square().mean().backward()
+        assert "a.weight" not in copied and "b.weight" not in copied and "a.bias" not in copied, copied
+        for name, p in ref.named_parameters():
+            p.grad = None
+        ref(x).float().square().mean().backward()
+        for i, (name, p) in enumerate(net.named_parameters()):
+            q = dict(ref.named_parameters())[name]
+            assert _rel(p.grad, q.grad) < 2e-2, (it, name)
+        assert all(ddp.flat.grad_is_view(i) for i in range(len(ddp.flat.params)))
+
+
 def test_llama_tiny_fsdp_trains_on_gpu():
     from distributed_training_amd.models.llama import Block, Llama, LlamaConfig
     from distributed_training_amd.ops.optim import FusedAdamW
