@@ -98,6 +98,12 @@ class _Unit:
         self.full.register_post_accumulate_grad_hook(self._post_backward)
         self._bwd_ready = False
         self.in_backward = False  # between this unit's pre-backward and post-backward
+        # one rank: the shard IS the whole flat parameter, so "gathering" is
+        # pointing the unit at the shard's compute copy (no buffer, no copy) --
+        # torch's FSDP likewise runs FULL_SHARD as NO_SHARD at world size 1
+        self.alias = ws == 1
+        if self.alias:
+            self.full.untyped_storage().resize_(0)  # until unshard() points it at the shard
         self.free()  # storage exists only while the unit is gathered
 
     # ---------------------------------------------------------- storage
@@ -107,6 +113,9 @@ class _Unit:
             st.resize_(self._nbytes)
 
     def free(self) -> None:
+        if self.alias:  # the storage is the shard's: never released here
+            self.gathered = False
+            return
         self.full.untyped_storage().resize_(0)
         self.gathered = False
 
@@ -121,6 +130,12 @@ class _Unit:
         if self.gathered or self.pending is not None:
             if not async_op:
                 self.wait()
+            return
+        if self.alias:
+            src = self.shard_source()
+            if self.full.data_ptr() != src.data_ptr():
+                self.full.data = src
+            self.gathered = True
             return
         self._alloc()
         work = self.owner.comm.all_gather_into(self.full.data, self.shard_source(), async_op=True)

@@ -102,6 +102,7 @@ def _fsdp_parity(rank, ws, wrap, opt_name, accum=False):
     assert len(fs.units) == (4 if wrap else 1)
     for u in fs.units:
         assert u.total % (ws * 16) == 0 and u.shard_size * ws == u.total
+        assert u.alias == (ws == 1)
     if opt_name == "adamw":
         o1 = torch.optim.AdamW(ref.parameters(), lr=1e-2)
         o2 = FusedAdamW(fs.parameters(), lr=1e-2)
@@ -152,6 +153,13 @@ def test_native_fsdp_matches_single_process(wrap, opt_name, accum):
 
 def _fsdp_ws(rank, ws):
     _fsdp_parity(rank, ws, True, "adamw", False)
+
+
+@pytest.mark.parametrize("wrap,opt_name,accum", [(True, "adamw", True), (False, "sgd", False)])
+def test_native_fsdp_single_rank_aliases_shard(wrap, opt_name, accum):
+    """World size 1: units point at the shard's compute copy instead of gathering
+    a copy of it (NO_SHARD behaviour); training, accumulation, state dicts still match."""
+    run_gloo(_fsdp_parity, 1, wrap, opt_name, accum)
 
 
 @pytest.mark.parametrize("ws", [4, 8])
