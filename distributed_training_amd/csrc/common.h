@@ -44,16 +44,37 @@ __device__ __forceinline__ void store8(float* p, const float* f) {
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// DPP move of `v` (lanes outside ROWMASK keep `old`): a VALU modifier, a few
+// cycles, where __shfl_xor is an LDS-path ds_bpermute with ~100+ cycles of
+// latency per step -- six of those sat on the per-step critical path of the
+// persistent MLP loop's loss phase.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_mov(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                               CTRL, ROWMASK, 0xf, false));
+}
+
+// Full-wave sum / max, result in every lane (requires all 64 lanes active):
+// quad swaps, half-row and row mirrors give each 16-lane row its total; row
+// broadcasts 15 and 31 chain the rows into lane 63, which is read back.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
+  v += dpp_mov<0xB1, 0xf>(0.f, v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E, 0xf>(0.f, v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141, 0xf>(0.f, v);  // row_half_mirror
+  v += dpp_mov<0x140, 0xf>(0.f, v);  // row_mirror
+  v += dpp_mov<0x142, 0xa>(0.f, v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_mov<0x143, 0xc>(0.f, v);  // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
-  return v;
+  v = fmaxf(v, dpp_mov<0xB1, 0xf>(v, v));
+  v = fmaxf(v, dpp_mov<0x4E, 0xf>(v, v));
+  v = fmaxf(v, dpp_mov<0x141, 0xf>(v, v));
+  v = fmaxf(v, dpp_mov<0x140, 0xf>(v, v));
+  v = fmaxf(v, dpp_mov<0x142, 0xa>(v, v));
+  v = fmaxf(v, dpp_mov<0x143, 0xc>(v, v));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // Sum over the 32 lanes that share one half of the wave (lanes 0-31 or 32-63).
