@@ -464,6 +464,9 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   const SgdH hbase{a.lr, a.momentum, a.dampening, a.weight_decay, a.nesterov, a.maximize, 0};
   const float lscale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
 
+  float dy_keep[OUT], loss_keep = 0.f;  // one rank: wave 0's dY / loss, finished after its backward
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) dy_keep[o] = 0.f;
   for (int s = 0; s < a.nsteps; ++s) {
     const int cb = s & 1;
     const bf16* Xb = Xs + cb * 32 * kMpXs;
@@ -567,26 +570,28 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           row[IN + 1 + o] = f2bf(dy[o]);
         }
       }
-      // db2 = sum over samples; loss
+      if constexpr (multi) {
+        // db2 = sum over samples, pushed into the exchange with the other gradients; loss
 #pragma unroll
-      for (int o = 0; o < OUT; ++o) {
-        const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
-        if (lane == 0) {
-          if (multi) {
+        for (int o = 0; o < OUT; ++o) {
+          const float db = wave_sum(hh == 0 ? dy[o] : 0.f);
+          if (lane == 0) {
             if (XM == 3) st_sc(a.xg_out + (long long)((xe0 + s + 1) & 1) * a.xe + NT * 1024 + o, db);
             else if (XM == 2) xpush_owner(a, xe0 + s + 1, a.hidden * IN + 2 * a.hidden + o, db);
             else xpush(a, xe0 + s + 1, a.o_b2 + o, db);
-          } else {
-            SgdH hs = hbase;
-            hs.first = first;
-            sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hs);
           }
         }
-      }
-      const float lsum = wave_sum(hh == 0 ? lossr : 0.f);
-      if (lane == 0) {
-        a.loss_ring[lcur % a.loss_len] = lsum * lscale;
-        ++lcur;
+        const float lsum = wave_sum(hh == 0 ? lossr : 0.f);
+        if (lane == 0) {
+          a.loss_ring[lcur % a.loss_len] = lsum * lscale;
+          ++lcur;
+        }
+      } else {
+        // one rank: only wave 0 reads b2, so its update (and the loss sum) wait
+        // for the tail of wave 0's backward instead of holding every wave at barrier 2
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) dy_keep[o] = hh == 0 ? dy[o] : 0.f;
+        loss_keep = hh == 0 ? lossr : 0.f;
       }
     }
     if (gthr && s + 1 < a.nsteps) store_rows(cb ^ 1);
@@ -783,6 +788,24 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         xreduce_sgd<PLAIN, false>(a, xe0 + s + 1, Pf, Mf, Wb, hbase, first);
       }
       if (XM != 3) lds_barrier();
+    }
+    if constexpr (!multi) {
+      if (wave == 0) {  // the deferred output-bias update and loss of this step (see the loss phase)
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          const float db = wave_sum(dy_keep[o]);
+          if (lane == 0) {
+            SgdH hb = hbase;
+            hb.first = first;
+            sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hb);
+          }
+        }
+        const float lsum = wave_sum(loss_keep);
+        if (lane == 0) {
+          a.loss_ring[lcur % a.loss_len] = lsum * lscale;
+          ++lcur;
+        }
+      }
     }
     MP_STAMP(5);
     first = 0;
