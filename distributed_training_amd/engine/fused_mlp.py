@@ -19,6 +19,7 @@ device ring and a device-side cursor walks it.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 from typing import Dict, List, Optional
@@ -134,7 +135,10 @@ class FusedMLPProgram:
         # index ring: whole epochs, at least one graph (or one persistent launch)
         # beyond an epoch, so uploads for epoch e+1 can be enqueued while epoch
         # e's steps are still queued
-        ahead = self.chunk_steps if self.persistent else 2 * self.graph_steps  # (covers both modes)
+        # persistent: room for two launches plus an epoch, so the next launch's
+        # indices upload on a side stream while the current launch runs (slots
+        # of the two launches never overlap; _run_persistent)
+        ahead = 2 * self.chunk_steps if self.persistent else 2 * self.graph_steps
         k = max(2, -(-ahead // S) + 1)
         self.R = S * k
         self.ring = torch.zeros(self.R, self.B, dtype=torch.int32, device=dev)
@@ -142,6 +146,12 @@ class FusedMLPProgram:
         self.stage = mf.make_stage(dev)
         self.loss_ring = torch.zeros(loss_len, device=dev)
         self._staging: List = []   # (pinned tensor, event) kept alive until the copy ran
+        # persistent mode: index uploads on their own stream, ordered after the
+        # launch before the current one (whose ring slots they may reuse) and
+        # before the launch that reads them
+        self._up_stream = torch.cuda.Stream(dev) if self.persistent and dev.type == "cuda" else None
+        self._launch_done: List = []  # completion events of the last two persistent launches
+        self._up_done = None
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.loss_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
@@ -153,9 +163,14 @@ class FusedMLPProgram:
     def _reset_state(self) -> None:
         """Training state back to step 0 with the module's weights (the module
         itself is only written by :meth:`store_to_module`)."""
+        if self._up_stream is not None:  # uploads in flight land before the ring is cleared ...
+            torch.cuda.current_stream(self.device).wait_stream(self._up_stream)
+            self._launch_done, self._up_done = [], None
         for t in (*self.P, *self.G, *(m for m in self.M if m is not None)):
             t.zero_()
         self.ring.zero_()
+        if self._up_stream is not None:  # ... and later ones after it
+            self._up_stream.wait_stream(torch.cuda.current_stream(self.device))
         self.cursor.zero_()
         self.loss_ring.zero_()
         self.loss_cursor.zero_()
@@ -166,6 +181,7 @@ class FusedMLPProgram:
         self.mom_started = False
         self.launched = 0          # global steps enqueued (== device cursor when drained)
         self.host_step = 0         # global steps whose indices are uploaded
+        self._last_start = 0       # first step of the last persistent launch
         self.next_epoch = 0        # next epoch to upload
         self._batch_of: Dict[int, int] = {}
         self.load_from_module()
@@ -379,7 +395,11 @@ class FusedMLPProgram:
     def _upload_epoch(self) -> None:
         e = self.next_epoch
         S, B, R = self.steps_per_epoch, self.B, self.R
-        assert self.host_step + S - R <= self.launched, "index ring overrun"
+        # slots of steps still to run are never overwritten; with side-stream uploads
+        # the launch in flight (from _last_start on) must keep its slots as well
+        side = self._up_stream is not None and self.persistent  # (calibration may pick the per-step form)
+        floor = self._last_start if side else self.launched
+        assert self.host_step + S - R <= floor, "index ring overrun"
         self.loader.sampler.set_epoch(e)
         idx = self.loader.epoch_indices().to(torch.int32)
         host = self._pinned_buffer(S, B)
@@ -388,11 +408,17 @@ class FusedMLPProgram:
         last = idx.numel() - (S - 1) * B
         r0 = self.host_step % R
         n1 = min(S, R - r0)
-        self.ring[r0:r0 + n1].copy_(host[:n1], non_blocking=True)
-        if n1 < S:
-            self.ring[0:S - n1].copy_(host[n1:], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        up = self._up_stream if side else None
+        with torch.cuda.stream(up) if up is not None else contextlib.nullcontext():
+            if up is not None and len(self._launch_done) == 2:
+                up.wait_event(self._launch_done[0])  # the launch before the current one has run
+            self.ring[r0:r0 + n1].copy_(host[:n1], non_blocking=True)
+            if n1 < S:
+                self.ring[0:S - n1].copy_(host[n1:], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        if up is not None:
+            self._up_done = ev
         self._staging.append((host, ev))
         for j in range(S):
             self._batch_of[self.host_step + j] = B if j < S - 1 else last
@@ -424,14 +450,38 @@ class FusedMLPProgram:
         end = self.launched + n
         hp = self.hyper()
         while self.launched < end:
-            k = min(end - self.launched, self.R - self.steps_per_epoch)
+            k = min(end - self.launched, self.chunk_steps)
             self._ensure(self.launched + k)
+            if self._up_done is not None:
+                torch.cuda.current_stream(self.device).wait_event(self._up_done)
+                self._up_done = None
             mf.persistent_steps(self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor,
                                 self.mom_started_dev, self.P[0], self.M[0], self.layout, self.B, k, self.act,
                                 self.loss, 1.0 / self.ws, hp, xinfo=self._xinfo)
+            self._last_start = self.launched
+            if self._up_stream is not None:
+                done = torch.cuda.Event()
+                done.record()
+                self._launch_done = (self._launch_done + [done])[-2:]
             for j in range(k):
                 self._batch_of.pop(self.launched + j, None)
             self.launched += k
+            self._prefetch()
+
+    def _prefetch(self) -> None:
+        """Pipelined index loading: while a launch runs, upload the indices of
+        the next one (host sampler work + H2D on the side stream), so the next
+        ``run_steps`` call -- e.g. the first after a warm-up -- finds them ready.
+        The sampler's epoch is left as it was."""
+        if self._up_stream is None or not self.persistent:
+            return
+        S = self.steps_per_epoch
+        upto = min(self.launched + self.chunk_steps, self._last_start + self.R - S)
+        sampler = self.loader.sampler
+        ep = getattr(sampler, "epoch", None)
+        self._ensure(upto)
+        if ep is not None:
+            sampler.set_epoch(ep)
 
     @torch.no_grad()
     def run_steps(self, n: int) -> None:
@@ -456,9 +506,15 @@ class FusedMLPProgram:
             self.launched += 1
 
     def run_epoch(self, epoch: int) -> int:
-        if self.host_step == self.launched and self.next_epoch != epoch:
-            self.seek_epoch(epoch)
         S = self.steps_per_epoch
+        ahead = (self.host_step - self.launched) // S  # whole epochs uploaded ahead (prefetch)
+        if self.launched % S == 0 and self.next_epoch - ahead != epoch:
+            # the prefetched epochs are not the requested one: drop them (nothing has
+            # read their ring slots) and restart the index stream at ``epoch``
+            for j in range(self.launched, self.host_step):
+                self._batch_of.pop(j, None)
+            self.host_step = self.launched
+            self.seek_epoch(epoch)
         self.run_steps(S)
         return S
 
