@@ -1,0 +1,77 @@
+"""T3: the 8-rank node's sharding / bucketing arithmetic in ONE
+process over torch's ``fake`` process group (collectives are no-ops, so only
+shapes, padding, unit layout and the control flow of a step are checked; the
+numerics at ws = 4 / 8 are covered over gloo in test_parallel_cpu.py)."""
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+@pytest.fixture
+def fake_pg():
+    from torch.testing._internal.distributed.fake_pg import FakeStore
+
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    dist.init_process_group("fake", store=FakeStore(), rank=3, world_size=8)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fsdp_units_at_world_8(fake_pg):
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_layer=3, n_head=2, n_embd=40, vocab_size=101, block_size=16)
+    m = GPT2(cfg)
+    n_params = sum(p.numel() for p in m.parameters())
+    fs = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={GPT2.block_class})
+    assert fs.world_size == 8 and len(fs.units) == cfg.n_layer + 1  # blocks + root
+    covered = 0
+    for u in fs.units:
+        assert u.total % (8 * 16) == 0 and u.shard_size * 8 == u.total  # 16-element aligned shards
+        assert sum(u._split_sizes) == u.total
+        assert all(o % 16 == 0 for o in u.offsets)  # every parameter 16-element aligned in the flat unit
+        covered += sum(u.numels)
+        assert not u.alias
+    assert covered == n_params  # tied wte / lm_head counted once
+    # this rank's shards: one flat master buffer of the summed shard sizes
+    assert fs.shards.total >= sum(u.shard_size for u in fs.units)
+    # a whole step runs through the unit hooks (no-op collectives: values are not checked)
+    opt = FusedAdamW(fs.parameters(), lr=1e-3)
+    x = torch.randint(0, 101, (2, 17))
+    lo = fs(x[:, :-1])
+    V = lo.shape[-1]  # vocabulary padded for the LM head
+    assert lo.shape[:2] == (2, 16) and V >= 101
+    F.cross_entropy(lo.reshape(-1, V), x[:, 1:].reshape(-1)).backward()
+    opt.step()
+    assert all(not u.gathered for u in fs.units if not u.is_root)  # resharded after backward
+
+
+def test_ddp_buckets_at_world_8(fake_pg):
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(0)
+    m = GPT2(GPT2Config(n_layer=4, n_head=2, n_embd=64, vocab_size=128, block_size=16))
+    ddp = DistributedDataParallel(m, comm=TorchComm(), device=torch.device("cpu"), bucket_cap_mb=0.05,
+                                  first_bucket_mb=0.01, init_sync=False)
+    assert ddp.world_size == 8
+    sizes = ddp.bucket_sizes()
+    assert len(sizes) > 2 and sum(sizes) == ddp.flat.total
+    # reverse registration order: the first bucket (launched first in backward) holds the last parameters
+    names = [n for n, p in m.named_parameters() if p.requires_grad]
+    first = ddp.buckets[0]
+    assert ddp.flat.names[min(first.param_ids)] == names[-1]
+    assert ddp.flat.names[max(ddp.buckets[-1].param_ids)] == names[0]
+    x = torch.randint(0, 128, (2, 17))
+    lo = ddp(x[:, :-1])
+    F.cross_entropy(lo.reshape(-1, lo.shape[-1]), x[:, 1:].reshape(-1)).backward()
+    assert all(ddp.flat.grad_is_view(i) for i in range(len(ddp.flat.params)))
