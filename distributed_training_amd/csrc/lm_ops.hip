@@ -405,6 +405,91 @@ __global__ void __launch_bounds__(256) cross_entropy_kernel(const bf16* logits, 
   }
 }
 
+// Opaque to the compiler: the row stays packed bf16 (4 VGPRs per chunk) between
+// passes instead of being kept converted to fp32 (8 per chunk), which would cut
+// occupancy to one wave per SIMD; re-widening is one shift per value.
+template <int CH>
+__device__ __forceinline__ void keep_packed(bf16x8 (&r)[CH]) {
+  typedef int i4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    i4 w = __builtin_bit_cast(i4, r[k]);
+    asm volatile("" : "+v"(w));
+    r[k] = __builtin_bit_cast(bf16x8, w);
+  }
+}
+
+// Same op with the row held in registers between the two passes, so it is
+// read from HBM once (the two-pass kernel above re-reads its 100 KB GPT-2 row,
+// mostly from the Infinity Cache): NT threads x CH chunks of 8 bf16 cover up
+// to NT * 8 * CH logits; V % 8 == 0.  (GPT-2 vocabulary; a Llama-3 row would
+// need 1024 threads x 16 chunks, over the 128 VGPRs such a block allows.)
+template <int NT, int CH>
+__global__ void __launch_bounds__(NT) cross_entropy_rows_kernel(const bf16* logits, bf16* dlogits,
+                                                                const int64_t* __restrict__ target,
+                                                                float* __restrict__ loss, int64_t V,
+                                                                float grad_scale, int64_t ignore_index) {
+  constexpr int NW = NT / 64;
+  const int64_t row = blockIdx.x;
+  const bf16* x = logits + row * V;
+  bf16* dx = dlogits + row * V;
+  const int64_t t = target[row];
+  __shared__ float sm[NW], ss[NW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  bf16x8 r[CH];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {  // every load in flight before any use
+    const int64_t c = ((int64_t)k * NT + threadIdx.x) * 8;
+    if (c < V) r[k] = *reinterpret_cast<const bf16x8*>(x + c);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = ((int64_t)k * NT + threadIdx.x) * 8;
+    if (c < V)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, bf2f(r[k][j]));
+  }
+  m = wave_max(m);
+  keep_packed<CH>(r);
+  if (lane == 0) sm[wave] = m;
+  __syncthreads();
+  float M = sm[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) M = fmaxf(M, sm[w]);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = ((int64_t)k * NT + threadIdx.x) * 8;
+    if (c < V)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf(bf2f(r[k][j]) - M);
+  }
+  s = wave_sum(s);
+  keep_packed<CH>(r);
+  if (lane == 0) ss[wave] = s;
+  __syncthreads();
+  float Ssum = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) Ssum += ss[w];
+  const float lse = M + __logf(Ssum);
+  const bool ignore = t == ignore_index || t < 0 || t >= V;
+  const float xt = ignore ? 0.f : bf2f(x[ignore ? 0 : t]);
+  if (threadIdx.x == 0) loss[row] = ignore ? 0.f : lse - xt;
+  __syncthreads();  // x[t] read by thread 0 before it may be overwritten (in place)
+  const float gs = ignore ? 0.f : grad_scale;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int64_t c = ((int64_t)k * NT + threadIdx.x) * 8;
+    if (c < V) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__expf(bf2f(r[k][j]) - lse) - (c + j == t ? 1.f : 0.f)) * gs;
+      store8(dx + c, v);
+    }
+  }
+}
+
 static inline int egrid(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
@@ -546,7 +631,14 @@ hipError_t dta_rope(void* x, const float* cs, const float* sn, int B, int S, int
 }
 hipError_t dta_cross_entropy(const void* logits, void* dlogits, const int64_t* target, float* loss, int64_t N,
                              int64_t V, float grad_scale, int64_t ignore_index, hipStream_t st) {
-  hipLaunchKernelGGL(cross_entropy_kernel, dim3((unsigned)N), dim3(256), 0, st, (const bf16*)logits, (bf16*)dlogits,
-                     target, loss, V, grad_scale, ignore_index);
+  const bf16* L = (const bf16*)logits;
+  bf16* DL = (bf16*)dlogits;
+  if (V % 8 == 0 && V <= 512 * 8 * 13) {  // GPT-2 (50304): 13 chunks of 8 per thread
+    hipLaunchKernelGGL((cross_entropy_rows_kernel<512, 13>), dim3((unsigned)N), dim3(512), 0, st, L, DL, target, loss,
+                       V, grad_scale, ignore_index);
+  } else {  // larger vocabularies (Llama-3: 128256) stream the row twice
+    hipLaunchKernelGGL(cross_entropy_kernel, dim3((unsigned)N), dim3(256), 0, st, L, DL, target, loss, V, grad_scale,
+                       ignore_index);
+  }
   return hipGetLastError();
 }
