@@ -80,6 +80,14 @@ __device__ __forceinline__ int img_off(int row, int col, int IMG) {
   return row * IMG + (((col >> 2) ^ ((row >> 1) & 7)) << 2) + (col & 3);
 }
 
+// bf16 W1 image [H][32] (the forward's A operand, 64-B rows): the 16-byte
+// chunk of element (h, k) is XOR-swizzled by (h >> 2) & 3, so the 16 rows one
+// ds_read_b128 lane group reads land on 16 distinct bank slots (unswizzled,
+// four rows share each slot: 4-way).
+__device__ __forceinline__ int wb_off(int h, int k) {
+  return h * 32 + ((((k >> 3) ^ ((h >> 2) & 3))) << 3) + (k & 7);
+}
+
 __device__ __forceinline__ bf16x8 img_trfrag(const bf16* X, int IMG, int s, int c0, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = 16 * s + 8 * (g >> 1) + (i >> 2);
@@ -275,7 +283,7 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
         }
         p -= hs.lr * g;
         Pf[o] = p;
-        if (j < a.hidden * a.in_dim) Wb[(j / a.in_dim) * 32 + j % a.in_dim] = f2bf(p);
+        if (j < a.hidden * a.in_dim) Wb[wb_off(j / a.in_dim, j % a.in_dim)] = f2bf(p);
       }
     }
   }
@@ -413,7 +421,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   }
   for (int i = tid; i < H * 32; i += kMpThreads) {
     const int h = i >> 5, k = i & 31;
-    Wb[i] = f2bf(k < IN ? a.P[a.o_w1 + h * IN + k] : 0.f);
+    Wb[wb_off(h, k)] = f2bf(k < IN ? a.P[a.o_w1 + h * IN + k] : 0.f);
   }
   int c0 = *a.cursor;
   int lcur = *a.loss_cursor;
@@ -500,9 +508,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           w2v[4 * g] = wv.x; w2v[4 * g + 1] = wv.y; w2v[4 * g + 2] = wv.z; w2v[4 * g + 3] = wv.w;
         }
         // A operand W1: lane (row h = h0 + r32), k = 16ks + 8hh + j: one 16-B read of the bf16 image
-        const bf16* wr = Wb + (h0 + r32) * 32 + hh * 8;
-        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(wr), xb0, acc);
-        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(wr + 16), xb1, acc);
+        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(Wb + wb_off(h0 + r32, hh * 8)), xb0, acc);
+        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(Wb + wb_off(h0 + r32, 16 + hh * 8)), xb1, acc);
         hpre[tt] = acc;
         // layer 2 partial: y[sample] += W2[h] * act(hpre[h][sample]) over this lane's 16 rows
 #pragma unroll
@@ -700,7 +707,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
               const int off = pbase + h * pstride;
               Pf[off] = pv[u];
               if (!PLAIN && hs.mom != 0.f) Mf[off] = mv[u];
-              if (c < IN) Wb[h * 32 + c] = f2bf(pv[u]);
+              if (c < IN) Wb[wb_off(h, c)] = f2bf(pv[u]);
             }
           }
         }
@@ -772,7 +779,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
                 const int off = pbase + hrow * pstride;
                 Pf[off] = pv[u];
                 if (!PLAIN && hs2.mom != 0.f) Mf[off] = mv[u];
-                if (c < IN) Wb[hrow * 32 + c] = f2bf(pv[u]);
+                if (c < IN) Wb[wb_off(hrow, c)] = f2bf(pv[u]);
               }
             }
           }

@@ -58,6 +58,10 @@ def make_layout(in_dim: int, hidden: int, out_dim: int) -> MlpLayout:
     o_w1 = 0
     o_b1 = _align(o_w1 + hidden * in_dim)
     o_w2 = _align(o_b1 + hidden)
+    # LDS banks: in the persistent loop's SGD one instruction updates b1[h] (one
+    # lane) and W2[h] (another): keep the two 4 banks apart, not on one bank
+    if (o_w2 - o_b1) % 32 == 0:
+        o_w2 += 4
     o_b2 = _align(o_w2 + out_dim * hidden)
     total = _align(o_b2 + out_dim)
     return MlpLayout(in_dim, hidden, out_dim, o_w1, o_b1, o_w2, o_b2, total)

@@ -7,7 +7,9 @@ from distributed_training_amd.ops import mlp_fused as mf
 
 def test_layout_alignment_and_views():
     lay = mf.make_layout(20, 512, 1)
-    assert lay.o_w1 == 0 and all(o % 16 == 0 for o in lay.offsets) and lay.total % 16 == 0
+    # 16-byte aligned regions (float4 access); b1 and W2 four LDS banks apart
+    assert lay.o_w1 == 0 and all(o % 4 == 0 for o in lay.offsets) and lay.total % 16 == 0
+    assert (lay.o_w2 - lay.o_b1) % 32 == 4
     flat = torch.arange(lay.total, dtype=torch.float32)
     v = lay.views(flat)
     assert v["fc1.weight"].shape == (512, 20) and v["fc2.weight"].shape == (1, 512)
