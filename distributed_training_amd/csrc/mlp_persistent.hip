@@ -46,14 +46,22 @@ __device__ __forceinline__ bf16x4 mp_tr4(const bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-// Natural-k-order transposed fragment of a row-major LDS image X (row stride
-// ST elements): lane l gets X[16s + 8(l>>5) + j][c0 + (l & 31)], j = 0..7.
-__device__ __forceinline__ bf16x8 mp_trfrag(const bf16* X, int ST, int s, int c0, int lane) {
+// Batch tile [32 samples][kMpXs] bf16 (64-B rows): element (row, col), its
+// 16-byte chunk XOR-swizzled by (row >> 2) & 3 -- the forward's row reads
+// (ds_read_b128) become conflict-free (4-way unswizzled) and the backward's
+// transposed reads stay conflict-free.
+__device__ __forceinline__ int xs_off(int row, int col) {
+  return row * kMpXs + ((((col >> 3) ^ ((row >> 2) & 3))) << 3) + (col & 7);
+}
+
+// Natural-k-order transposed fragment of the batch tile X: lane l gets
+// X[16s + 8(l>>5) + j][c0 + (l & 31)], j = 0..7.
+__device__ __forceinline__ bf16x8 mp_trfrag(const bf16* X, int s, int c0, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int row = 16 * s + 8 * (g >> 1) + (i >> 2);
   const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
-  const bf16x4 lo = mp_tr4(X + row * ST + col);
-  const bf16x4 hi = mp_tr4(X + (row + 4) * ST + col);
+  const bf16x4 lo = mp_tr4(X + xs_off(row, col));
+  const bf16x4 hi = mp_tr4(X + xs_off(row + 4, col));
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -451,13 +459,13 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   };
   auto store_rows = [&](int buf) {
     // row gr of the batch tile: X | 1 | 0 (the dY columns are written by the loss phase)
-    bf16x8* row = reinterpret_cast<bf16x8*>(Xs + (buf * 32 + gr) * kMpXs);
+    bf16* tile = Xs + buf * 32 * kMpXs;
     const bool live = gr < B;
     bf16x8 z;
 #pragma unroll
     for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) row[c] = live ? xv[c] : z;
+    for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(tile + xs_off(gr, 8 * c)) = live ? xv[c] : z;
 #pragma unroll
     for (int o = 0; o < OUT; ++o) Ts[(buf * 32 + gr) * OUT + o] = live ? tv[o] : 0.f;
   };
@@ -489,8 +497,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
 #pragma unroll
     for (int o = 0; o < OUT; ++o) yp[o] = 0.f;
     // B operand X^T: lane (col = sample r32), k = 16ks + 8hh + j  (row read of the batch tile)
-    const bf16x8 xb0 = *reinterpret_cast<const bf16x8*>(Xb + r32 * kMpXs + hh * 8);
-    const bf16x8 xb1 = *reinterpret_cast<const bf16x8*>(Xb + r32 * kMpXs + 16 + hh * 8);
+    const bf16x8 xb0 = *reinterpret_cast<const bf16x8*>(Xb + xs_off(r32, hh * 8));
+    const bf16x8 xb1 = *reinterpret_cast<const bf16x8*>(Xb + xs_off(r32, 16 + hh * 8));
     f32x16 hpre[TPW];
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
@@ -570,11 +578,10 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
 #pragma unroll
       for (int o = 0; o < OUT; ++o) dy[o] *= a.grad_scale;
       if (hh == 0) {
-        bf16* row = const_cast<bf16*>(Xb) + r * kMpXs;
 #pragma unroll
         for (int o = 0; o < OUT; ++o) {
           dYf[o * 32 + r] = dy[o];
-          row[IN + 1 + o] = f2bf(dy[o]);
+          const_cast<bf16*>(Xb)[xs_off(r, IN + 1 + o)] = f2bf(dy[o]);
         }
       }
       if constexpr (multi) {
@@ -617,7 +624,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     const int pbase = c < IN ? a.o_w1 + c : (c == IN ? a.o_b1 : a.o_w2);
     const int pstride = c < IN ? IN : 1;
     // B operand [X | 1 | dY] of both gradient GEMMs (same for every tile)
-    const bf16x8 xf0 = mp_trfrag(Xb, kMpXs, 0, 0, lane), xf1 = mp_trfrag(Xb, kMpXs, 1, 0, lane);
+    const bf16x8 xf0 = mp_trfrag(Xb, 0, 0, lane), xf1 = mp_trfrag(Xb, 1, 0, lane);
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
       const int t = wave + kMpWaves * tt;
