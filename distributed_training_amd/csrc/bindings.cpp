@@ -422,8 +422,11 @@ std::vector<torch::Tensor> norm_fwd(torch::Tensor x, torch::Tensor w, c10::optio
 
 // returns (dx, dw, db); dw/db dtype follow the weight
 // dres: gradient arriving on the residual stream, added into dx in the same pass
+// dw_out / db_out (optional): write the weight / bias gradients there (e.g. the
+// parameters' slices of a flat gradient buffer) instead of fresh tensors
 std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
-                                    torch::Tensor rstd, bool rms, int64_t stream, c10::optional<torch::Tensor> dres) {
+                                    torch::Tensor rstd, bool rms, int64_t stream, c10::optional<torch::Tensor> dres,
+                                    c10::optional<torch::Tensor> dw_out, c10::optional<torch::Tensor> db_out) {
   check_bf16_2d(dy, "dy");
   check_bf16_2d(x, "x");
   check_bf16_2d(w, "weight");
@@ -442,8 +445,14 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   auto dwp = torch::empty({nblk, C}, f32);
   auto dbp = rms ? torch::empty({0}, f32) : torch::empty({nblk, C}, f32);
   auto dx = torch::empty_like(x);
-  auto dw = torch::empty({C}, w.options());
-  auto db = rms ? torch::empty({0}, w.options()) : torch::empty({C}, w.options());
+  auto out_ok = [&](const c10::optional<torch::Tensor>& o) {
+    if (!o || !o->defined()) return false;
+    TORCH_CHECK(o->is_cuda() && o->scalar_type() == w.scalar_type() && o->numel() == C && o->is_contiguous(),
+                "norm_bwd: gradient outputs must be contiguous [C] tensors of the weight dtype");
+    return true;
+  };
+  auto dw = out_ok(dw_out) ? *dw_out : torch::empty({C}, w.options());
+  auto db = rms ? torch::empty({0}, w.options()) : (out_ok(db_out) ? *db_out : torch::empty({C}, w.options()));
   hip_ok(dta_norm_bwd(rms, dy.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), dx.data_ptr(), dwp.data_ptr<float>(),
                       rms ? nullptr : dbp.data_ptr<float>(), dw.data_ptr(), rms ? nullptr : db.data_ptr(), N, (int)C,
@@ -888,7 +897,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("rms"), py::arg("eps"),
         py::arg("stream") = -1, py::arg("res") = py::none());
   m.def("norm_bwd", &norm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
-        py::arg("rms"), py::arg("stream") = -1, py::arg("dres") = py::none());
+        py::arg("rms"), py::arg("stream") = -1, py::arg("dres") = py::none(), py::arg("dw_out") = py::none(),
+        py::arg("db_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -137,13 +137,16 @@ class _Norm(Function):
         y, mean, rstd, _ = native().norm_fwd(x2, w.contiguous(), None if rms else b.contiguous(), rms, eps, -1)
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.rms, ctx.shape = rms, shape
+        ctx.params = (w, b)  # their .grad decides a direct write into the flat gradient (_grad_dest)
         return y.view(shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
+        pw, pb = ctx.params
         dx, dw, db = native().norm_bwd(dy.reshape(x2.shape).contiguous(), x2, w.contiguous(), mean, rstd, ctx.rms,
-                                       -1)
+                                       -1, None, _grad_dest(pw) if ctx.needs_input_grad[1] else None,
+                                       _grad_dest(pb) if not ctx.rms and ctx.needs_input_grad[2] else None)
         return dx.view(ctx.shape), dw, (None if ctx.rms else db), None, None
 
 
@@ -159,6 +162,7 @@ class _AddNorm(Function):
                                                 res.reshape(x2.shape).contiguous())
         ctx.save_for_backward(xsum, w, mean, rstd)
         ctx.rms, ctx.shape = rms, shape
+        ctx.params = (w, b)
         return xsum.view(shape), y.view(shape)
 
     @staticmethod
@@ -166,9 +170,11 @@ class _AddNorm(Function):
         xsum, w, mean, rstd = ctx.saved_tensors
         if g_y is None:
             return g_x, g_x, None, None, None, None
+        pw, pb = ctx.params
         dres = None if g_x is None else g_x.reshape(xsum.shape).contiguous()
         dx, dw, db = native().norm_bwd(g_y.reshape(xsum.shape).contiguous(), xsum, w.contiguous(), mean, rstd,
-                                       ctx.rms, -1, dres)
+                                       ctx.rms, -1, dres, _grad_dest(pw) if ctx.needs_input_grad[2] else None,
+                                       _grad_dest(pb) if not ctx.rms and ctx.needs_input_grad[3] else None)
         dx = dx.view(ctx.shape)
         return dx, dx, dw, (None if ctx.rms else db), None, None
 

@@ -143,9 +143,9 @@ def test_gpt2_tiny_trains_on_gpu():
 
 
 def test_ddp_linear_gradients_written_into_flat_buffer():
-    """Native Linear backward writes dW / db straight into the DDP engine's flat
-    gradient slices (no bucket copy), a Linear used twice in one backward still
-    gets the sum of both uses, and gradients match an un-wrapped copy."""
+    """Native Linear and LayerNorm backwards write dW / db straight into the DDP
+    engine's flat gradient slices (no bucket copy), a Linear used twice in one
+    backward still gets the sum of both uses, and gradients match an un-wrapped copy."""
     import copy
 
     from distributed_training_amd.parallel.comm import RcclComm
@@ -157,8 +157,10 @@ def test_ddp_linear_gradients_written_into_flat_buffer():
             self.a = lm.Linear(128, 256)
             self.b = lm.Linear(256, 128)
             self.shared = lm.Linear(128, 128)
+            self.ln = torch.nn.LayerNorm(128)
 
         def forward(self, x):
+            x = lm.layer_norm(x, self.ln.weight, self.ln.bias)
             h = self.shared(self.b(lm.gelu(self.a(x))))
             return self.shared(h)  # second use of the same weight in this backward
 
@@ -180,7 +182,7 @@ def test_ddp_linear_gradients_written_into_flat_buffer():
         ddp.zero_grad(set_to_none=True)
         copied.clear()
         ddp(x).float().square().mean().backward()
-        assert "a.weight" not in copied and "b.weight" not in copied and "a.bias" not in copied, copied
+        assert not {"a.weight", "b.weight", "a.bias", "ln.weight", "ln.bias"} & set(copied), copied
         for name, p in ref.named_parameters():
             p.grad = None
         ref(x).float().square().mean().backward()
