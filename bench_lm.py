@@ -181,6 +181,14 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    if os.environ.get("DTA_PROFILE_OPS") and rank == 0:  # diagnostics: one more (untimed) step under torch.profiler
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            step()
+            torch.cuda.synchronize(dev)
+        print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40),
+              file=sys.stderr)
     tokens = args.batch * args.seq * ws * args.steps
     flops_tok = 6 * (n_params - (cfg.block_size * cfg.n_embd if is_gpt else 0)) + 12 * cfg.n_layer * cfg.n_embd * args.seq
     tps = tokens / el
