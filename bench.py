@@ -227,9 +227,9 @@ def main():
 
     def barrier():
         torch.cuda.synchronize(dev)
-        if ws > 1:
+        if ws > 1:  # (one rank: the synchronize is the whole bracket; a second one is host time in the timed region)
             dist.barrier(device_ids=[dev.index])
-        torch.cuda.synchronize(dev)
+            torch.cuda.synchronize(dev)
 
     step_fn(args.warmup)
     barrier()

@@ -765,12 +765,12 @@ class PyP2PAllReduce {
 };
 
 // Persistent single-workgroup MLP train loop: `nsteps` full steps in one launch
-void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
+static dta::MlpPArgs make_mlp_pargs(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
                     torch::Tensor loss_ring, torch::Tensor loss_cursor, torch::Tensor mom_started, torch::Tensor P,
                     c10::optional<torch::Tensor> M, std::vector<int64_t> offsets, int64_t total, int64_t in_dim,
-                    int64_t hidden, int64_t out_dim, int64_t B, int64_t nsteps, int64_t act, int64_t loss_type,
+                    int64_t hidden, int64_t out_dim, int64_t B, int64_t nsteps, int64_t loss_type,
                     double grad_scale, double lr, double momentum, double dampening, double wd, bool nesterov,
-                    bool maximize, int64_t stream, c10::optional<torch::Tensor> dbg, int64_t dbg_step,
+                    bool maximize, c10::optional<torch::Tensor> dbg, int64_t dbg_step,
                     std::vector<int64_t> xinfo) {
   check_gpu(Xp, "Xp");
   TORCH_CHECK(Xp.scalar_type() == torch::kBFloat16 && Xp.dim() == 2 && Xp.size(1) == 32 &&
@@ -785,11 +785,13 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
   check_f32(loss_ring, "loss_ring", false);
   check_f32(P, "P", false);
   TORCH_CHECK(offsets.size() == 4 && P.numel() >= total, "mlp_persistent: layout");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(P.data_ptr()) % 16 == 0, "mlp_persistent: P must be 16-byte aligned");
   TORCH_CHECK(T.numel() == Xp.size(0) * out_dim, "mlp_persistent: X/T shapes");
   const bool has_m = M && M->defined();
   if (has_m) {
     check_f32(*M, "M", false);
     TORCH_CHECK(M->numel() >= total, "momentum size");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(M->data_ptr()) % 16 == 0, "mlp_persistent: M must be 16-byte aligned");
   }
   TORCH_CHECK(momentum == 0.0 || has_m, "momentum needs a buffer");
   dta::MlpPArgs a{};
@@ -823,6 +825,10 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
   a.weight_decay = (float)wd;
   a.nesterov = nesterov;
   a.maximize = maximize;
+  {
+    const char* e = std::getenv("DTA_MLP_SETPRIO");
+    a.prio_young = e ? std::atoi(e) : 0;
+  }
   // xinfo (DDP exchange, empty for one rank): world, rank, slot_elems, local_ll, xerr, xepoch,
   // timeout_iters, xmode, LL elements per rank buffer, peer_ll[0..world)
   a.world = 1;
@@ -861,11 +867,56 @@ void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, t
     }
   }
   if (dbg && dbg->defined()) {
-    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= 64, "dbg: int64 [64]");
+    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= (dbg_step < 0 ? 72 : 64),
+                "dbg: int64 [64] (step stamps) or [72] (dbg_step < 0: launch timeline stamps at 64..68)");
     a.dbg = reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>());
     a.dbg_step = (int)dbg_step;
   }
+  return a;
+}
+
+void mlp_persistent(torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor,
+                    torch::Tensor loss_ring, torch::Tensor loss_cursor, torch::Tensor mom_started, torch::Tensor P,
+                    c10::optional<torch::Tensor> M, std::vector<int64_t> offsets, int64_t total, int64_t in_dim,
+                    int64_t hidden, int64_t out_dim, int64_t B, int64_t nsteps, int64_t act, int64_t loss_type,
+                    double grad_scale, double lr, double momentum, double dampening, double wd, bool nesterov,
+                    bool maximize, int64_t stream, c10::optional<torch::Tensor> dbg, int64_t dbg_step,
+                    std::vector<int64_t> xinfo) {
+  dta::MlpPArgs a = make_mlp_pargs(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, offsets,
+                                   total, in_dim, hidden, out_dim, B, nsteps, loss_type, grad_scale, lr, momentum,
+                                   dampening, wd, nesterov, maximize, dbg, dbg_step, xinfo);
   hip_ok(dta_mlp_persistent(&a, (int)act, pick_stream(stream)), "mlp_persistent");
+}
+
+// The same launch with every argument checked and packed once: the timed region of
+// a short run (e.g. 20 steps) then pays one kernel launch of host work, not ~30
+// argument conversions and checks (the persistent program re-creates it only when
+// its buffers, exchange form or hyper-parameters change).
+struct MlpPersistentLaunch {
+  dta::MlpPArgs a;
+  int act;
+  std::vector<torch::Tensor> keep;  // the buffers the packed pointers refer to
+  void launch(int64_t nsteps, int64_t stream) {
+    TORCH_CHECK(nsteps >= 1 && nsteps <= (1 << 30), "mlp_persistent: nsteps");
+    a.nsteps = (int)nsteps;
+    hip_ok(dta_mlp_persistent(&a, act, pick_stream(stream)), "mlp_persistent");
+  }
+};
+
+std::shared_ptr<MlpPersistentLaunch> mlp_persistent_prepare(
+    torch::Tensor Xp, torch::Tensor T, torch::Tensor idx_ring, torch::Tensor cursor, torch::Tensor loss_ring,
+    torch::Tensor loss_cursor, torch::Tensor mom_started, torch::Tensor P, c10::optional<torch::Tensor> M,
+    std::vector<int64_t> offsets, int64_t total, int64_t in_dim, int64_t hidden, int64_t out_dim, int64_t B,
+    int64_t act, int64_t loss_type, double grad_scale, double lr, double momentum, double dampening, double wd,
+    bool nesterov, bool maximize, std::vector<int64_t> xinfo) {
+  auto L = std::make_shared<MlpPersistentLaunch>();
+  L->a = make_mlp_pargs(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, offsets, total, in_dim,
+                        hidden, out_dim, B, 1, loss_type, grad_scale, lr, momentum, dampening, wd, nesterov, maximize,
+                        c10::nullopt, 0, xinfo);
+  L->act = (int)act;
+  L->keep = {Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P};
+  if (M && M->defined()) L->keep.push_back(*M);
+  return L;
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -893,6 +944,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("maximize"), py::arg("stream") = -1, py::arg("dbg") = py::none(), py::arg("dbg_step") = 0,
         py::arg("xinfo") = std::vector<int64_t>{});
   m.def("mlp_persistent_lds_bytes", &dta_mlp_persistent_lds_bytes);
+  py::class_<MlpPersistentLaunch, std::shared_ptr<MlpPersistentLaunch>>(m, "MlpPersistentLaunch")
+      .def("launch", &MlpPersistentLaunch::launch, py::arg("nsteps"), py::arg("stream") = -1);
+  m.def("mlp_persistent_prepare", &mlp_persistent_prepare, py::arg("Xp"), py::arg("T"), py::arg("idx_ring"),
+        py::arg("cursor"), py::arg("loss_ring"), py::arg("loss_cursor"), py::arg("mom_started"), py::arg("P"),
+        py::arg("M"), py::arg("offsets"), py::arg("total"), py::arg("in_dim"), py::arg("hidden"), py::arg("out_dim"),
+        py::arg("B"), py::arg("act"), py::arg("loss_type"), py::arg("grad_scale"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("maximize"),
+        py::arg("xinfo") = std::vector<int64_t>{});
   m.def("attn_fwd", &attn_fwd);
   m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("rms"), py::arg("eps"),
         py::arg("stream") = -1, py::arg("res") = py::none());

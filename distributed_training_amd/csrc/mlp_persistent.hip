@@ -75,6 +75,12 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// launch-timeline stamps (diagnostic build of one launch: dbg_step < 0), s_memrealtime (100 MHz)
+#define MP_TSTAMP(k)                                                                        \
+  do {                                                                                      \
+    if (a.dbg && a.dbg_step < 0 && tid == 0) a.dbg[64 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 #define MP_STAMP(k)                                                                             \
   do {                                                                                          \
     if (a.dbg && s == a.dbg_step && lane == 0) a.dbg[wave * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
@@ -422,15 +428,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   q += 16;
   bf16* Wb = reinterpret_cast<bf16*>(q);                            // [H][32] bf16 W1 (k >= in zero)
 
-  // ---- load parameters (+ momentum), build the bf16 W1 fragment image ----
-  for (int i = tid; i < a.total; i += kMpThreads) {
-    Pf[i] = a.P[i];
-    if (a.M) Mf[i] = a.M[i];
-  }
-  for (int i = tid; i < H * 32; i += kMpThreads) {
-    const int h = i >> 5, k = i & 31;
-    Wb[wb_off(h, k)] = f2bf(k < IN ? a.P[a.o_w1 + h * IN + k] : 0.f);
-  }
   int c0 = *a.cursor;
   int lcur = *a.loss_cursor;
   int first = a.M ? (*a.mom_started == 0) : 0;
@@ -469,17 +466,67 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
 #pragma unroll
     for (int o = 0; o < OUT; ++o) Ts[(buf * 32 + gr) * OUT + o] = live ? tv[o] : 0.f;
   };
+  // the first batch's dependent loads (index -> feature row) are issued before the
+  // parameter loads, so their two round trips overlap the parameter fetch
   if (gthr) {
     load_rows(load_idx(0));
-    store_rows(0);
     idx_next = load_idx(1);
   }
+  MP_TSTAMP(0);
+  // ---- load parameters (+ momentum), build the bf16 W1 fragment image ----
+  // All of a thread's 16-B loads are issued before any LDS store (indices clamped,
+  // stores masked: no select around a load), so the ~45 KB arrive in one HBM round
+  // trip instead of one dependent miss per loop iteration (that was ~20 us of fixed
+  // cost per launch, a fifth of a 20-step launch).
+  {
+    const int nv = a.total >> 2;  // whole float4s; P / M are 16-B aligned allocations
+    const float4* P4 = reinterpret_cast<const float4*>(a.P);
+    const float4* M4 = reinterpret_cast<const float4*>(a.M);
+    constexpr int kLd = 8;
+    for (int base = 0; base < nv; base += kMpThreads * kLd) {
+      float4 pv[kLd], mv[kLd];
+#pragma unroll
+      for (int j = 0; j < kLd; ++j) pv[j] = P4[min(base + j * kMpThreads + tid, nv - 1)];
+      if (a.M) {
+#pragma unroll
+        for (int j = 0; j < kLd; ++j) mv[j] = M4[min(base + j * kMpThreads + tid, nv - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < kLd; ++j) {
+        const int i = base + j * kMpThreads + tid;
+        if (i < nv) {
+          Pf[4 * i] = pv[j].x; Pf[4 * i + 1] = pv[j].y; Pf[4 * i + 2] = pv[j].z; Pf[4 * i + 3] = pv[j].w;
+          if (a.M) {
+            Mf[4 * i] = mv[j].x; Mf[4 * i + 1] = mv[j].y; Mf[4 * i + 2] = mv[j].z; Mf[4 * i + 3] = mv[j].w;
+          }
+        }
+      }
+    }
+    for (int i = 4 * nv + tid; i < a.total; i += kMpThreads) {
+      Pf[i] = a.P[i];
+      if (a.M) Mf[i] = a.M[i];
+    }
+  }
+  __syncthreads();
+  MP_TSTAMP(1);
+  for (int i = tid; i < H * 4; i += kMpThreads) {  // from the LDS copy: no second HBM pass
+    const int h = i >> 2, k0 = (i & 3) * 8;        // one 16-B chunk (8 k) of row h per iteration
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f2bf(k0 + j < IN ? Pf[a.o_w1 + h * IN + k0 + j] : 0.f);
+    *reinterpret_cast<bf16x8*>(Wb + wb_off(h, k0)) = v;
+  }
+  if (gthr) store_rows(0);
   if (tid == 0) *lossbuf = 0.f;
   __syncthreads();
+  MP_TSTAMP(2);
 
   const SgdH hbase{a.lr, a.momentum, a.dampening, a.weight_decay, a.nesterov, a.maximize, 0};
   const float lscale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
 
+  // static priority for the younger half of the workgroup (MI355X_MICROARCH "Two waves per
+  // SIMD" item 4): one s_setprio before the loop, wave-uniform guard, no per-phase flips
+  if (a.prio_young && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   float dy_keep[OUT], loss_keep = 0.f;  // one rank: wave 0's dY / loss, finished after its backward
 #pragma unroll
   for (int o = 0; o < OUT; ++o) dy_keep[o] = 0.f;
@@ -828,6 +875,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     // tile, both published before barrier 2 of this step
   }
   __syncthreads();
+  MP_TSTAMP(3);
   for (int i = tid; i < a.total; i += kMpThreads) {
     a.P[i] = Pf[i];
     if (a.M) a.M[i] = Mf[i];
@@ -838,6 +886,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     *a.loss_cursor = lcur;
     if (a.M && a.nsteps > 0) *a.mom_started = 1;
   }
+  MP_TSTAMP(4);
 }
 
 }  // namespace dta
@@ -852,7 +901,11 @@ size_t dta_mlp_persistent_lds_bytes(int total, int hidden, int out_dim, int has_
 template <int ACT, int OUT, int TPW, bool PLAIN, int XM>
 static hipError_t mp_launch(const MlpPArgs& a, size_t lds, hipStream_t st) {
   auto k = &mlp_persistent_kernel<ACT, OUT, TPW, PLAIN, XM>;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static int lds_set = -1;  // per instantiation: the attribute call is host work on every launch otherwise
+  if ((int)lds > lds_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    lds_set = (int)lds;
+  }
   const int grid = XM == 3 ? 1 + a.nh : 1;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kMpThreads), lds, st, a);
   return hipGetLastError();

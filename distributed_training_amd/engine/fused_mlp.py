@@ -138,7 +138,7 @@ class FusedMLPProgram:
         # persistent: room for two launches plus an epoch, so the next launch's
         # indices upload on a side stream while the current launch runs (slots
         # of the two launches never overlap; _run_persistent)
-        ahead = 2 * self.chunk_steps if self.persistent else 2 * self.graph_steps
+        ahead = 3 * self.chunk_steps if self.persistent else 2 * self.graph_steps
         k = max(2, -(-ahead // S) + 1)
         self.R = S * k
         self.ring = torch.zeros(self.R, self.B, dtype=torch.int32, device=dev)
@@ -150,9 +150,10 @@ class FusedMLPProgram:
         # launch before the current one (whose ring slots they may reuse) and
         # before the launch that reads them
         self._up_stream = torch.cuda.Stream(dev) if self.persistent and dev.type == "cuda" else None
-        self._launch_done: List = []  # completion events of the last two persistent launches
+        self._up_fence_at = -1  # value of `launched` when the upload stream last waited on the compute stream
         self._up_done = None
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self._plaunch = None  # (key, packed persistent launch): re-packed when the form or hyper-parameters change
         self.loss_cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.mom_started_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # persistent mode
         self.Xp = mf.pad_features(self.X) if self.persistent else None
@@ -165,7 +166,7 @@ class FusedMLPProgram:
         itself is only written by :meth:`store_to_module`)."""
         if self._up_stream is not None:  # uploads in flight land before the ring is cleared ...
             torch.cuda.current_stream(self.device).wait_stream(self._up_stream)
-            self._launch_done, self._up_done = [], None
+            self._up_fence_at, self._up_done = -1, None
         for t in (*self.P, *self.G, *(m for m in self.M if m is not None)):
             t.zero_()
         self.ring.zero_()
@@ -409,9 +410,17 @@ class FusedMLPProgram:
         r0 = self.host_step % R
         n1 = min(S, R - r0)
         up = self._up_stream if side else None
+        compute = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(up) if up is not None else contextlib.nullcontext():
-            if up is not None and len(self._launch_done) == 2:
-                up.wait_event(self._launch_done[0])  # the launch before the current one has run
+            if up is not None and self._up_fence_at != self.launched:
+                # the overwritten slots belong to launches before the current one (ring
+                # assertion above); waiting for every launch enqueued so far is a superset
+                # that needs one event per upload batch instead of one per launch (an event
+                # behind every launch would add a marker packet to each timed region)
+                fence = torch.cuda.Event()
+                fence.record(compute)
+                up.wait_event(fence)
+                self._up_fence_at = self.launched
             self.ring[r0:r0 + n1].copy_(host[:n1], non_blocking=True)
             if n1 < S:
                 self.ring[0:S - n1].copy_(host[n1:], non_blocking=True)
@@ -449,20 +458,28 @@ class FusedMLPProgram:
     def _run_persistent(self, n: int) -> None:
         end = self.launched + n
         hp = self.hyper()
+        if self.launched == 0 and self._up_stream is not None:
+            # first call (warm-up): upload two launches of indices before the first
+            # launch, so later short calls find them in place and the device is not
+            # left idle between the warm-up launch and the next call
+            self._ensure(min(2 * self.chunk_steps, self.R - self.steps_per_epoch))
         while self.launched < end:
             k = min(end - self.launched, self.chunk_steps)
             self._ensure(self.launched + k)
             if self._up_done is not None:
-                torch.cuda.current_stream(self.device).wait_event(self._up_done)
+                # an upload that already landed needs no cross-stream dependency (a wait
+                # packet ahead of the launch costs dispatch latency on the timed path)
+                if not self._up_done.query():
+                    torch.cuda.current_stream(self.device).wait_event(self._up_done)
                 self._up_done = None
-            mf.persistent_steps(self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor,
-                                self.mom_started_dev, self.P[0], self.M[0], self.layout, self.B, k, self.act,
-                                self.loss, 1.0 / self.ws, hp, xinfo=self._xinfo)
+            key = (id(self._xinfo), tuple(sorted(hp.items())))
+            if self._plaunch is None or self._plaunch[0] != key:
+                self._plaunch = (key, mf.persistent_prepare(
+                    self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor, self.mom_started_dev,
+                    self.P[0], self.M[0], self.layout, self.B, self.act, self.loss, 1.0 / self.ws, hp,
+                    xinfo=self._xinfo))
+            self._plaunch[1].launch(k)
             self._last_start = self.launched
-            if self._up_stream is not None:
-                done = torch.cuda.Event()
-                done.record()
-                self._launch_done = (self._launch_done + [done])[-2:]
             for j in range(k):
                 self._batch_of.pop(self.launched + j, None)
             self.launched += k
@@ -475,8 +492,13 @@ class FusedMLPProgram:
         The sampler's epoch is left as it was."""
         if self._up_stream is None or not self.persistent:
             return
+        # hysteresis: top up only below one launch of indices ahead, then fill to two,
+        # so a short run_steps call (e.g. a 20-step timed region after warm-up) finds
+        # everything uploaded and does no host sampler work behind its launch
+        if self.host_step - self.launched >= self.chunk_steps:
+            return
         S = self.steps_per_epoch
-        upto = min(self.launched + self.chunk_steps, self._last_start + self.R - S)
+        upto = min(self.launched + 2 * self.chunk_steps, self._last_start + self.R - S)
         sampler = self.loader.sampler
         ep = getattr(sampler, "epoch", None)
         self._ensure(upto)

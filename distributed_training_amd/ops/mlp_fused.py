@@ -122,6 +122,19 @@ def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_starte
         list(xinfo) if xinfo else [])
 
 
+def persistent_prepare(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout: MlpLayout,
+                       batch: int, act: str, loss: str, grad_scale: float, sgd: Dict[str, float], xinfo=None):
+    """:func:`persistent_steps` with its arguments checked and packed once: returns a
+    native object whose ``launch(nsteps, stream=-1)`` enqueues the loop (host cost of
+    one kernel launch)."""
+    return native().mlp_persistent_prepare(
+        Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout.offsets, layout.total,
+        layout.in_dim, layout.hidden, layout.out_dim, int(batch), ACTIVATIONS[act], LOSSES[loss],
+        float(grad_scale), float(sgd.get("lr", 1e-3)), float(sgd.get("momentum", 0.0)),
+        float(sgd.get("dampening", 0.0)), float(sgd.get("weight_decay", 0.0)), bool(sgd.get("nesterov", False)),
+        bool(sgd.get("maximize", False)), list(xinfo) if xinfo else [])
+
+
 XMODES = {"oneshot": 1, "rsag": 2, "helpers": 3}
 
 
