@@ -63,12 +63,18 @@ def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    from distributed_training_amd.parallel.ipc import device_index, dist_backend, shared_gpu
+
     if ws != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={ws}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU (RCCL); DTA_SHARED_GPU=1 rehearses N ranks on fewer GPUs
+    # (gloo control plane + IPC data plane; the numbers are then not a scaling result)
+    dev = torch.device("cuda", device_index(local))
+    torch.cuda.set_device(dev)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = dist_backend(True)
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    args.shared_gpu = shared_gpu() and ws > 1
     return rank, ws, dev
 
 
@@ -225,10 +231,16 @@ def main():
     runner = {"fused": run_fused, "generic": run_generic, "torch": run_torch}[args.impl]
     step_fn, finish, comm = runner(args, dev, ws)
 
+    def dbarrier():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[dev.index])
+        else:
+            dist.barrier()
+
     def barrier():
         torch.cuda.synchronize(dev)
         if ws > 1:  # (one rank: the synchronize is the whole bracket; a second one is host time in the timed region)
-            dist.barrier(device_ids=[dev.index])
+            dbarrier()
             torch.cuda.synchronize(dev)
 
     step_fn(args.warmup)
@@ -239,7 +251,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if ws > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     last_loss = finish()
@@ -274,6 +286,8 @@ def main():
                    "impl": args.impl},
         "final_loss": last_loss,
     }
+    if getattr(args, "shared_gpu", False):
+        out["shared_gpu"] = f"{ws} ranks on {torch.cuda.device_count()} GPU(s): correctness rehearsal, not a scaling number"
     out.update(getattr(finish, "info", {}))
     if rank == 0:
         line = json.dumps(out)
@@ -281,7 +295,7 @@ def main():
         if args.json_out:
             Path(args.json_out).write_text(line + "\n")
     if ws > 1:
-        dist.barrier(device_ids=[dev.index])
+        dbarrier()
         dist.destroy_process_group()
 
 

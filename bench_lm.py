@@ -73,13 +73,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from distributed_training_amd.parallel.ipc import device_index, dist_backend
+
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", device_index(local))  # DTA_SHARED_GPU=1: several ranks per GPU (rehearsal)
+    local = dev.index
+    torch.cuda.set_device(dev)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = dist_backend(True)
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
     torch.manual_seed(0)
     cfg = model_cfg(args.model, args.layers)
     is_gpt = args.model == "gpt2"
@@ -163,10 +167,16 @@ def main():
         opt.step()
         state["loss"] = loss
 
+    def dbarrier():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[local])
+        else:
+            dist.barrier()
+
     def barrier():
         torch.cuda.synchronize(dev)
         if ws > 1:
-            dist.barrier(device_ids=[local])
+            dbarrier()
         torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
@@ -177,18 +187,22 @@ def main():
         step()
     barrier()
     el = time.perf_counter() - t0
+    peak_mem = torch.cuda.max_memory_allocated(dev)
     if ws > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    if os.environ.get("DTA_PROFILE_OPS") and rank == 0:  # diagnostics: one more (untimed) step under torch.profiler
+    if os.environ.get("DTA_PROFILE_OPS"):
+        # diagnostics: one more (untimed) step under torch.profiler on EVERY rank (the
+        # step's collectives must match across ranks); rank 0 prints the table
         from torch.profiler import ProfilerActivity, profile
 
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             step()
             torch.cuda.synchronize(dev)
-        print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40),
-              file=sys.stderr)
+        if rank == 0:
+            print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40),
+                  file=sys.stderr)
     tokens = args.batch * args.seq * ws * args.steps
     flops_tok = 6 * (n_params - (cfg.block_size * cfg.n_embd if is_gpt else 0)) + 12 * cfg.n_layer * cfg.n_embd * args.seq
     tps = tokens / el
@@ -197,8 +211,10 @@ def main():
            "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
            "higher_is_better": True, "scaling": "weak", "dtype": "bf16", "data": "synthetic tokens",
            "samples_per_s": round(args.batch * ws * args.steps / el, 2), "mfu": round(mfu, 4),
-           "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+           "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(peak_mem / 1e9, 2),
            "final_loss": float(state["loss"].item()),
+           "comm": ("none: one rank (DDP skips the all-reduce, FSDP runs NO_SHARD)" if ws == 1 else
+                    type(getattr(wrapped, "comm", None)).__name__ if args.impl == "native" else "torch"),
            "config": {"model": args.model, "layers": cfg.n_layer, "global_batch": args.batch * ws,
                       "seq_len": args.seq, "parallelism": f"{args.strategy}{ws}", "impl": args.impl, "tunableop": args.tunableop,
                       "activation_checkpointing": args.ckpt}}
@@ -207,7 +223,7 @@ def main():
         if args.json_out:
             Path(args.json_out).write_text(json.dumps(out) + "\n")
     if dist.is_initialized():
-        dist.barrier(device_ids=[local])
+        dbarrier()
         dist.destroy_process_group()
 
 

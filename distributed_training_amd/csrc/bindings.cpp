@@ -53,6 +53,15 @@ size_t dta_mlp2_lds_bytes(int64_t, int, int);
 hipError_t dta_mlp_persistent(const dta::MlpPArgs*, int, hipStream_t);
 size_t dta_mlp_persistent_lds_bytes(int, int, int, int);
 hipError_t dta_p2p_create(int, int, int64_t, void**, void*);
+hipError_t dta_ipc_create(int, int, int64_t, void**, void*);
+int dta_ipc_handle_bytes();
+hipError_t dta_ipc_open(void*, const void*);
+int64_t dta_ipc_slot_bytes(void*);
+hipError_t dta_ipc_launch(void*, int, int, int, float, void*, const void*, int64_t, int64_t, int64_t, int, double,
+                          hipStream_t);
+int dta_ipc_error(void*);
+hipError_t dta_ipc_clear_error(void*);
+void dta_ipc_destroy(void*);
 int dta_p2p_handle_bytes();
 hipError_t dta_p2p_open(void*, const void*);
 int dta_p2p_num_wg(int64_t);
@@ -701,6 +710,118 @@ class PyRcclComm {
 
 }  // namespace
 
+// Intra-node collectives over IPC-mapped peer memory: csrc/ipc_coll.hip.
+// Every launch is validated here (dtype, alignment, capacity, shapes): the kernel
+// trusts its arguments.  Messages larger than one slot are split by the caller.
+class PyIpcColl {
+ public:
+  PyIpcColl(int rank, int world, int64_t slot_bytes) : rank_(rank), world_(world) {
+    std::string h(dta_ipc_handle_bytes(), '\0');
+    hip_ok(dta_ipc_create(rank, world, slot_bytes, &state_, h.data()), "ipc create");
+    handle_ = h;
+    slot_bytes_ = dta_ipc_slot_bytes(state_);
+  }
+  ~PyIpcColl() { destroy(); }
+  py::bytes handle() const { return py::bytes(handle_); }
+  void open(std::vector<py::bytes> handles) {
+    TORCH_CHECK((int)handles.size() == world_, "ipc open: need one handle per rank");
+    std::string all;
+    for (auto& h : handles) {
+      std::string s = h;
+      TORCH_CHECK((int)s.size() == dta_ipc_handle_bytes(), "ipc open: bad handle size");
+      all += s;
+    }
+    hip_ok(dta_ipc_open(state_, all.data()), "ipc open");
+  }
+  static int arith_bytes(const torch::Tensor& t) {
+    if (t.scalar_type() == torch::kFloat32) return 4;
+    if (t.scalar_type() == torch::kBFloat16) return 2;
+    TORCH_CHECK(false, "ipc: reductions support fp32 and bf16");
+    return 0;
+  }
+  static void check_buf(const torch::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "ipc ", what, ": contiguous GPU tensor");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "ipc ", what, ": 16-byte aligned");
+  }
+  // all-reduce in place; red: 0 sum, 1 max, 2 min; the whole tensor must fit W slots
+  void all_reduce(torch::Tensor t, int64_t red, double scale, double timeout_s, int64_t stream) {
+    check_buf(t, "all_reduce");
+    const int es = arith_bytes(t);
+    const int64_t n = t.numel();
+    int64_t m = (n + world_ - 1) / world_;
+    m = (m + 7) / 8 * 8;
+    TORCH_CHECK(m * es <= slot_bytes_, "ipc all_reduce: chunk larger than a slot (split the message)");
+    TORCH_CHECK(red >= 0 && red <= 2, "ipc all_reduce: op");
+    if (n == 0) return;
+    hip_ok(dta_ipc_launch(state_, 0, es, (int)red, (float)scale, t.data_ptr(), nullptr, n, m, m * es, 0, timeout_s,
+                          pick_stream(stream)),
+           "ipc all_reduce");
+  }
+  // out[m] = reduce over ranks of chunk `rank` of inp, where chunk q = inp[q * stride .. + m) (elements)
+  void reduce_scatter(torch::Tensor out, torch::Tensor inp, int64_t in_off, int64_t stride, int64_t m, int64_t red,
+                      double scale, double timeout_s, int64_t stream) {
+    check_buf(out, "reduce_scatter out");
+    TORCH_CHECK(inp.is_cuda() && inp.is_contiguous() && inp.scalar_type() == out.scalar_type(), "ipc reduce_scatter: inp");
+    const int es = arith_bytes(out);
+    TORCH_CHECK(m >= 0 && m <= out.numel() && in_off >= 0 && stride >= m &&
+                    in_off + (int64_t)(world_ - 1) * stride + m <= inp.numel(),
+                "ipc reduce_scatter: shapes");
+    const char* src = static_cast<const char*>(inp.data_ptr()) + in_off * es;
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(src) % 16 == 0 && (stride * es) % 16 == 0,
+                "ipc reduce_scatter: chunks must start 16-byte aligned");
+    TORCH_CHECK(m * es <= slot_bytes_, "ipc reduce_scatter: chunk larger than a slot");
+    if (m == 0) return;
+    hip_ok(dta_ipc_launch(state_, 1, es, (int)red, (float)scale, out.data_ptr(), src, m, m, stride * es, 0, timeout_s,
+                          pick_stream(stream)),
+           "ipc reduce_scatter");
+  }
+  // chunk q of out (at out_off + q * stride elements, m elements) = rank q's inp[in_off .. + m)
+  void all_gather(torch::Tensor out, torch::Tensor inp, int64_t out_off, int64_t stride, int64_t in_off, int64_t m,
+                  double timeout_s, int64_t stream) {
+    TORCH_CHECK(out.is_cuda() && out.is_contiguous() && inp.is_cuda() && inp.is_contiguous() &&
+                    out.element_size() == inp.element_size(),
+                "ipc all_gather: contiguous GPU tensors of one element size");
+    const int64_t es = out.element_size();
+    TORCH_CHECK((m * es) % 2 == 0, "ipc all_gather: even byte count");
+    TORCH_CHECK(m >= 0 && in_off >= 0 && in_off + m <= inp.numel() && out_off >= 0 && stride >= m &&
+                    out_off + (int64_t)(world_ - 1) * stride + m <= out.numel(),
+                "ipc all_gather: shapes");
+    char* dst = static_cast<char*>(out.data_ptr()) + out_off * es;
+    const char* src = static_cast<const char*>(inp.data_ptr()) + in_off * es;
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                    (stride * es) % 16 == 0,
+                "ipc all_gather: 16-byte aligned chunks");
+    TORCH_CHECK(m * es <= slot_bytes_, "ipc all_gather: shard larger than a slot");
+    if (m == 0) return;
+    hip_ok(dta_ipc_launch(state_, 2, 2, 0, 1.f, dst, src, (m * es) / 2, (m * es) / 2, stride * es, 0, timeout_s,
+                          pick_stream(stream)),
+           "ipc all_gather");
+  }
+  void broadcast(torch::Tensor t, int64_t root, double timeout_s, int64_t stream) {
+    check_buf(t, "broadcast");
+    const int64_t nb = t.numel() * t.element_size();
+    TORCH_CHECK(nb % 2 == 0 && nb <= slot_bytes_, "ipc broadcast: even byte count within one slot");
+    TORCH_CHECK(root >= 0 && root < world_, "ipc broadcast: root");
+    if (nb == 0) return;
+    hip_ok(dta_ipc_launch(state_, 3, 2, 0, 1.f, t.data_ptr(), nullptr, nb / 2, nb / 2, 0, (int)root, timeout_s,
+                          pick_stream(stream)),
+           "ipc broadcast");
+  }
+  int error() const { return state_ ? dta_ipc_error(state_) : 0; }
+  void clear_error() { hip_ok(dta_ipc_clear_error(state_), "ipc clear_error"); }
+  void destroy() {
+    if (state_) dta_ipc_destroy(state_);
+    state_ = nullptr;
+  }
+  int64_t slot_bytes() const { return slot_bytes_; }
+
+ private:
+  void* state_ = nullptr;
+  int rank_, world_;
+  int64_t slot_bytes_ = 0;
+  std::string handle_;
+};
+
 // One-shot intra-node all-reduce over peer (xGMI) memory: csrc/p2p_allreduce.hip
 class PyP2PAllReduce {
  public:
@@ -983,6 +1104,18 @@ PYBIND11_MODULE(_C, m) {
     return v;
   });
   m.def("p2p_num_wg", &dta_p2p_num_wg);
+  py::class_<PyIpcColl>(m, "IpcColl")
+      .def(py::init<int, int, int64_t>())
+      .def("handle", &PyIpcColl::handle)
+      .def("open", &PyIpcColl::open)
+      .def("all_reduce", &PyIpcColl::all_reduce)
+      .def("reduce_scatter", &PyIpcColl::reduce_scatter)
+      .def("all_gather", &PyIpcColl::all_gather)
+      .def("broadcast", &PyIpcColl::broadcast)
+      .def("error", &PyIpcColl::error)
+      .def("clear_error", &PyIpcColl::clear_error)
+      .def("destroy", &PyIpcColl::destroy)
+      .def_property_readonly("slot_bytes", &PyIpcColl::slot_bytes);
   py::class_<PyP2PAllReduce>(m, "P2PAllReduce")
       .def(py::init<int, int, int64_t>())
       .def("handle", &PyP2PAllReduce::handle)

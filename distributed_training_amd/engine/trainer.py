@@ -125,7 +125,7 @@ class Trainer:
                            first_bucket_mb=c.first_bucket_mb, mixed_precision=c.mixed_precision)
 
     def _setup_model(self, model: torch.nn.Module) -> torch.nn.Module:
-        device = self.env.local_rank if self.env.is_gpu else self.env.device
+        device = self.env.torch_device.index if self.env.is_gpu else self.env.device
         model = model.to(self.device)
         self._strategy = self._make_strategy()
         self.checkpoint = ModelCheckpoint(Path(self.config.snapshot_path), self.env, self._strategy)

@@ -163,7 +163,34 @@ class TorchComm(Communicator):
             dist.barrier(group=self.group)
 
 
-class RcclComm(Communicator):
+class _StreamComm(Communicator):
+    """Collectives enqueued on the communicator's own HIP stream: the stream
+    first waits on the caller's (compute) stream, the returned work's event
+    makes a consumer stream wait in turn -- no host synchronisation, and the
+    caching allocator is told (``record_stream``) that the tensors are in use
+    on the comm stream."""
+
+    stream: torch.cuda.Stream
+
+    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor]) -> Optional[CommWork]:
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        fn(int(self.stream.cuda_stream))
+        for t in tensors:  # keep the caching allocator from recycling the memory early
+            t.record_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        work = CommWork(event=ev)
+        if async_op:
+            return work
+        work.wait(cur)
+        return None
+
+    def poll_errors(self) -> None:
+        """Raise if a bounded peer wait timed out (cheap: no device sync)."""
+
+
+class RcclComm(_StreamComm):
     """Native RCCL communicator on a dedicated HIP stream (GPU hot path)."""
 
     name = "rccl"
@@ -199,20 +226,6 @@ class RcclComm(Communicator):
                 torch.cuda.current_stream(device).synchronize()
 
             self._p2p = maybe_create(rank, world_size, device, store, _min, tag=tag)
-
-    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor]) -> Optional[CommWork]:
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        fn(int(self.stream.cuda_stream))
-        for t in tensors:  # keep the caching allocator from recycling the memory early
-            t.record_stream(self.stream)
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        work = CommWork(event=ev)
-        if async_op:
-            return work
-        work.wait(cur)
-        return None
 
     def supports_avg(self) -> bool:
         return True
@@ -270,10 +283,20 @@ class RcclComm(Communicator):
 
 
 def make_comm(device: torch.device, prefer: str = "auto", group=None) -> Communicator:
-    """Pick the communicator for ``device``: native RCCL for GPU tensors
-    (``prefer`` = auto|rccl), torch.distributed otherwise."""
+    """Pick the communicator for ``device``.
+
+    GPU: native RCCL (``prefer`` auto|rccl, the default); the IPC direct-push
+    collectives (:class:`~.ipc.IpcComm`) with ``prefer="ipc"`` / ``DTA_COMM=ipc``,
+    and always when several ranks share one GPU (``DTA_SHARED_GPU=1``: RCCL
+    refuses that).  CPU, or ``DTA_COMM=torch``: torch.distributed (gloo)."""
+    from .ipc import IpcComm, shared_gpu
+
     rank = dist.get_rank() if dist.is_initialized() else 0
     ws = dist.get_world_size() if dist.is_initialized() else 1
-    if device.type == "cuda" and prefer in ("auto", "rccl") and os.environ.get("DTA_COMM", "") != "torch":
-        return RcclComm(rank, ws, device)
+    env = os.environ.get("DTA_COMM", "")
+    if device.type == "cuda" and env != "torch":
+        if ws > 1 and (shared_gpu() or prefer == "ipc" or env == "ipc"):
+            return IpcComm(rank, ws, device)
+        if prefer in ("auto", "rccl", "ipc"):
+            return RcclComm(rank, ws, device)
     return TorchComm(group=group, device=device)

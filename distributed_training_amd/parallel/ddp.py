@@ -211,10 +211,11 @@ class DistributedDataParallel(nn.Module):
     def state_dict(self, *args, **kwargs):
         sd = super().state_dict(*args, **kwargs)
         if self.flat.mixed:  # checkpoints carry the fp32 master, not the bf16 compute copy
-            prefix = kwargs.get("prefix", "")
-            for i, name in enumerate(self.flat.names):
-                key = f"{prefix}module.{name}"
-                if key in sd:
+            # matched by storage, so tied aliases (GPT-2 lm_head.weight = wte.weight) get it too
+            master_of = {self.flat.param_view(i).data_ptr(): i for i in range(len(self.flat.params))}
+            for key, v in sd.items():
+                i = master_of.get(v.data_ptr()) if v.dtype == self.flat.param_dtype else None
+                if i is not None and tuple(v.shape) == self.flat.shapes[i]:
                     sd[key] = self.flat.master_view(i).detach()
         return sd
 

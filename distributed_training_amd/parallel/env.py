@@ -56,7 +56,9 @@ class DistributedEnvironment:
 
     @property
     def torch_device(self) -> torch.device:
-        return torch.device("cuda", self.local_rank) if self.is_gpu else torch.device("cpu")
+        from .ipc import device_index
+
+        return torch.device("cuda", device_index(self.local_rank)) if self.is_gpu else torch.device("cpu")
 
     def setup(self) -> None:
         if self.is_gpu and ("LOCAL_RANK" not in os.environ or "RANK" not in os.environ):
@@ -69,13 +71,15 @@ class DistributedEnvironment:
         os.environ.setdefault("RANK", str(self.global_rank))
         os.environ.setdefault("WORLD_SIZE", str(self.world_size))
         if self.is_gpu:
-            torch.cuda.set_device(self.local_rank)
-        backend = self.backend or ("nccl" if self.is_gpu else "gloo")
+            torch.cuda.set_device(self.torch_device)
+        from .ipc import dist_backend
+
+        backend = self.backend or dist_backend(self.is_gpu)
         if not dist.is_initialized():
             kwargs = {}
             if self.timeout_s:
                 kwargs["timeout"] = datetime.timedelta(seconds=float(self.timeout_s))
-            if self.is_gpu:
+            if self.is_gpu and backend == "nccl":
                 kwargs["device_id"] = self.torch_device
             dist.init_process_group(backend=backend, **kwargs)
             self._owns_pg = True
@@ -94,8 +98,8 @@ class DistributedEnvironment:
 
     def barrier(self) -> None:
         if dist.is_initialized() and dist.get_world_size() > 1:
-            if self.is_gpu:
-                dist.barrier(device_ids=[self.local_rank])
+            if self.is_gpu and dist.get_backend() == "nccl":
+                dist.barrier(device_ids=[self.torch_device.index])
             else:
                 dist.barrier()
 

@@ -41,7 +41,7 @@ def check_replicas_in_sync(model: torch.nn.Module, env, rtol: float = 0.0) -> No
     if hasattr(model, "full_state_dict"):  # FSDP: shards differ by construction
         return
     c = param_checksums(model)
-    dev = torch.device("cuda", env.local_rank) if env.is_gpu else torch.device("cpu")
+    dev = env.torch_device if env.is_gpu and dist.get_backend() == "nccl" else torch.device("cpu")
     hi = c.to(dev).clone()
     lo = c.to(dev).clone()
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)

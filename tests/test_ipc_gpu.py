@@ -1,0 +1,249 @@
+"""IPC direct-push collectives (csrc/ipc_coll.hip) and the multi-rank DDP / FSDP
+GPU engines on top of them, with several processes sharing the box's single
+GPU (DTA_SHARED_GPU=1).  Same kernels, comm stream, record_stream, storage
+resize_ and prefetch code as on a real 8-GPU node; only the link differs.
+
+References: every collective against exact expectations built from all ranks'
+inputs (gathered over gloo), reduced in rank order in fp32 and rounded once;
+the engines against the same model trained by ONE rank on the global batch."""
+import os
+
+import pytest
+import torch
+
+from dist_utils import run_gloo
+
+pytestmark = pytest.mark.gpu
+
+
+def _shared():
+    os.environ["DTA_SHARED_GPU"] = "1"
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+def _gather_cpu(x):
+    """All ranks' copies of x as fp32 CPU tensors (exact for fp32 / bf16 inputs; gloo has no bf16)."""
+    import torch.distributed as dist
+
+    c = x.detach().float().cpu().contiguous()
+    parts = [torch.empty_like(c) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, c)
+    return parts
+
+
+def _coll_worker(rank, ws, slot_mb):
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    comm = IpcComm(rank, ws, dev, slot_mb=slot_mb)
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    # all-reduce: sizes around vector / chunk / segment boundaries, both dtypes, every op
+    for dt in (torch.float32, torch.bfloat16):
+        for n in (1, 7, 8 * ws + 3, 4097, 70001, 300007):
+            for op in ("sum", "avg", "max", "min"):
+                x = torch.randn(n, generator=g).to(dt).to(dev)
+                parts = _gather_cpu(x)
+                acc = parts[0].clone()
+                for p in parts[1:]:  # rank order, fp32, like the kernel
+                    acc = acc + p if op in ("sum", "avg") else (torch.maximum(acc, p) if op == "max"
+                                                                else torch.minimum(acc, p))
+                if op == "avg":
+                    acc = acc * (1.0 / ws)
+                want = acc.to(dt)
+                comm.all_reduce(x, op)
+                torch.cuda.synchronize()
+                assert torch.equal(x.cpu(), want), (dt, n, op, (x.cpu().float() - want.float()).abs().max())
+    # reduce-scatter / all-gather: aligned and unaligned chunk sizes, async + wait
+    for dt in (torch.float32, torch.bfloat16):
+        for m in (5, 64, 1000, 40000):
+            inp = torch.randn(ws * m, generator=g).to(dt).to(dev)
+            parts = _gather_cpu(inp)
+            full = sum(parts[1:], parts[0].clone()) * (1.0 / ws)
+            out = torch.empty(m, dtype=dt, device=dev)
+            w = comm.reduce_scatter_into(out, inp, op="avg", async_op=True)
+            w.wait()
+            torch.cuda.synchronize()
+            assert torch.equal(out.cpu(), full[rank * m:(rank + 1) * m].to(dt)), (dt, m)
+            shard = torch.randn(m, generator=g).to(dt).to(dev)
+            gathered = torch.empty(ws * m, dtype=dt, device=dev)
+            comm.all_gather_into(gathered, shard)
+            torch.cuda.synchronize()
+            assert torch.equal(gathered.float().cpu(), torch.cat(_gather_cpu(shard))), (dt, m)
+    # broadcast: even / odd byte counts, every root
+    for root in range(ws):
+        for n in (3, 1001, 200003):
+            b = torch.full((n,), float(rank * 10 + 1), device=dev)
+            comm.broadcast(b, src=root)
+            torch.cuda.synchronize()
+            assert torch.equal(b, torch.full_like(b, float(root * 10 + 1))), (root, n)
+        c = torch.full((7,), rank + 3, dtype=torch.uint8, device=dev)  # 7 bytes: control-plane path
+        comm.broadcast(c, src=root)
+        assert int(c[0]) == root + 3
+    # many back-to-back async ops with compute in between (parity reuse, stream ordering)
+    xs = [torch.full((11280,), float(rank + i), device=dev) for i in range(40)]
+    works = []
+    for x in xs:
+        x.mul_(2.0)
+        works.append(comm.all_reduce(x, "sum", async_op=True))
+    for w in works:
+        w.wait()
+    torch.cuda.synchronize()
+    for i, x in enumerate(xs):
+        assert torch.equal(x, torch.full_like(x, float(sum(2 * (r + i) for r in range(ws))))), i
+    # hipGraph capture of the inline all-reduce (device epochs advance on replay)
+    buf = torch.zeros(5000, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            for _ in range(3):
+                buf.add_(1.0)
+                comm.all_reduce_inline(buf, "sum", stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    for rep in range(2):
+        buf.fill_(float(rank))
+        graph.replay()
+        torch.cuda.synchronize()
+        b = [float(r) for r in range(ws)]
+        for _ in range(3):
+            b = [sum(v + 1.0 for v in b)] * ws
+        assert torch.equal(buf, torch.full_like(buf, b[0])), rep
+    comm.poll_errors()
+    comm.destroy()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_ipc_collectives_shared_gpu(ws):
+    run_gloo(_coll_worker, ws, 0.25)  # 256 KiB slots: multi-segment messages
+
+
+def _bf16_8rank_worker(rank, ws):
+    """bf16 all-reduce at 8 ranks: ONE rounding of the exact fp32 rank-order sum."""
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    comm = IpcComm(rank, ws, dev)
+    g = torch.Generator(device="cpu").manual_seed(7 + rank)
+    x = torch.randn(1 << 18, generator=g).to(torch.bfloat16).to(dev)
+    parts = [p.double() for p in _gather_cpu(x)]  # exact bf16 values
+    exact = sum(parts)                      # fp64 reference of the bf16 inputs
+    comm.all_reduce(x, "sum")
+    torch.cuda.synchronize()
+    got = x.cpu().double()
+    # one rounding to bf16 (8 significant bits) of a sum accumulated in fp32
+    rel = ((got - exact).abs() / exact.abs().clamp_min(1e-3)).max().item()
+    assert rel <= 2 ** -8 + 1e-6, rel
+    allx = _gather_cpu(x)
+    assert all(torch.equal(allx[0], a) for a in allx), "ranks disagree"
+    comm.destroy()
+
+
+def test_ipc_bf16_allreduce_error_8_ranks():
+    run_gloo(_bf16_8rank_worker, 8)
+
+
+def _timeout_worker(rank, ws):
+    import torch.distributed as dist
+
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    comm = IpcComm(rank, ws, dev, timeout_s=1.0)
+    if rank == 0:  # the peer never joins: bounded wait, sticky error seen by the host poll
+        x = torch.ones(1000, device=dev)
+        comm.all_reduce(x)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="timed out"):
+            comm.poll_errors()
+    dist.barrier()
+    comm.destroy()
+
+
+def test_ipc_timeout_raises():
+    run_gloo(_timeout_worker, 2)
+
+
+# ---------------------------------------------------------------- engines
+def _tiny_gpt2():
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+
+    torch.manual_seed(0)
+    return GPT2(GPT2Config(n_layer=2, n_head=2, n_embd=128, vocab_size=512, block_size=64))
+
+
+def _train(model_wrapped, opt, batches, steps):
+    losses = []
+    for it in range(steps):
+        x = batches[it]
+        opt.zero_grad(set_to_none=True)
+        loss = model_wrapped(x[:, :-1], x[:, 1:])
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.item()))
+    return losses
+
+
+def _engine_worker(rank, ws, strategy):
+    import torch.distributed as dist
+
+    from distributed_training_amd.models.gpt2 import GPT2
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    B, T, steps = 2, 64, 3
+    g = torch.Generator(device="cpu").manual_seed(5)
+    glob = [torch.randint(0, 512, (ws * B, T + 1), generator=g).to(dev) for _ in range(steps)]
+    # reference: one rank, the global batch, same bf16 engine with no communication
+    ref = _tiny_gpt2().to(dev)
+    ref_w = DistributedDataParallel(ref, comm=IpcComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    ref_opt = FusedSGD(ref_w.parameters(), lr=0.05, momentum=0.9)
+    init_sd = {k[len("module."):]: v.float().cpu().clone() for k, v in ref_w.state_dict().items()}
+    ref_losses = _train(ref_w, ref_opt, glob, steps)
+    ref_sd = {k[len("module."):]: v.float().cpu() for k, v in ref_w.state_dict().items()}
+
+    comm = IpcComm(rank, ws, dev)
+    model = _tiny_gpt2().to(dev)
+    if rank == 1:  # a different init on one rank: the wrap-time broadcast must fix it
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(0.5)
+    if strategy == "ddp":
+        w = DistributedDataParallel(model, comm=comm, device=dev, param_dtype=torch.bfloat16,
+                                    bucket_cap_mb=0.25, first_bucket_mb=0.05)  # several buckets: overlap path
+        assert len(w.buckets) >= 3
+    else:
+        w = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy={GPT2.block_class},
+                                     param_dtype=torch.bfloat16)
+        assert len(w.units) == 3
+    opt = FusedSGD(w.parameters(), lr=0.05, momentum=0.9)
+    local = [x[rank * B:(rank + 1) * B] for x in glob]
+    losses = _train(w, opt, local, steps)
+    comm.poll_errors()
+    # mean of the per-rank losses == the reference's global-batch loss (before any update diverges)
+    l0 = torch.tensor([losses[0]])
+    dist.all_reduce(l0)
+    assert abs(l0.item() / ws - ref_losses[0]) < 2e-2 * abs(ref_losses[0]), (l0.item() / ws, ref_losses[0])
+    sd = w.full_state_dict(rank0_only=False) if strategy == "fsdp" else {
+        k[len("module."):]: v for k, v in w.state_dict().items()}
+    assert set(sd) == set(ref_sd), (sorted(set(sd) ^ set(ref_sd)))
+    for k, v in sd.items():
+        a, b = v.float().cpu(), ref_sd[k]
+        moved = (b - init_sd[k]).abs().max().item()
+        # bf16 compute + bf16 gradient reduction across ranks vs one rank on the global batch:
+        # the SGD trajectories agree to a small fraction of how far the weights moved
+        assert (a - b).abs().max().item() <= 0.05 * moved + 1e-5, (k, (a - b).abs().max().item(), moved)
+    # replicas are bit-identical across ranks (DDP: every parameter; FSDP: the gathered state)
+    parts = _gather_cpu(torch.cat([v.float().reshape(-1).cpu() for v in sd.values()]))
+    assert all(torch.equal(parts[0], p) for p in parts), "replicas diverged"
+    comm.destroy()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("strategy", ["ddp", "fsdp"])
+def test_engines_multi_rank_shared_gpu(strategy, ws):
+    run_gloo(_engine_worker, ws, strategy)
