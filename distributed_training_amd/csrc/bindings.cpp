@@ -67,6 +67,7 @@ hipError_t dta_p2p_open(void*, const void*);
 int dta_p2p_num_wg(int64_t);
 hipError_t dta_p2p_allreduce(void*, float*, int64_t, float, int, hipStream_t);
 hipError_t dta_p2p_error(void*, int*);
+int dta_p2p_error_nosync(void*);
 hipError_t dta_p2p_clear_error(void*);
 void dta_p2p_destroy(void*);
 void dta_p2p_set_ll(void*, int);
@@ -854,6 +855,7 @@ class PyP2PAllReduce {
     hip_ok(dta_p2p_error(state_, &e), "p2p error");
     return e;
   }
+  int error_nosync() const { return state_ ? dta_p2p_error_nosync(state_) : 0; }
   void clear_error() { hip_ok(dta_p2p_clear_error(state_), "p2p clear_error"); }
   void destroy() {
     if (state_) dta_p2p_destroy(state_);
@@ -1122,6 +1124,7 @@ PYBIND11_MODULE(_C, m) {
       .def("open", &PyP2PAllReduce::open)
       .def("all_reduce", &PyP2PAllReduce::all_reduce)
       .def("error", &PyP2PAllReduce::error)
+      .def("error_nosync", &PyP2PAllReduce::error_nosync)
       .def("destroy", &PyP2PAllReduce::destroy)
       .def("set_ll", &PyP2PAllReduce::set_ll)
       .def("ll_info", &PyP2PAllReduce::ll_info)

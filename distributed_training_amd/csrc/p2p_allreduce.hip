@@ -54,6 +54,7 @@ struct P2PArgs {
   const float* local_data;          // == peer_data[rank]
   int* epoch_ctr;                   // [kP2PMaxWG], local, not shared
   int* err;
+  int* err_host;                    // host-mapped copy of err: polled by the engines without a device sync
   int timeout_iters;
   uint64_t* peer_ll[kP2PMaxRanks];  // LL slots [2][world][max_elems] of {f32, epoch}
   const uint64_t* local_ll;
@@ -61,6 +62,11 @@ struct P2PArgs {
 
 __device__ __forceinline__ bool peer_failed(int* err) {
   return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+__device__ __forceinline__ void raise_err(const P2PArgs& a) {
+  atomicOr(a.err, 1);
+  if (a.err_host) __hip_atomic_store(a.err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The epoch is global per call: every workgroup slot counter advances together
@@ -105,7 +111,7 @@ __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_ll_kernel(P2PArgs a
         // bounded wait; once any wait timed out (sticky error flag) every later
         // wait gives up at once, so a dead peer costs one timeout, not one per element
         if (++it > a.timeout_iters || ((it & 1023) == 1 && peer_failed(a.err))) {
-          atomicOr(a.err, 1);
+          raise_err(a);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -149,7 +155,7 @@ __global__ void __launch_bounds__(kP2PThreads) p2p_allreduce_kernel(P2PArgs a) {
     int it = 0;
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (++it > a.timeout_iters || ((it & 1023) == 1 && peer_failed(a.err))) {
-        atomicOr(a.err, 1);
+        raise_err(a);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -193,6 +199,7 @@ struct P2PState {
   int ll = 1;
   int* epoch = nullptr;
   int* err = nullptr;
+  int* err_host = nullptr;
   char* peers[kP2PMaxRanks] = {};
   bool opened = false;
 };
@@ -216,12 +223,16 @@ hipError_t dta_p2p_create(int rank, int world, int64_t max_elems, void** state_o
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->epoch), kP2PMaxWG * sizeof(int) + 64);
   if (e == hipSuccess) e = hipMemset(s->epoch, 0, kP2PMaxWG * sizeof(int) + 64);
   if (e == hipSuccess) s->err = s->epoch + kP2PMaxWG;
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&s->err_host), 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) *s->err_host = 0;
   hipIpcMemHandle_t h;
   if (e == hipSuccess) e = hipIpcGetMemHandle(&h, s->buf);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     if (s->buf) (void)hipFree(s->buf);
     if (s->epoch) (void)hipFree(s->epoch);
+    if (s->err_host) (void)hipHostFree(s->err_host);
     delete s;
     return e;
   }
@@ -310,6 +321,7 @@ hipError_t dta_p2p_allreduce(void* state, float* data, int64_t n, float scale, i
   a.local_data = reinterpret_cast<const float*>(s->buf);
   a.epoch_ctr = s->epoch;
   a.err = s->err;
+  a.err_host = s->err_host;
   a.timeout_iters = timeout_iters;
   const int grid = (int)((n + a.chunk - 1) / a.chunk);
   if (s->ll) hipLaunchKernelGGL(p2p_allreduce_ll_kernel, dim3(grid), dim3(kP2PThreads), 0, st, a);
@@ -322,10 +334,17 @@ hipError_t dta_p2p_error(void* state, int* out) {
   return hipMemcpy(out, s->err, sizeof(int), hipMemcpyDeviceToHost);
 }
 
+// The all-reduce kernels' timeout flag as seen by the host, without a device sync
+// (the persistent MLP loop raises only the device flag: dta_p2p_error covers it).
+int dta_p2p_error_nosync(void* state) {
+  return __atomic_load_n(static_cast<P2PState*>(state)->err_host, __ATOMIC_ACQUIRE);
+}
+
 // Re-arm after a timed-out exchange that was expected to be survivable (e.g. a
 // probe of an exchange form during calibration); every rank clears together.
 hipError_t dta_p2p_clear_error(void* state) {
   auto* s = static_cast<P2PState*>(state);
+  __atomic_store_n(s->err_host, 0, __ATOMIC_RELEASE);
   return hipMemset(s->err, 0, sizeof(int));
 }
 
@@ -337,5 +356,6 @@ void dta_p2p_destroy(void* state) {
     if (q != s->rank && s->peers[q]) (void)hipIpcCloseMemHandle(s->peers[q]);
   if (s->buf) (void)hipFree(s->buf);
   if (s->epoch) (void)hipFree(s->epoch);
+  if (s->err_host) (void)hipHostFree(s->err_host);
   delete s;
 }

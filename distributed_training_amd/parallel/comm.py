@@ -273,6 +273,12 @@ class RcclComm(_StreamComm):
         if self._p2p is not None:
             self._p2p.check()
 
+    def poll_errors(self) -> None:
+        """Per-step check of the p2p path's sticky timeout flag (no device sync): a peer
+        that never delivered leaves a partial sum, so training must not go on silently."""
+        if self._p2p is not None:
+            self._p2p.poll()
+
     def barrier(self):
         x = torch.zeros(1, device=self.device)
         self.all_reduce(x)

@@ -189,6 +189,8 @@ class DistributedDataParallel(nn.Module):
         for w in self._works:
             w.wait()
         self._reset_iteration()
+        if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
+            self.comm.poll_errors()  # a timed-out peer exchange raises here, not silently later
 
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self.world_size > 1 and self.require_sync:

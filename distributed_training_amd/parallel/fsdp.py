@@ -413,6 +413,8 @@ class FullyShardedDataParallel(nn.Module):
             self._written = set()
         self._pending_rs = []
         self._cb_queued = False
+        if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
+            self.comm.poll_errors()
         for u in self.units:  # any unit not used in backward: drop its gathered copy
             u.in_backward = False
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):

@@ -77,6 +77,12 @@ class P2PAllReduce:
         if self._h.error():
             raise RuntimeError(f"rank {self.rank}: p2p all-reduce timed out waiting for a peer")
 
+    def poll(self) -> None:
+        """Raise if an all-reduce launch timed out (host-mapped flag: no device sync)."""
+        if self._h.error_nosync():
+            raise RuntimeError(f"rank {self.rank}: p2p all-reduce timed out waiting for a peer; "
+                               "gradients of that step are partial")
+
     def destroy(self) -> None:
         self._h.destroy()
 

@@ -165,6 +165,36 @@ def test_ipc_timeout_raises():
     run_gloo(_timeout_worker, 2)
 
 
+def _ddp_stall_worker(rank, ws):
+    """A rank that stops taking part: the DDP engine of the others raises at its next
+    step instead of training on partial gradient sums (no hang: bounded waits)."""
+    import torch.distributed as dist
+    import torch.nn.functional as F
+
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    comm = IpcComm(rank, ws, dev, timeout_s=1.0)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 1)).to(dev)
+    ddp = DistributedDataParallel(net, comm=comm, device=dev)
+    x, y = torch.randn(8, 16, device=dev), torch.randn(8, 1, device=dev)
+    F.mse_loss(ddp(x), y).backward()  # both ranks: a normal step
+    torch.cuda.synchronize()
+    if rank == 0:
+        F.mse_loss(ddp(x), y).backward()  # the peer is gone: this exchange times out
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="timed out"):
+            F.mse_loss(ddp(x), y).backward()
+    dist.barrier()
+    comm.destroy()
+
+
+def test_ddp_raises_when_a_peer_stalls():
+    run_gloo(_ddp_stall_worker, 2)
+
+
 # ---------------------------------------------------------------- engines
 def _tiny_gpt2():
     from distributed_training_amd.models.gpt2 import GPT2, GPT2Config

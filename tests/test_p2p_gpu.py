@@ -91,6 +91,8 @@ def _timeout_worker(rank, ws, protocol):
         torch.cuda.synchronize()
         with pytest.raises(RuntimeError, match="timed out"):
             p2p.check()
+        with pytest.raises(RuntimeError, match="timed out"):  # the engines' per-step poll (no device sync)
+            p2p.poll()
     dist.barrier()
     p2p.destroy()
 
