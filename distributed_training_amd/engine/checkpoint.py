@@ -7,8 +7,9 @@ strategies' ``save_checkpoint``/``load_checkpoint``
 Format (unchanged, byte-compatible): a ``torch.save`` of
 ``{"MODEL_STATE": OrderedDict[str, Tensor], "EPOCHS_RUN": int}`` -- DDP keys
 ``module.<name>``, FSDP keys unprefixed -- loadable with
-``torch.load(..., weights_only=True)``.  Optional extra keys (``OPTIM_STATE``)
-do not break reference loaders.
+``torch.load(..., weights_only=True)``.  Optional extra keys (``OPTIM_STATE``:
+the complete optimizer state -- FSDP's gathered from every rank's shards and
+keyed by parameter name -- restored on resume) do not break reference loaders.
 
 Fixes: the model state is collected on ALL ranks (the
 FSDP full-state-dict gather is a collective), only global rank 0 writes, the
@@ -39,21 +40,30 @@ class ModelCheckpoint:
     def save(self, model: torch.nn.Module, epoch: int, optimizer: Optional[torch.optim.Optimizer] = None) -> None:
         # collective on every rank (FSDP full-state gather), write on rank 0
         model_state = self.strategy.model_state(model)
+        optim_state = None
+        if self.save_optimizer and optimizer is not None:  # collective too (FSDP gathers its shards)
+            optim_state = self.strategy.optim_state(model, optimizer)
         if self.env.global_rank == 0:
             state_dict = {"MODEL_STATE": model_state, "EPOCHS_RUN": epoch}
-            if self.save_optimizer and optimizer is not None:
-                state_dict["OPTIM_STATE"] = optimizer.state_dict()
+            if optim_state is not None:
+                state_dict["OPTIM_STATE"] = optim_state
             self.strategy.save_checkpoint(model, state_dict, str(self.path))
             logger.info(f"Epoch {epoch} | Training snapshot saved at {self.path}")
         self.env.barrier()
 
-    def load(self, model: torch.nn.Module, device: Any) -> Tuple[torch.nn.Module, int]:
+    def load(self, model: torch.nn.Module, device: Any,
+             optimizer: Optional[torch.optim.Optimizer] = None) -> Tuple[torch.nn.Module, int]:
         if not self.path.exists():
             return model, 0
         logger.info("Loading snapshot")
-        map_loc = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
-        snapshot = torch.load(self.path, map_location=map_loc, weights_only=True)
-        return self.strategy.load_checkpoint(model, snapshot, device)
+        # tensors stay on the host: the strategy copies each into place (an 8B-parameter
+        # FSDP snapshot would otherwise be materialised on every rank's GPU at once)
+        snapshot = torch.load(self.path, map_location="cpu", weights_only=True)
+        model, epochs = self.strategy.load_checkpoint(model, snapshot, device)
+        if optimizer is not None and "OPTIM_STATE" in snapshot:
+            self.strategy.load_optim_state(model, optimizer, snapshot["OPTIM_STATE"])
+            logger.info("Optimizer state restored")
+        return model, epochs
 
 
 def atomic_torch_save(obj: Any, path: str) -> None:

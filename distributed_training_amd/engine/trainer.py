@@ -132,7 +132,7 @@ class Trainer:
         original_params = [p for g in self.optimizer.param_groups for p in g["params"]]
         model = self._strategy.prepare_model(model, self.device)
         self._rebind_optimizer(model, original_params)
-        model, self.epochs_run = self.checkpoint.load(model, device)
+        model, self.epochs_run = self.checkpoint.load(model, device, self.optimizer)
         return model
 
     def _rebind_optimizer(self, model: torch.nn.Module, original_params) -> None:
@@ -182,7 +182,10 @@ class Trainer:
             loss = self._loss_fn(output, targets)
         loss.backward()
         if self.config.grad_clip:
-            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.grad_clip)
+            if hasattr(self.model, "clip_grad_norm_"):  # native engines: global norm over the flat (sharded) grads
+                self.model.clip_grad_norm_(self.config.grad_clip)
+            else:
+                torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.grad_clip)
         self.optimizer.step()
         return loss
 

@@ -59,6 +59,42 @@ def _sgd_ref(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], lr, 
     p.add_(d, alpha=-lr)
 
 
+def _saved_state_by_param(opt: torch.optim.Optimizer, state_dict: dict) -> Dict[torch.nn.Parameter, dict]:
+    """Map a ``torch.optim.Optimizer.state_dict()`` onto this optimizer's parameters
+    (same param-group structure), restoring the groups' hyper-parameters.  Unlike
+    torch's ``load_state_dict`` nothing is cast to the parameter dtype: under bf16
+    mixed precision the parameters are bf16 compute copies while the optimizer
+    state is fp32 and lives in flat buffers beside the fp32 master."""
+    saved_groups = state_dict["param_groups"]
+    if len(saved_groups) != len(opt.param_groups) or any(
+            len(g["params"]) != len(sg["params"]) for g, sg in zip(opt.param_groups, saved_groups)):
+        raise ValueError("optimizer state dict does not match the optimizer's parameter groups")
+    saved = state_dict["state"]
+    out: Dict[torch.nn.Parameter, dict] = {}
+    for g, sg in zip(opt.param_groups, saved_groups):
+        for k, v in sg.items():
+            if k != "params":
+                g[k] = v
+        for p, pid in zip(g["params"], sg["params"]):
+            st = saved.get(pid, saved.get(str(pid)))
+            if st:
+                out[p] = st
+    return out
+
+
+def _restore_flat(fg, by_param: Dict[torch.nn.Parameter, dict], key: str) -> Optional[torch.Tensor]:
+    """A fresh flat fp32 buffer (the layout of ``fg.master``) filled with each
+    parameter's saved ``key`` tensor; None when no parameter has one."""
+    if not any(key in by_param.get(p, {}) for p in fg.params):
+        return None
+    flat = torch.zeros_like(fg.master)
+    for i, p in enumerate(fg.params):
+        v = by_param.get(p, {}).get(key)
+        if v is not None:
+            fg._view(flat, i).copy_(v.reshape(fg.shapes[i]).to(flat.device, torch.float32))
+    return flat
+
+
 class FusedSGD(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False):
@@ -117,6 +153,30 @@ class FusedSGD(torch.optim.Optimizer):
                 else:
                     _sgd_ref(p, p.grad, buf, lr, mom, damp, wd, nest, maxi, first)
         return loss
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict: dict) -> None:
+        """Resume: momentum buffers go back into the flat fp32 state (resumable after a
+        checkpoint written by ``state_dict()``)."""
+        by_param = _saved_state_by_param(self, state_dict)
+        for group in self.param_groups:
+            flats, singles = _split_params(group["params"])
+            for fg, ps in flats:
+                flat = _restore_flat(fg, by_param, "momentum_buffer")
+                if flat is None:
+                    continue
+                if len(ps) == len(fg.params):
+                    self._flat_state[id(fg)] = {"first": False, "mom": flat}
+                    for i, p in enumerate(fg.params):
+                        self.state[p]["momentum_buffer"] = fg._view(flat, i)
+                else:
+                    for p in ps:
+                        i = fg.index_of(p)
+                        self.state[p]["momentum_buffer"] = fg._view(flat, i).reshape(-1).clone()
+            for p in singles:
+                v = by_param.get(p, {}).get("momentum_buffer")
+                if v is not None:
+                    self.state[p]["momentum_buffer"] = v.to(p.device, torch.float32).reshape(p.shape).clone()
 
     def _single_gpu(self, fg, p, lr, mom, damp, wd, nest, maxi):
         i = fg.index_of(p)
@@ -234,6 +294,45 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
     zero_grad = FusedSGD.zero_grad
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict: dict) -> None:
+        """Resume: first / second moments and the step count go back into the flat fp32
+        state (the fused step keeps them there, not in per-parameter tensors)."""
+        by_param = _saved_state_by_param(self, state_dict)
+        for group in self.param_groups:
+            flats, singles = _split_params(group["params"])
+            for fg, _ps in flats:
+                m = _restore_flat(fg, by_param, "exp_avg")
+                if m is None:
+                    continue
+                v = _restore_flat(fg, by_param, "exp_avg_sq")
+                vmax = _restore_flat(fg, by_param, "max_exp_avg_sq") if group["amsgrad"] else None
+                if group["amsgrad"] and vmax is None:
+                    vmax = torch.zeros_like(fg.master)
+                steps = [by_param[p]["step"] for p in fg.params if p in by_param and "step" in by_param[p]]
+                step = torch.zeros(1, device=fg.master.device)
+                if steps:
+                    step.fill_(float(torch.as_tensor(steps[0]).reshape(-1)[0]))
+                st = {"m": m, "v": v if v is not None else torch.zeros_like(fg.master), "vmax": vmax, "step": step}
+                self._flat_state[id(fg)] = st
+                for i, p in enumerate(fg.params):
+                    self.state[p]["exp_avg"] = fg._view(st["m"], i)
+                    self.state[p]["exp_avg_sq"] = fg._view(st["v"], i)
+                    self.state[p]["step"] = st["step"]
+                    if vmax is not None:
+                        self.state[p]["max_exp_avg_sq"] = fg._view(vmax, i)
+            for p in singles:
+                sv = by_param.get(p)
+                if not sv:
+                    continue
+                st = self.state[p]
+                for k in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"):
+                    if k in sv:
+                        st[k] = sv[k].to(p.device, torch.float32).reshape(p.shape).clone()
+                if "step" in sv:
+                    st["step"] = (torch.zeros(1, device=p.device) if p.is_cuda else torch.zeros(())).fill_(
+                        float(torch.as_tensor(sv["step"]).reshape(-1)[0]))
 
 
 def build_optimizer(name: str, params, **kw) -> torch.optim.Optimizer:

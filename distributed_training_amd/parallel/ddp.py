@@ -209,6 +209,12 @@ class DistributedDataParallel(nn.Module):
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.flat.zero_grad(set_to_none)
 
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global-norm clip of the (all-reduced, replicated) flat gradient."""
+        from .flat import clip_flat_grad_norm_
+
+        return clip_flat_grad_norm_(self.flat, max_norm)
+
     # ------------------------------------------------------------ state
     def state_dict(self, *args, **kwargs):
         sd = super().state_dict(*args, **kwargs)

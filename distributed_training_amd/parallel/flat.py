@@ -178,6 +178,35 @@ class FlatParamGroup:
         return buckets
 
 
+@torch.no_grad()
+def clip_flat_grad_norm_(fg: FlatParamGroup, max_norm: float, comm=None, sharded: bool = False) -> torch.Tensor:
+    """Global-norm gradient clipping over ONE flat gradient buffer (what
+    ``torch.nn.utils.clip_grad_norm_`` computes over the module's parameters).
+
+    ``sharded``: the buffer holds this rank's shard only (FSDP), so the squared
+    norm is all-reduced (sum) over ``comm`` before the coefficient is formed --
+    every rank then scales its shard by the SAME coefficient.  Replicated
+    buffers (DDP after the all-reduce) need no collective.  No host sync: the
+    coefficient stays on the device.  Padding between parameters is zero and
+    does not change the norm.  Returns the total norm (0-dim tensor)."""
+    if not fg.prepare_grads_for_step():
+        return torch.zeros((), device=fg.grad.device)
+    g = fg.grad
+    if g.is_cuda and g.dtype == torch.float32:
+        from ..ops import native
+
+        sq = torch.zeros(1, dtype=torch.float32, device=g.device)
+        native().flat_sumsq(g, sq, -1)
+    else:
+        sq = g.float().pow(2).sum().reshape(1)
+    if sharded and comm is not None and comm.world_size > 1:
+        comm.all_reduce(sq, op="sum")
+    norm = sq.sqrt()
+    coef = (float(max_norm) / (norm + 1e-6)).clamp(max=1.0)
+    g.mul_(coef.to(g.dtype))
+    return norm.reshape(())
+
+
 def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]], device: torch.device,
                      param_dtype=torch.float32, grad_dtype=None, reverse: bool = True) -> FlatParamGroup:
     items = list(params_with_names)

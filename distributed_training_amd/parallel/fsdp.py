@@ -432,6 +432,14 @@ class FullyShardedDataParallel(nn.Module):
             self._grad_fresh = False
         self.shards.zero_grad(set_to_none)
 
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global-norm clip across the shards (torch FSDP's ``clip_grad_norm_``): the
+        squared norms of every rank's gradient shard are all-reduced before the
+        coefficient is formed, so all ranks scale by the same factor."""
+        from .flat import clip_flat_grad_norm_
+
+        return clip_flat_grad_norm_(self.shards, max_norm, comm=self.comm, sharded=True)
+
     # ------------------------------------------------------------ state dict
     @torch.no_grad()
     def full_state_dict(self, rank0_only: bool = True, offload_to_cpu: bool = True) -> Dict[str, torch.Tensor]:
@@ -481,6 +489,69 @@ class FullyShardedDataParallel(nn.Module):
         if strict and missing:
             raise RuntimeError(f"FSDP.load_state_dict: missing keys {missing}")
         return None
+
+    # ------------------------------------------------------------ optimizer state
+    _OPT_FORMAT = "dta_fsdp_full_optim_v1"
+
+    @torch.no_grad()
+    def full_optim_state_dict(self, optimizer, rank0_only: bool = True) -> Dict:
+        """Collective: the optimizer state of the WHOLE model, keyed by original
+        parameter names (world-size independent, like ``FULL_STATE_DICT``).  Each
+        shard-sized state tensor (momentum, Adam moments) is all-gathered per unit
+        and cut into per-parameter tensors; scalars (step) are taken as they are."""
+        keep = (not rank0_only) or self.rank == 0
+        out_state: Dict[str, Dict] = {}
+        for u in self.units:
+            st = optimizer.state.get(u.shard_param, {})
+            # identical key order on every rank (the gathers are collectives)
+            for k in sorted(st):
+                v = st[k]
+                if isinstance(v, torch.Tensor) and v.numel() == u.shard_size:
+                    full = torch.empty(u.total, dtype=torch.float32, device=self.device)
+                    self.comm.all_gather_into(full, v.reshape(-1).float().contiguous())
+                    if keep:
+                        for (_, _, name, _), o, n, shp in zip(u.entries, u.offsets, u.numels, u.shapes):
+                            out_state.setdefault(name, {})[k] = full[o:o + n].view(shp).cpu().clone()
+                elif keep:
+                    for _, _, name, _ in u.entries:
+                        out_state.setdefault(name, {})[k] = v.detach().cpu().clone() if isinstance(
+                            v, torch.Tensor) else v
+        if not keep:
+            return {}
+        groups = [{k: v for k, v in g.items() if k != "params"} for g in optimizer.param_groups]
+        return {"format": self._OPT_FORMAT, "state": out_state, "param_groups": groups}
+
+    @torch.no_grad()
+    def load_full_optim_state_dict(self, optimizer, osd: Dict) -> None:
+        """Inverse of :meth:`full_optim_state_dict` on any world size: every rank
+        rebuilds each unit's flat state from the per-parameter tensors and keeps its
+        shard, then hands the optimizer a local state dict of its shard params."""
+        if osd.get("format") != self._OPT_FORMAT:
+            raise ValueError("not a full FSDP optimizer state dict")
+        state = osd["state"]
+        pid = {id(p): i for i, p in enumerate(p for g in optimizer.param_groups for p in g["params"])}
+        local: Dict[int, Dict] = {}
+        for u in self.units:
+            names = [name for _, _, name, _ in u.entries]
+            keys = sorted({k for name in names for k in state.get(name, {})})
+            if not keys or id(u.shard_param) not in pid:
+                continue
+            ent = {}
+            for k in keys:
+                vals = [state.get(name, {}).get(k) for name in names]
+                if all(isinstance(v, torch.Tensor) and v.numel() == n for v, n in zip(vals, u.numels)):
+                    full = torch.zeros(u.total, dtype=torch.float32, device=self.device)
+                    for v, o, n in zip(vals, u.offsets, u.numels):
+                        full[o:o + n].copy_(v.reshape(-1).to(self.device, torch.float32))
+                    ent[k] = full[self.rank * u.shard_size:(self.rank + 1) * u.shard_size].clone()
+                else:
+                    ent[k] = next(v for v in vals if v is not None)
+            local[pid[id(u.shard_param)]] = ent
+        groups, i = [], 0
+        for g, sg in zip(optimizer.param_groups, osd["param_groups"]):
+            groups.append(dict(sg, params=list(range(i, i + len(g["params"])))))
+            i += len(g["params"])
+        optimizer.load_state_dict({"state": local, "param_groups": groups})
 
     def unit_summary(self) -> List[Dict[str, int]]:
         return [{"unit": u.index, "params": len(u.entries), "numel": sum(u.numels), "padded": u.total,

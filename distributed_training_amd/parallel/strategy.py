@@ -61,6 +61,14 @@ class DistributedStrategy(ABC):
         """State dict to checkpoint; called on ALL ranks."""
         return model.state_dict()
 
+    def optim_state(self, model: Module, optimizer) -> Dict[str, Any]:
+        """Optimizer state to checkpoint; called on ALL ranks (replicated engines:
+        every rank holds the complete state)."""
+        return optimizer.state_dict()
+
+    def load_optim_state(self, model: Module, optimizer, osd: Dict[str, Any]) -> None:
+        optimizer.load_state_dict(osd)
+
 
 class DDPStrategy(DistributedStrategy):
     def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
@@ -113,6 +121,14 @@ class FSDPStrategy(DistributedStrategy):
     def model_state(self, model: Module) -> Dict[str, torch.Tensor]:
         # FULL_STATE_DICT, offload_to_cpu=True, rank0_only=True (fsdp_strategy.py:31-35) -- on all ranks
         return model.full_state_dict(rank0_only=True, offload_to_cpu=True)
+
+    def optim_state(self, model: Module, optimizer) -> Dict[str, Any]:
+        # each rank holds only its shards' state: gathered per unit into a full,
+        # world-size independent state keyed by parameter name (collective)
+        return model.full_optim_state_dict(optimizer, rank0_only=True)
+
+    def load_optim_state(self, model: Module, optimizer, osd: Dict[str, Any]) -> None:
+        model.load_full_optim_state_dict(optimizer, osd)
 
     def save_checkpoint(self, model: Module, state_dict: dict, path: str) -> None:
         from ..engine.checkpoint import atomic_torch_save

@@ -169,6 +169,43 @@ def test_native_fsdp_world(ws):
     run_gloo(_fsdp_ws, ws)
 
 
+def _clip_parity(rank, ws, strategy):
+    """Global-norm clipping: each rank's shard (FSDP) / replica (DDP) scaled by the
+    coefficient of the WHOLE gradient, as torch's clip_grad_norm_ on one process."""
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    ref = Net()
+    m = copy.deepcopy(ref)
+    if strategy == "fsdp":
+        w = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={Block})
+    else:
+        w = DistributedDataParallel(m, TorchComm())
+    g = torch.Generator().manual_seed(3)
+    X, Y = torch.randn(8 * ws, 20, generator=g), torch.randn(8 * ws, 1, generator=g)
+    F.mse_loss(ref(X), Y).backward()
+    F.mse_loss(w(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+    want = torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.05)
+    got = w.clip_grad_norm_(0.05)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    assert float(want) > 0.05  # the clip is active
+    o1 = torch.optim.SGD(ref.parameters(), lr=1.0)
+    o2 = torch.optim.SGD(w.parameters(), lr=1.0)
+    o1.step()
+    o2.step()
+    sd = w.full_state_dict(rank0_only=False) if strategy == "fsdp" else {
+        k[len("module."):]: v for k, v in w.state_dict().items()}
+    for k, v in ref.state_dict().items():
+        torch.testing.assert_close(sd[k], v, rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("strategy", ["fsdp", "ddp"])
+def test_clip_grad_norm_global(strategy):
+    run_gloo(_clip_parity, 2, strategy)
+
+
 def _comm_ops(rank, ws):
     from distributed_training_amd.parallel.comm import TorchComm
 
@@ -265,3 +302,62 @@ def _fsdp_tied(rank, ws):
 
 def test_native_fsdp_tied_weights_gpt2():
     run_gloo(_fsdp_tied, 2)
+
+
+def _resume_parity(rank, ws, strategy, opt_name, tmpdir):
+    """Checkpoint with OPTIM_STATE mid-training, resume into fresh engine + optimizer:
+    the continued run matches an uninterrupted one (momentum / Adam moments and
+    step restored; FSDP's per-rank shards gathered and re-sharded)."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.engine.checkpoint import ModelCheckpoint
+    from distributed_training_amd.ops.optim import FusedAdamW, FusedSGD
+    from distributed_training_amd.parallel.strategy import DDPStrategy, FSDPStrategy
+
+    class Env:
+        global_rank = rank
+
+        @staticmethod
+        def barrier():
+            dist.barrier()
+
+    def make():
+        torch.manual_seed(0)
+        strat = FSDPStrategy(False, wrap_policy={Block}) if strategy == "fsdp" else DDPStrategy(0, False)
+        w = strat.prepare_model(Net(), torch.device("cpu"))
+        o = FusedAdamW(w.parameters(), lr=1e-2) if opt_name == "adamw" else FusedSGD(w.parameters(), lr=0.1,
+                                                                                        momentum=0.9)
+        return strat, w, o
+
+    def steps(w, o, its):
+        for it in its:
+            g = torch.Generator().manual_seed(200 + it)
+            X, Y = torch.randn(8 * ws, 20, generator=g), torch.randn(8 * ws, 1, generator=g)
+            o.zero_grad()
+            F.mse_loss(w(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+            o.step()
+
+    def state(strat, w):
+        return strat.model_state(w) if strategy == "fsdp" else w.state_dict()
+
+    strat, w, o = make()
+    steps(w, o, range(6))
+    want = state(strat, w)
+    strat, w, o = make()
+    steps(w, o, range(3))
+    ck = ModelCheckpoint(f"{tmpdir}/snap.pt", Env, strat, save_optimizer=True)
+    ck.save(w, 3, o)
+    strat2, w2, o2 = make()
+    w2, ep = ck.load(w2, "cpu", o2)
+    assert ep == 3
+    steps(w2, o2, range(3, 6))
+    got = state(strat2, w2)
+    if rank == 0 or strategy == "ddp":
+        for k in want:
+            torch.testing.assert_close(got[k], want[k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("strategy,opt_name", [("fsdp", "adamw"), ("fsdp", "sgd"), ("ddp", "adamw"),
+                                               ("ddp", "sgd")])
+def test_resume_restores_optimizer_state(strategy, opt_name, tmp_path):
+    run_gloo(_resume_parity, 2, strategy, opt_name, str(tmp_path))
