@@ -150,7 +150,10 @@ def main():
     nb = data.shape[0] // args.batch
     state = {"i": 0, "loss": None}
 
+    from distributed_training_amd.utils import profiling as prof
+
     def step():
+        prof.push("step")
         i = state["i"] % nb
         state["i"] += 1
         xb = data[i * args.batch:(i + 1) * args.batch]
@@ -162,10 +165,14 @@ def main():
         elif args.impl == "torch":
             loss = loss_fn(wrapped(xb[:, :-1]), xb[:, 1:])
         else:  # LM head + loss fused inside the model
-            loss = wrapped(xb[:, :-1], xb[:, 1:])
-        loss.backward()
-        opt.step()
+            with prof.range_("forward"):
+                loss = wrapped(xb[:, :-1], xb[:, 1:])
+        with prof.range_("backward"):
+            loss.backward()
+        with prof.range_("optimizer"):
+            opt.step()
         state["loss"] = loss
+        prof.pop()
 
     def dbarrier():
         if dist.get_backend() == "nccl":

@@ -38,6 +38,7 @@ from torch.utils.data import DataLoader
 from ..parallel.env import DistributedEnvironment
 from ..parallel.sampler import DistributedSampler as DtaSampler
 from ..parallel.strategy import DDPStrategy, DistributedStrategy, FSDPStrategy, default_comm
+from ..utils import profiling as prof
 from .checkpoint import ModelCheckpoint
 
 logger = logging.getLogger("distributed_training_amd.trainer")
@@ -174,19 +175,24 @@ class Trainer:
 
     # ------------------------------------------------------------------ loop
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        # roctx ranges (DTA_ROCTX=1): step phases on the rocprofv3 --marker-trace timeline
         self.optimizer.zero_grad()
-        if self.config.loss == "lm":  # transformer LMs fuse the head and the loss (models/gpt2.py, llama.py)
-            loss = self.model(source, targets)
-        else:
-            output = self.model(source)
-            loss = self._loss_fn(output, targets)
-        loss.backward()
-        if self.config.grad_clip:
-            if hasattr(self.model, "clip_grad_norm_"):  # native engines: global norm over the flat (sharded) grads
-                self.model.clip_grad_norm_(self.config.grad_clip)
+        with prof.range_("forward"):
+            if self.config.loss == "lm":  # transformer LMs fuse the head and the loss (models/gpt2.py, llama.py)
+                loss = self.model(source, targets)
             else:
-                torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.grad_clip)
-        self.optimizer.step()
+                output = self.model(source)
+                loss = self._loss_fn(output, targets)
+        with prof.range_("backward"):
+            loss.backward()
+        if self.config.grad_clip:
+            with prof.range_("clip_grad_norm"):
+                if hasattr(self.model, "clip_grad_norm_"):  # native engines: global norm over the flat (sharded) grads
+                    self.model.clip_grad_norm_(self.config.grad_clip)
+                else:
+                    torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.grad_clip)
+        with prof.range_("optimizer"):
+            self.optimizer.step()
         return loss
 
     def _batch_size_for_log(self) -> int:

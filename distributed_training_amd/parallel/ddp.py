@@ -45,6 +45,7 @@ import torch
 import torch.nn as nn
 from torch.autograd import Variable
 
+from ..utils import profiling as prof
 from .comm import Communicator, TorchComm
 from .flat import FlatParamGroup, build_flat_group
 
@@ -160,6 +161,10 @@ class DistributedDataParallel(nn.Module):
         return len(ids) == len(self.buckets[b].param_ids)
 
     def _launch(self, b: int) -> None:
+        with prof.range_(f"ddp.bucket{b}.allreduce"):  # host enqueue; the collective runs on the comm stream
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b: int) -> None:
         bk = self.buckets[b]
         sl = self.flat.grad[bk.start:bk.end]
         prescale = self.world_size > 1 and not self.comm.supports_avg()
@@ -177,6 +182,10 @@ class DistributedDataParallel(nn.Module):
         return len(self._pending[b]) == len(self.buckets[b].param_ids)
 
     def _finalize(self) -> None:
+        with prof.range_("ddp.finalize"):
+            self._finalize_impl()
+
+    def _finalize_impl(self) -> None:
         # unused parameters: their (zeroed) grads still take part, in bucket order
         for b in range(self._next, len(self.buckets)):
             for i in self.buckets[b].param_ids:

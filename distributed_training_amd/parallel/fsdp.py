@@ -39,6 +39,7 @@ import torch
 import torch.nn as nn
 from torch.autograd import Variable
 
+from ..utils import profiling as prof
 from .comm import CommWork, Communicator, TorchComm
 from .flat import FlatParamGroup
 
@@ -138,7 +139,8 @@ class _Unit:
             self.gathered = True
             return
         self._alloc()
-        work = self.owner.comm.all_gather_into(self.full.data, self.shard_source(), async_op=True)
+        with prof.range_(f"fsdp.unit{self.index}.allgather"):
+            work = self.owner.comm.all_gather_into(self.full.data, self.shard_source(), async_op=True)
         self.pending = work
         if not async_op:
             self.wait()
@@ -182,7 +184,8 @@ class _Unit:
             op = "avg" if own.comm.supports_avg() else "sum"
             if op == "sum":
                 g.div_(own.world_size)
-            work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
+            with prof.range_(f"fsdp.unit{self.index}.reduce_scatter"):
+                work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
             own._pending_rs.append((self, work, out, g))
         self.in_backward = False
         if not self.is_root or own.reshard_root_after_backward:
@@ -382,6 +385,10 @@ class FullyShardedDataParallel(nn.Module):
             self._cb_queued = True
 
     def _finalize_backward(self) -> None:
+        with prof.range_("fsdp.finalize"):
+            self._finalize_backward_impl()
+
+    def _finalize_backward_impl(self) -> None:
         fg = self.shards
         fresh = self._grad_fresh
         done: Set[int] = set()

@@ -22,7 +22,9 @@ def _load_roctx():
     global _roctx
     if _roctx is not None:
         return _roctx if _roctx else None
-    for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+    # rocprofiler-sdk's roctx first: rocprofv3 --marker-trace intercepts that one
+    for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so",
+                 "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
         try:
             lib = ctypes.CDLL(name)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
@@ -37,26 +39,60 @@ def _load_roctx():
     return None
 
 
+_ENABLED: Optional[bool] = None
+
+
 def enabled() -> bool:
-    return os.environ.get("DTA_ROCTX", "0") == "1" and _load_roctx() is not None
+    """``DTA_ROCTX=1`` and libroctx64 loadable (read once per process: the ranges sit on
+    per-bucket / per-unit hot paths, so a disabled range costs one global lookup)."""
+    global _ENABLED
+    if _ENABLED is None:
+        _ENABLED = os.environ.get("DTA_ROCTX", "0") == "1" and _load_roctx() is not None
+    return _ENABLED
 
 
-@contextlib.contextmanager
+def set_enabled(on: bool) -> None:
+    global _ENABLED
+    _ENABLED = bool(on) and _load_roctx() is not None
+
+
+class _Range:
+    __slots__ = ("name",)
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        _roctx.roctxRangePushA(self.name.encode())
+        return self
+
+    def __exit__(self, *exc):
+        _roctx.roctxRangePop()
+        return False
+
+
+_NULL = contextlib.nullcontext()
+
+
 def range_(name: str):
-    lib = _load_roctx() if os.environ.get("DTA_ROCTX", "0") == "1" else None
-    if lib is not None:
-        lib.roctxRangePushA(name.encode())
-    try:
-        yield
-    finally:
-        if lib is not None:
-            lib.roctxRangePop()
+    """Context manager: a named roctx range around host work (enqueue of kernels /
+    collectives); a shared no-op context when tracing is off."""
+    return _Range(name) if enabled() else _NULL
+
+
+def push(name: str) -> None:
+    if enabled():
+        _roctx.roctxRangePushA(name.encode())
+
+
+def pop() -> None:
+    if enabled():
+        _roctx.roctxRangePop()
 
 
 def mark(name: str) -> None:
-    lib = _load_roctx() if os.environ.get("DTA_ROCTX", "0") == "1" else None
-    if lib is not None:
-        lib.roctxMarkA(name.encode())
+    if enabled():
+        _roctx.roctxMarkA(name.encode())
 
 
 class StepTimer:
