@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--impl", choices=["fused", "generic", "torch"], default="fused")
+    ap.add_argument("--model", choices=["mlp2", "linear"], default="mlp2",
+                    help="linear: the reference's default nn.Linear(20, 1) + cross-entropy, fp32 (not the headline)")
     ap.add_argument("--hidden", type=int, default=512)
     ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
     ap.add_argument("--dataset-size", type=int, default=2048)
@@ -123,6 +125,43 @@ def run_fused(args, dev, ws):
     form = ("persistent" + (f"/{prog.xmode}" if ws > 1 else "")) if prog.persistent else "per-step"
     finish.info = {"step_form": form,
                    "calibration_ms": getattr(prog, "exchange_times_ms", None)}
+    return step_fn, finish, comm
+
+
+def run_fused_linear(args, dev, ws):
+    """The reference's default workload (src/distributed_trainer.py:160-165, 199-200):
+    nn.Linear(20, 1), F.cross_entropy on float targets, fp32, SGD, DDP -- on the fused
+    Linear step program (csrc/linear_step.hip)."""
+    import torch
+
+    from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
+    from distributed_training_amd.engine.fused_linear import FusedLinearProgram, linear_eligible
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import make_comm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.sampler import DistributedSampler
+
+    torch.manual_seed(0)
+    ds = MyTrainDataset(args.dataset_size, 20, 1, seed=0)
+    model = torch.nn.Linear(20, 1).to(dev)
+    rank = int(os.environ.get("RANK", "0"))
+    loader = DeviceDataLoader(ds, args.batch, sampler=DistributedSampler(ds, num_replicas=ws, rank=rank), device=dev)
+    comm = make_comm(dev)
+    ddp = DistributedDataParallel(model, comm=comm, device=dev)
+    opt = FusedSGD(ddp.parameters(), lr=args.lr)
+    why = linear_eligible(model, opt, loader, "cross_entropy", dev)
+    if why:
+        raise SystemExit(f"fused Linear path not applicable: {why}")
+    prog = FusedLinearProgram(model, opt, loader, comm, loss="cross_entropy")
+
+    def step_fn(n):
+        prog.run_steps(n)
+
+    def finish():
+        prog.store_to_module()
+        return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
+
+    finish.info = {"step_form": "persistent" if ws == 1 else "per-step graph"}
     return step_fn, finish, comm
 
 
@@ -229,6 +268,10 @@ def main():
 
     rank, ws, dev = setup_dist(args)
     runner = {"fused": run_fused, "generic": run_generic, "torch": run_torch}[args.impl]
+    if args.model == "linear":
+        if args.impl != "fused":
+            raise SystemExit("--model linear: only --impl fused")
+        runner = run_fused_linear
     step_fn, finish, comm = runner(args, dev, ws)
 
     def dbarrier():
@@ -277,13 +320,14 @@ def main():
         "ms_per_step": round(elapsed / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / base, 3) if base else None,
-        "dtype": "bf16",
+        "vs_baseline": round(value / base, 3) if base and args.model == "mlp2" else None,
+        "dtype": "bf16" if args.model == "mlp2" else "fp32",
         "data": "synthetic (reference MyTrainDataset: 2048 x (rand(20), rand(1)), DistributedSampler order)",
-        "config": {"model": f"mlp2 Linear(20,{args.hidden})-ReLU-Linear({args.hidden},1)",
+        "config": {"model": f"mlp2 Linear(20,{args.hidden})-ReLU-Linear({args.hidden},1)" if args.model == "mlp2"
+                   else "linear nn.Linear(20,1) (reference default)",
                    "global_batch": args.batch * ws, "seq_len": None, "parallelism": f"dp{ws}",
-                   "per_gpu_batch": args.batch, "optimizer": "SGD(lr=1e-3)", "loss": "mse",
-                   "impl": args.impl},
+                   "per_gpu_batch": args.batch, "optimizer": "SGD(lr=1e-3)",
+                   "loss": "mse" if args.model == "mlp2" else "cross_entropy", "impl": args.impl},
         "final_loss": last_loss,
     }
     if getattr(args, "shared_gpu", False):

@@ -1042,7 +1042,10 @@ std::shared_ptr<MlpPersistentLaunch> mlp_persistent_prepare(
   return L;
 }
 
+void dta_register_ext(pybind11::module_& m);
+
 PYBIND11_MODULE(_C, m) {
+  dta_register_ext(m);
   m.doc() = "distributed_training_amd native runtime (gfx950 HIP kernels + RCCL communicator)";
   m.def("flat_sgd", &flat_sgd);
   m.def("flat_adam", &flat_adam);

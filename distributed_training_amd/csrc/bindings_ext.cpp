@@ -1,0 +1,194 @@
+// Python bindings, second translation unit: the reference-default Linear step
+// program and the general bf16 GEMM family (registered into the same _C
+// module by dta_register_ext, called from bindings.cpp).
+//
+// As in bindings.cpp, every entry point checks device / dtype / contiguity /
+// shape on the host before enqueueing, so a bad call raises in Python
+// instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace dta {
+struct LinStepArgs {
+  const float* X;
+  const float* T;
+  const int* ring;
+  const int* counts;
+  int* cursor;
+  float* P;
+  float* M;
+  int* flags;
+  const float* G_in;
+  float* G_out;
+  float* loss_ring;
+  int* loss_cursor;
+  int loss_len;
+  int R, B, I, C, nsteps, loss_kind;
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, maximize;
+};
+}  // namespace dta
+
+hipError_t dta_linear_step(const dta::LinStepArgs*, hipStream_t);
+int dta_gemm_bf16_tile(int, int, int, int);
+hipError_t dta_gemm_bf16(const void*, int64_t, bool, const void*, int64_t, bool, void*, float*, int64_t, int, int, int,
+                         float, const void*, int, const void*, int64_t, int, hipStream_t);
+size_t dta_linear_step_lds_bytes(int, int, int, int);
+int dta_linear_step_supported(int, int, int, int);
+
+namespace {
+
+hipStream_t stream_of(int64_t s) {
+  if (s == -1) return c10::hip::getCurrentHIPStream().stream();
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+void ok(hipError_t e, const char* what) { TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e)); }
+
+void gpu_contig(const torch::Tensor& t, const char* name, c10::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has the wrong dtype");
+}
+
+bool has(const c10::optional<torch::Tensor>& t) { return t.has_value() && t->defined(); }
+
+void linear_step(torch::Tensor X, torch::Tensor T, torch::Tensor ring, torch::Tensor counts, torch::Tensor cursor,
+                 torch::Tensor P, c10::optional<torch::Tensor> M, torch::Tensor flags,
+                 c10::optional<torch::Tensor> G_in, c10::optional<torch::Tensor> G_out, torch::Tensor loss_ring,
+                 torch::Tensor loss_cursor, int64_t nsteps, int64_t loss_kind, double lr, double momentum,
+                 double dampening, double wd, double grad_scale, bool nesterov, bool maximize, int64_t stream) {
+  gpu_contig(X, "X", torch::kFloat32);
+  gpu_contig(T, "T", torch::kFloat32);
+  gpu_contig(ring, "ring", torch::kInt32);
+  gpu_contig(counts, "counts", torch::kInt32);
+  gpu_contig(cursor, "cursor", torch::kInt32);
+  gpu_contig(P, "P", torch::kFloat32);
+  gpu_contig(flags, "flags", torch::kInt32);
+  gpu_contig(loss_ring, "loss_ring", torch::kFloat32);
+  gpu_contig(loss_cursor, "loss_cursor", torch::kInt32);
+  TORCH_CHECK(X.dim() == 2 && T.dim() == 2 && X.size(0) == T.size(0), "X [N, I] and T [N, C]");
+  TORCH_CHECK(ring.dim() == 2 && counts.numel() == ring.size(0), "ring [R, B], counts [R]");
+  const int I = (int)X.size(1), C = (int)T.size(1), B = (int)ring.size(1);
+  const int64_t np = (int64_t)C * I + C;
+  TORCH_CHECK(P.numel() == np, "P must hold C*I + C parameters");
+  TORCH_CHECK(dta_linear_step_supported(I, C, B, has(M)), "linear_step: shape outside the kernel's limits");
+  TORCH_CHECK(nsteps >= 0 && loss_kind >= 0 && loss_kind <= 1, "linear_step: bad nsteps / loss");
+  TORCH_CHECK(cursor.numel() >= 1 && flags.numel() >= 2 && loss_cursor.numel() >= 1 && loss_ring.numel() >= 1,
+              "linear_step: empty state tensor");
+  if (has(M)) {
+    gpu_contig(*M, "M", torch::kFloat32);
+    TORCH_CHECK(M->numel() == np, "M size");
+  }
+  if (has(G_in)) {
+    gpu_contig(*G_in, "G_in", torch::kFloat32);
+    TORCH_CHECK(G_in->numel() == np, "G_in size");
+  }
+  if (has(G_out)) {
+    gpu_contig(*G_out, "G_out", torch::kFloat32);
+    TORCH_CHECK(G_out->numel() == np, "G_out size");
+  }
+  // indices must address rows of X: checked where they are uploaded (host side, FusedLinearProgram)
+  dta::LinStepArgs a{};
+  a.X = X.data_ptr<float>();
+  a.T = T.data_ptr<float>();
+  a.ring = ring.data_ptr<int>();
+  a.counts = counts.data_ptr<int>();
+  a.cursor = cursor.data_ptr<int>();
+  a.P = P.data_ptr<float>();
+  a.M = has(M) ? M->data_ptr<float>() : nullptr;
+  a.flags = flags.data_ptr<int>();
+  a.G_in = has(G_in) ? G_in->data_ptr<float>() : nullptr;
+  a.G_out = has(G_out) ? G_out->data_ptr<float>() : nullptr;
+  a.loss_ring = loss_ring.data_ptr<float>();
+  a.loss_cursor = loss_cursor.data_ptr<int>();
+  a.loss_len = (int)loss_ring.numel();
+  a.R = (int)ring.size(0);
+  a.B = B;
+  a.I = I;
+  a.C = C;
+  a.nsteps = (int)nsteps;
+  a.loss_kind = (int)loss_kind;
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.weight_decay = (float)wd;
+  a.grad_scale = (float)grad_scale;
+  a.nesterov = nesterov;
+  a.maximize = maximize;
+  ok(dta_linear_step(&a, stream_of(stream)), "linear_step");
+}
+
+bool aligned16(const torch::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
+
+// C[M, N] = alpha * op(A) op(B)^T (+ bias, act, + residual).  a: [M, K] (a_t: [K, M]); b: [N, K] (b_t: [K, N]);
+// both bf16 with unit inner stride, row strides multiples of 8 elements.
+torch::Tensor gemm_bf16(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t, c10::optional<torch::Tensor> out,
+                        bool out_f32, double alpha, c10::optional<torch::Tensor> bias, int64_t act,
+                        c10::optional<torch::Tensor> residual, int64_t tile, int64_t stream) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm: GPU tensors");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm: bf16 operands");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, unit inner stride");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && aligned16(a) && aligned16(b),
+              "gemm: row strides multiples of 8 elements, 16-byte aligned bases");
+  const int64_t M = a_t ? a.size(1) : a.size(0), K = a_t ? a.size(0) : a.size(1);
+  const int64_t N = b_t ? b.size(1) : b.size(0), Kb = b_t ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: inner dimensions differ");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm: dims too large");
+  TORCH_CHECK(dta_gemm_bf16_tile((int)M, (int)N, (int)K, (int)tile) != 0,
+              "gemm: shape not covered (M, N multiples of the tile, K a multiple of 32)");
+  TORCH_CHECK(act == 0 || act == 2, "gemm: act 0 (none) or 2 (gelu_tanh)");
+  torch::Tensor c;
+  if (out && out->defined()) {
+    c = *out;
+    TORCH_CHECK(c.is_cuda() && c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 &&
+                    c.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
+                "gemm: out must be [M, N], unit inner stride, 16-byte aligned rows");
+    TORCH_CHECK(c.scalar_type() == (out_f32 ? torch::kFloat32 : torch::kBFloat16), "gemm: out dtype");
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  }
+  const void* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() &&
+                    bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  if (residual && residual->defined()) {
+    TORCH_CHECK(!out_f32, "gemm: residual with bf16 output only");
+    TORCH_CHECK(residual->is_cuda() && residual->scalar_type() == torch::kBFloat16 && residual->dim() == 2 &&
+                    residual->size(0) == M && residual->size(1) == N && residual->stride(1) == 1 &&
+                    residual->stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(residual->data_ptr()) % 8 == 0,
+                "gemm: residual bf16 [M, N]");
+    rp = residual->data_ptr();
+    ldr = residual->stride(0);
+  }
+  ok(dta_gemm_bf16(a.data_ptr(), a.stride(0), a_t, b.data_ptr(), b.stride(0), b_t, out_f32 ? nullptr : c.data_ptr(),
+                   out_f32 ? c.data_ptr<float>() : nullptr, c.stride(0), (int)M, (int)N, (int)K, (float)alpha, bp,
+                   (int)act, rp, ldr, (int)tile, stream_of(stream)),
+     "gemm_bf16");
+  return c;
+}
+
+}  // namespace
+
+void dta_register_ext(pybind11::module_& m) {
+  namespace py = pybind11;
+  m.def("linear_step", &linear_step, py::arg("X"), py::arg("T"), py::arg("ring"), py::arg("counts"),
+        py::arg("cursor"), py::arg("P"), py::arg("M"), py::arg("flags"), py::arg("G_in"), py::arg("G_out"),
+        py::arg("loss_ring"), py::arg("loss_cursor"), py::arg("nsteps"), py::arg("loss_kind"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
+        py::arg("maximize"), py::arg("stream") = -1);
+  m.def("gemm", &gemm_bf16, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
+        py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0, py::arg("bias") = py::none(),
+        py::arg("act") = 0, py::arg("residual") = py::none(), py::arg("tile") = 0, py::arg("stream") = -1);
+  m.def("gemm_tile", [](int M, int N, int K, int tile) { return dta_gemm_bf16_tile(M, N, K, tile); },
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
+  m.def("linear_step_supported", [](int I, int C, int B, bool mom) { return dta_linear_step_supported(I, C, B, mom) != 0; });
+}

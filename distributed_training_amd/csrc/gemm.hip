@@ -230,22 +230,6 @@ struct GemmGdArgs {
   int cs_workers, gemm_wgs;
 };
 
-// One global_load_lds_dwordx4: 64 lanes x 16 B from per-lane `gsrc` to the
-// wave-uniform LDS address `lds_base` + 16 * lane.  Inline asm, not the
-// builtin: with the builtin hipcc treats the DMA as a pending write to the
-// LDS array and waits vmcnt(0) before the next ds_read of ANY buffer, which
-// serialises the stage loads with the multiply.  The asm load is invisible to
-// hipcc's counters: the kernel counts them itself (vm_wait below).
-__device__ __forceinline__ void glds16(const void* gsrc, char* lds_base) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_base);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(dst)
-               : "memory");
-}
-
 // wait until at most 4 * `stages` of this wave's LDS-DMA loads are outstanding
 __device__ __forceinline__ void vm_wait(int stages) {
   if (stages >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");

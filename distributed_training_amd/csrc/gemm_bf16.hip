@@ -1,0 +1,311 @@
+// General bf16 GEMM for gfx950 with fused epilogues: the transformer
+// projections' forward (y = x W^T + b [, GELU] [, + residual]), input
+// gradient (dx = dy W) and weight gradient (dW = dy^T x) -- SURVEY.md N07, the
+// GEMMs of nn.Linear at src/distributed_trainer.py:162,164 scaled up to the
+// GPT-2 / Llama configs.
+//
+//   C[M, N] = alpha * sum_k A(m, k) B(n, k)   (+ bias[n], act, + R[m, n])
+//
+// Operand storage, both bf16 row-major:
+//   A: K-major [M][K] (lda)  or  M-major [K][M] (A_T)
+//   B: K-major [N][K] (ldb)  or  N-major [K][N] (B_T)
+// forward  y = x W^T : A = x [T][K],  B = W [N][K]          (A_T = 0, B_T = 0)
+// dgrad   dx = dy W  : A = dy [T][N], B = W [N][K] as [k][n] (A_T = 0, B_T = 1)
+// wgrad   dW = dy^T x: A = dy [T][N] as [k][m], B = x as [k][n] (A_T = 1, B_T = 1)
+//
+// Structure (cdna_hip_programming.md §5): a BM x BN tile per workgroup of 8
+// waves (2 x 4), each wave (BM/2) x (BN/4) on v_mfma_f32_16x16x32_bf16; the
+// k loop streams 32-deep stages by global_load_lds_dwordx4 (LDS-DMA, no
+// staging VGPRs) into a 4-deep LDS ring, so three stages are in flight while
+// one is multiplied; the wait before each barrier is a counted vmcnt (never 0
+// inside the loop) and the barrier is a raw s_barrier, so the DMA of later
+// stages spans it.
+//
+// LDS images (all lane-linear for the DMA; the XOR swizzle is applied to the
+// per-lane SOURCE address and undone on the read, rule 21):
+//  * K-major operand: [rows][32] bf16 = 64-B rows, 16-B chunk c of row r at
+//    physical chunk c ^ 3*((r >> 3) & 1).  A fragment read (ds_read_b128, lane
+//    l: row l & 15, chunk l >> 4) then hits 16 distinct 16-B bank slots in each
+//    of the instruction's four 16-lane bank groups: conflict-free.
+//  * M/N-major operand: [32 k][W] bf16 (rows of 2W bytes), chunk c of row k at
+//    c ^ 2*((k & 3) | ((k >> 3) & 1) << 2).  Fragments come from
+//    ds_read_b64_tr_b16 (two per fragment: k rows 8g..8g+3 and 8g+4..8g+7 of
+//    16-lane group g); the 8 rows a 32-lane bank group touches land on 8
+//    distinct 32-B bank ranges: conflict-free.
+//
+// The MFMA is issued as mfma(B-fragment, A-fragment) so each lane's four
+// accumulators are FOUR CONSECUTIVE OUTPUT COLUMNS of one row: the epilogue
+// adds the bias / applies GELU in fp32 and stores 8-byte bf16x4 pieces.
+//
+// Tile order: XCD-aware bijective remap of the workgroup id, then groups of 8
+// tile rows walked column by column, so the workgroups resident on one XCD
+// share A and B panels in its L2.
+#include "common.h"
+
+namespace dta {
+
+constexpr int kGbBK = 32;      // k per stage
+constexpr int kGbStages = 4;   // LDS ring depth (3 stages in flight)
+constexpr int kGbGroupM = 8;   // tile rows per group (L2 panel reuse)
+
+struct GemmBfArgs {
+  const bf16* a;
+  const bf16* b;
+  bf16* c;
+  float* c32;           // fp32 output instead of bf16 (nullptr: bf16 to c)
+  const bf16* bias;     // [N] or nullptr
+  const bf16* res;      // residual [M][ldr] added after rounding, or nullptr
+  int64_t lda, ldb, ldc, ldr;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  float alpha;
+  int act;              // ACT_NONE / ACT_GELU_TANH
+};
+
+__device__ __forceinline__ int kswz(int r) { return ((r >> 3) & 1) * 3; }
+__device__ __forceinline__ int mswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+__device__ __forceinline__ bf16x4 tr4(const char* lds, int byte_off) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lds + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// 16 rows (r0 .. r0+15) x 32 k of a K-major image: lane l -> row r0 + (l & 15), k 8(l >> 4) .. +7
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int r0, int lane) {
+  const int r = r0 + (lane & 15), c = lane >> 4;
+  return *reinterpret_cast<const bf16x8*>(img + r * 64 + 16 * (c ^ kswz(r)));
+}
+
+// 16 indices (i0 .. i0+15) x 32 k of an M/N-major image with ROWB-byte rows (same lane map)
+template <int ROWB>
+__device__ __forceinline__ bf16x8 frag_mn(const char* img, int i0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int k = 8 * g + q;
+  const int col = i0 + 4 * p;
+  const int off = 16 * ((col >> 3) ^ mswz(k)) + (col & 7) * 2;
+  const bf16x4 lo = tr4(img, k * ROWB + off);
+  const bf16x4 hi = tr4(img, (k + 4) * ROWB + off);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// counted wait + barrier: at most `ahead` stages (of L loads each) of this wave still in flight
+template <int L>
+__device__ __forceinline__ void stage_barrier(int ahead) {
+  if (ahead >= 2) vm_wait_n<2 * L>();
+  else if (ahead == 1) vm_wait_n<L>();
+  else vm_wait_n<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int BM, int BN, bool AT, bool BT>
+__global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
+  constexpr int A_BYTES = BM * kGbBK * 2, B_BYTES = BN * kGbBK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int WTM = BM / 2, WTN = BN / 4, MT = WTM / 16, NT = WTN / 16;
+  constexpr int AL = BM / 128, BL = BN / 128, L = AL + BL;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(1024))) char lds[kGbStages * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // tile: XCD remap, then groups of kGbGroupM tile rows walked column-major
+  const int nwg = g.tiles_m * g.tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int per_group = kGbGroupM * g.tiles_n;
+  const int grp = t / per_group, in_g = t - grp * per_group;
+  const int gm0 = grp * kGbGroupM, gh = min(kGbGroupM, g.tiles_m - gm0);
+  const int tm = gm0 + in_g % gh, tn = in_g / gh;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-lane DMA sources at stage 0 (stage s adds s * step)
+  const bf16* srcA[AL];
+  const bf16* srcB[BL];
+#pragma unroll
+  for (int j = 0; j < AL; ++j) {
+    const int i = wave * AL + j;
+    if constexpr (!AT) {  // K-major: instruction i = rows 16i .. 16i+15, 4 lanes per 64-B row
+      const int r = 16 * i + (lane >> 2), c = (lane & 3) ^ kswz(r);
+      srcA[j] = g.a + (int64_t)(m0 + r) * g.lda + 8 * c;
+    } else {  // M-major: rows of 2*BM bytes, 1024 / (2 BM) rows per instruction
+      constexpr int CPR = BM / 8, RPI = 64 / CPR;
+      const int r = RPI * i + lane / CPR, c = (lane % CPR) ^ mswz(r);
+      srcA[j] = g.a + (int64_t)r * g.lda + m0 + 8 * c;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < BL; ++j) {
+    const int i = wave * BL + j;
+    if constexpr (!BT) {
+      const int r = 16 * i + (lane >> 2), c = (lane & 3) ^ kswz(r);
+      srcB[j] = g.b + (int64_t)(n0 + r) * g.ldb + 8 * c;
+    } else {
+      constexpr int CPR = BN / 8, RPI = 64 / CPR;
+      const int r = RPI * i + lane / CPR, c = (lane % CPR) ^ mswz(r);
+      srcB[j] = g.b + (int64_t)r * g.ldb + n0 + 8 * c;
+    }
+  }
+  const int64_t stepA = AT ? (int64_t)kGbBK * g.lda : kGbBK;
+  const int64_t stepB = BT ? (int64_t)kGbBK * g.ldb : kGbBK;
+  auto issue = [&](int s) {
+    char* sa = lds + (s & (kGbStages - 1)) * STAGE;
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < AL; ++j) glds16(srcA[j] + s * stepA, sa + (wave * AL + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < BL; ++j) glds16(srcB[j] + s * stepB, sb + (wave * BL + j) * 1024);
+  };
+
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / kGbBK;
+  const int pre = min(nk, kGbStages - 1);
+  for (int s = 0; s < pre; ++s) issue(s);
+  stage_barrier<L>(pre - 1);  // stage 0 landed everywhere
+  for (int kt = 0; kt < nk; ++kt) {
+    // ring slot of stage kt+3 was last read in iteration kt-1, before its barrier
+    if (kt + kGbStages - 1 < nk) issue(kt + kGbStages - 1);
+    const char* sa = lds + (kt & (kGbStages - 1)) * STAGE;
+    const char* sb = sa + A_BYTES;
+    bf16x8 af[MT], bfr[NT];
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      if constexpr (!AT) af[j] = frag_k(sa, wm * WTM + 16 * j, lane);
+      else af[j] = frag_mn<2 * BM>(sa, wm * WTM + 16 * j, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      if constexpr (!BT) bfr[i] = frag_k(sb, wn * WTN + 16 * i, lane);
+      else bfr[i] = frag_mn<2 * BN>(sb, wn * WTN + 16 * i, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) stage_barrier<L>(min(nk - 1, kt + kGbStages - 1) - (kt + 1));
+  }
+
+  // epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + r (r = 0..3)
+  const int mrow = m0 + wm * WTM + (lane & 15);
+  const int ncol = n0 + wn * WTN + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int n = ncol + 16 * i;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias) {
+      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+    }
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = mrow + 16 * j;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = fmaf(acc[i][j][r], g.alpha, bv[r]);
+        if (g.act == ACT_GELU_TANH) v[r] = act_fwd(ACT_GELU_TANH, v[r]);
+      }
+      if (g.c32) {
+        *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
+      if (g.res) {  // residual stream: y = round(round(linear) + res), as two bf16 ops would give
+        const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);
+      }
+      *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    }
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT>
+static hipError_t launch_bf(const GemmBfArgs& g, hipStream_t st) {
+  // static LDS: 4 x (BM + BN) x 64 B (128 KiB at 256 x 256: one workgroup per CU)
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
+  return hipGetLastError();
+}
+
+template <int BM, int BN>
+static hipError_t launch_tile(const GemmBfArgs& g, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_bf<BM, BN, false, false>(g, st);
+  if (!at && bt) return launch_bf<BM, BN, false, true>(g, st);
+  if (at && bt) return launch_bf<BM, BN, true, true>(g, st);
+  return launch_bf<BM, BN, true, false>(g, st);
+}
+
+}  // namespace dta
+
+using namespace dta;
+
+// Tile choice: minimise (rounds of resident workgroups) x (tile work / tile efficiency).
+// tile = 0: auto; 1: 256x256, 2: 256x128, 3: 128x128 (when it divides the problem).
+int dta_gemm_bf16_tile(int M, int N, int K, int tile) {
+  static const int bm[4] = {0, 256, 256, 128}, bn[4] = {0, 256, 128, 128};
+  static const double eff[4] = {0, 1.0, 0.86, 0.72};   // relative MFMA efficiency of the tile shapes
+  static const int per_cu[4] = {0, 1, 1, 2};          // resident workgroups per CU (LDS ring size)
+  if (K % kGbBK || K < kGbBK) return 0;
+  if (tile) return (M % bm[tile] == 0 && N % bn[tile] == 0) ? tile : 0;
+  int best = 0;
+  double best_t = 1e30;
+  for (int t = 1; t <= 3; ++t) {
+    if (M % bm[t] || N % bn[t]) continue;
+    const int tiles = (M / bm[t]) * (N / bn[t]);
+    const int slots = 256 * per_cu[t];
+    const int rounds = (tiles + slots - 1) / slots;
+    // a round costs one tile's time on a CU shared by per_cu workgroups
+    const double tt = rounds * (double)bm[t] * bn[t] * per_cu[t] / eff[t];
+    if (tt < best_t * 0.999) {
+      best_t = tt;
+      best = t;
+    }
+  }
+  return best;
+}
+
+hipError_t dta_gemm_bf16(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
+                         float* c32, int64_t ldc, int M, int N, int K, float alpha, const void* bias, int act,
+                         const void* res, int64_t ldr, int tile, hipStream_t st) {
+  tile = dta_gemm_bf16_tile(M, N, K, tile);
+  if (!tile || N % 8 || (!c && !c32)) return hipErrorInvalidValue;
+  GemmBfArgs g{};
+  g.a = static_cast<const bf16*>(a);
+  g.b = static_cast<const bf16*>(b);
+  g.c = static_cast<bf16*>(c);
+  g.c32 = c32;
+  g.bias = static_cast<const bf16*>(bias);
+  g.res = static_cast<const bf16*>(res);
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.ldr = ldr;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.alpha = alpha;
+  g.act = act;
+  switch (tile) {
+    case 1:
+      g.tiles_m = M / 256;
+      g.tiles_n = N / 256;
+      return launch_tile<256, 256>(g, a_t, b_t, st);
+    case 2:
+      g.tiles_m = M / 256;
+      g.tiles_n = N / 128;
+      return launch_tile<256, 128>(g, a_t, b_t, st);
+    default:
+      g.tiles_m = M / 128;
+      g.tiles_n = N / 128;
+      return launch_tile<128, 128>(g, a_t, b_t, st);
+  }
+}

@@ -1,0 +1,223 @@
+// Fused train step of the reference's default model: ONE nn.Linear(in, out)
+// (src/distributed_trainer.py:199, conf/model/default.yaml) with the
+// reference's loss (F.cross_entropy against float targets = soft-label CE,
+// :163) or MSE, fp32 like the reference, and torch.optim.SGD (:200, :165).
+//
+// SURVEY.md §2.6 lists ~15 ATen launches per reference step for this model
+// (addmm, log_softmax, mul/sum/neg/div, their backwards, mm for dW, sum for
+// db, the DDP mul_out/copy kernels, SGD add_).  Here a step is a handful of
+// LDS phases inside one workgroup:
+//
+//   [pending SGD update from the all-reduced gradients of the previous step]
+//   gather the batch rows by DistributedSampler index (device index ring)
+//   logits z = x W^T + b                    (fp32 FMA, W resident in LDS)
+//   loss + dz (soft-label CE or MSE, mean over the batch)
+//   dW = dz^T x, db = sum_b dz             (fp32)
+//   world size 1: SGD in LDS, next step   |   world size > 1: dW, db * 1/ws -> G_out
+//
+// Two launch forms share the kernel:
+//  * persistent (one rank): `nsteps` complete steps per launch, parameters
+//    (and momentum) resident in LDS for the whole launch;
+//  * per-step (several ranks): nsteps = 1, the pending update of the previous
+//    step is applied first (from the RCCL / p2p all-reduced G_in), this step's
+//    gradients go to G_out for the all-reduce that follows in the same graph.
+//
+// The shapes are tiny (Linear(20, 1): 21 parameters, 32 x 20 batch): this
+// is latency-bound VALU work, not MFMA work -- one workgroup, fp32 FMA, no
+// global round trips between phases.
+#include "common.h"
+
+namespace dta {
+
+struct LinStepArgs {
+  const float* X;         // [N, I] fp32 (device-resident dataset)
+  const float* T;         // [N, C] fp32 targets
+  const int* ring;        // [R][B] sampler indices
+  const int* counts;      // [R] batch size of each slot (last batch of an epoch may be short)
+  int* cursor;            // global step counter (slot = cursor % R), advanced by the kernel
+  float* P;               // [C*I | C] weight (row-major [C][I]) then bias
+  float* M;               // momentum buffer (same layout) or nullptr
+  int* flags;             // [0] momentum buffer initialised, [1] G_in holds an update not yet applied
+  const float* G_in;      // per-step form: all-reduced gradients of the previous step (or nullptr)
+  float* G_out;           // per-step form: this step's gradients * grad_scale (nullptr: persistent form)
+  float* loss_ring;       // [loss_len] per-step mean loss
+  int* loss_cursor;
+  int loss_len;
+  int R, B, I, C, nsteps, loss_kind;  // loss_kind: 0 = MSE, 1 = soft-label cross-entropy
+  float lr, momentum, dampening, weight_decay, grad_scale;
+  int nesterov, maximize;
+};
+
+constexpr int kLinThreads = 256;
+constexpr int kLinMaxParams = 8192;  // C*I + C fp32 in LDS (x2 with momentum)
+constexpr int kLinMaxBI = 8192;      // batch rows in LDS (B*I fp32)
+constexpr int kLinMaxBC = 2048;      // B*C logits / targets / dz
+
+__device__ __forceinline__ float sgd_update(float p, float g, float* m, bool started, const LinStepArgs& a) {
+  float d = a.maximize ? -g : g;
+  if (a.weight_decay != 0.f) d += a.weight_decay * p;
+  if (m) {
+    const float buf = started ? a.momentum * (*m) + (1.f - a.dampening) * d : d;
+    *m = buf;
+    d = a.nesterov ? d + a.momentum * buf : buf;
+  }
+  return p - a.lr * d;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kLinThreads / 64; ++i) s += red[i];
+  return s;
+}
+
+__global__ void __launch_bounds__(kLinThreads) linear_step_kernel(LinStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int I = a.I, C = a.C, NP = C * I + C;
+  float* p_s = lds;                                  // [NP]
+  float* m_s = p_s + NP;                             // [NP] (momentum) -- present only with M
+  float* x_s = m_s + (a.M ? NP : 0);                 // [B][I]
+  float* t_s = x_s + a.B * I;                        // [B][C]
+  float* z_s = t_s + a.B * C;                        // [B][C] logits, then dz
+  float* red = z_s + a.B * C;                        // [4] block reduction
+  const int tid = threadIdx.x;
+
+  for (int e = tid; e < NP; e += kLinThreads) {
+    p_s[e] = a.P[e];
+    if (a.M) m_s[e] = a.M[e];
+  }
+  bool started = a.M ? (a.flags[0] != 0) : false;
+  const bool pending = a.G_in != nullptr && a.flags[1] != 0;
+  __syncthreads();
+  // per-step form: the previous step's update, from the all-reduced gradients
+  // (every launch of an epoch is the same graph node; the flag says whether
+  // there is an update to apply -- the first step after a flush has none)
+  if (pending) {
+    for (int e = tid; e < NP; e += kLinThreads) p_s[e] = sgd_update(p_s[e], a.G_in[e], a.M ? &m_s[e] : nullptr, started, a);
+    started = true;
+    __syncthreads();
+  }
+  const int cur0 = *a.cursor;
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int slot = (cur0 + s) % a.R;
+    const int nb = a.counts[slot];
+    const int* idx = a.ring + (int64_t)slot * a.B;
+    // gather this step's rows (features and targets) into LDS
+    for (int e = tid; e < nb * I; e += kLinThreads) {
+      const int b = e / I, i = e - b * I;
+      x_s[e] = a.X[(int64_t)idx[b] * I + i];
+    }
+    for (int e = tid; e < nb * C; e += kLinThreads) {
+      const int b = e / C, c = e - b * C;
+      t_s[e] = a.T[(int64_t)idx[b] * C + c];
+    }
+    __syncthreads();
+    // logits
+    for (int e = tid; e < nb * C; e += kLinThreads) {
+      const int b = e / C, c = e - b * C;
+      const float* w = p_s + c * I;
+      const float* x = x_s + b * I;
+      float z = p_s[C * I + c];
+      for (int i = 0; i < I; ++i) z = fmaf(x[i], w[i], z);
+      z_s[e] = z;
+    }
+    __syncthreads();
+    // loss and dz (one thread per row)
+    float lsum = 0.f;
+    for (int b = tid; b < nb; b += kLinThreads) {
+      float* z = z_s + b * C;
+      const float* t = t_s + b * C;
+      if (a.loss_kind == 1) {
+        float mx = z[0];
+        for (int c = 1; c < C; ++c) mx = fmaxf(mx, z[c]);
+        float se = 0.f, ts = 0.f;
+        for (int c = 0; c < C; ++c) {
+          se += __expf(z[c] - mx);
+          ts += t[c];
+        }
+        const float lse = mx + __logf(se);
+        // -sum_c t_c log_softmax(z)_c with log_softmax formed first (as ATen does):
+        // one logit gives log_softmax == 0 exactly, hence loss 0
+        for (int c = 0; c < C; ++c) lsum -= t[c] * (z[c] - lse);
+        const float inv = 1.f / (float)nb;
+        for (int c = 0; c < C; ++c) z[c] = (__expf(z[c] - lse) * ts - t[c]) * inv;
+      } else {
+        const float inv = 2.f / (float)(nb * C);
+        for (int c = 0; c < C; ++c) {
+          const float d = z[c] - t[c];
+          lsum += d * d;
+          z[c] = d * inv;
+        }
+      }
+    }
+    const float ltot = block_sum(lsum, red);  // (its barriers also publish dz)
+    if (tid == 0) {
+      const int lc = *a.loss_cursor;
+      a.loss_ring[lc % a.loss_len] = a.loss_kind == 1 ? ltot / (float)nb : ltot / (float)(nb * C);
+      *a.loss_cursor = lc + 1;
+    }
+    // gradients; one rank: SGD right here, several ranks: to the exchange buffer
+    for (int e = tid; e < NP; e += kLinThreads) {
+      float g = 0.f;
+      if (e < C * I) {
+        const int c = e / I, i = e - c * I;
+        for (int b = 0; b < nb; ++b) g = fmaf(z_s[b * C + c], x_s[b * I + i], g);
+      } else {
+        const int c = e - C * I;
+        for (int b = 0; b < nb; ++b) g += z_s[b * C + c];
+      }
+      if (a.G_out) {
+        a.G_out[e] = g * a.grad_scale;
+      } else {
+        p_s[e] = sgd_update(p_s[e], g, a.M ? &m_s[e] : nullptr, started, a);
+      }
+    }
+    if (!a.G_out) started = true;
+    __syncthreads();
+  }
+  for (int e = tid; e < NP; e += kLinThreads) {
+    a.P[e] = p_s[e];
+    if (a.M) a.M[e] = m_s[e];
+  }
+  if (tid == 0) {
+    *a.cursor = cur0 + a.nsteps;
+    if (a.M && started) a.flags[0] = 1;
+    if (a.G_in) a.flags[1] = (a.G_out != nullptr && a.nsteps > 0) ? 1 : 0;  // flush (no G_out): consumed
+  }
+}
+
+}  // namespace dta
+
+using namespace dta;
+
+size_t dta_linear_step_lds_bytes(int I, int C, int B, int momentum) {
+  const size_t np = (size_t)C * I + C;
+  return 4 * (np * (momentum ? 2 : 1) + (size_t)B * I + 2 * (size_t)B * C + 4);
+}
+
+int dta_linear_step_supported(int I, int C, int B, int momentum) {
+  const int64_t np = (int64_t)C * I + C;
+  return I >= 1 && C >= 1 && B >= 1 && np <= kLinMaxParams && (int64_t)B * I <= kLinMaxBI &&
+         (int64_t)B * C <= kLinMaxBC && dta_linear_step_lds_bytes(I, C, B, momentum) <= 160 * 1024;
+}
+
+hipError_t dta_linear_step(const LinStepArgs* a, hipStream_t st) {
+  if (!dta_linear_step_supported(a->I, a->C, a->B, a->M != nullptr) || a->nsteps < 0 || a->R < 1)
+    return hipErrorInvalidValue;
+  const size_t lds = dta_linear_step_lds_bytes(a->I, a->C, a->B, a->M != nullptr);
+  if (lds > 64 * 1024) {
+    static bool raised = false;  // dynamic LDS above 64 KiB must be opted into once
+    if (!raised) {
+      DTA_HIP_CHECK(hipFuncSetAttribute((const void*)linear_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
+      raised = true;
+    }
+  }
+  hipLaunchKernelGGL(linear_step_kernel, dim3(1), dim3(kLinThreads), lds, st, *a);
+  return hipGetLastError();
+}

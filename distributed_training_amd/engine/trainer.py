@@ -15,7 +15,8 @@ Engine differences (all behaviour-preserving unless noted):
   optimizers with identical hyper-parameters (``fused_optimizer``);
 * batches come from the device-resident loader (no per-step H2D copy, no
   extra batch fetched just to log its size -- SURVEY.md Q6);
-* for the 2-layer MLP + DDP + SGD configuration the whole step runs as the
+* for the 2-layer MLP (and the reference default, one nn.Linear) + DDP + SGD
+  configuration the whole step runs as the
   fused gfx950 kernel + RCCL all-reduce, hipGraph-captured
   (:mod:`.fused_mlp`);
 * checkpoint save is entered by every rank (rank 0 writes) -- required for
@@ -170,8 +171,17 @@ class Trainer:
             self._fused = FusedMLPProgram(module, self.optimizer, loader, default_comm(self.device),
                                           loss=self.config.loss, graph_steps=self.config.graph_steps)
             logger.debug("fused MLP step program enabled")
+            return
+        # the reference's default model (one nn.Linear, CE, fp32, SGD)
+        from .fused_linear import FusedLinearProgram, linear_eligible
+
+        why_lin = linear_eligible(module, self.optimizer, loader, self.config.loss, self.device)
+        if why_lin is None:
+            self._fused = FusedLinearProgram(module, self.optimizer, loader, default_comm(self.device),
+                                             loss=self.config.loss)
+            logger.debug("fused Linear step program enabled")
         else:
-            logger.debug(f"fused MLP step program not used: {why}")
+            logger.debug(f"fused step programs not used: {why}; {why_lin}")
 
     # ------------------------------------------------------------------ loop
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
