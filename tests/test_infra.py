@@ -85,3 +85,47 @@ def test_terraform_module_declares_template_variables():
         assert re.search(rf"\b{n}\s*=", main), n
     variables = (ROOT / "infrastructure/mi355x/cluster/variables.tf").read_text()
     assert "var.cluster_size > 0" in variables
+
+
+def _hcl_blocks(text):
+    """Top-level `resource "type" "name"` / `module "name"` / `variable "name"` headers of an HCL file."""
+    return re.findall(r'^(resource|module|variable|output|data)\s+"([^"]+)"(?:\s+"([^"]+)")?\s*\{', text, re.M)
+
+
+@pytest.mark.parametrize("mod", ["oci/cluster", "oci/single_gpu"])
+def test_oci_modules_are_consistent(mod):
+    """Provisioning modules (no terraform binary here): balanced braces, every var.X declared,
+    every resource / module reference defined, boot module sources resolve."""
+    d = ROOT / "infrastructure/mi355x" / mod
+    text = {p.name: p.read_text() for p in d.glob("*.tf")}
+    allt = "\n".join(text.values())
+    for name, t in text.items():
+        assert t.count("{") == t.count("}"), name
+    blocks = _hcl_blocks(allt)
+    declared_vars = {b[1] for b in blocks if b[0] == "variable"}
+    for v in set(re.findall(r"\bvar\.([A-Za-z_]\w*)", allt)):
+        assert v in declared_vars, v
+    resources = {(b[1], b[2]) for b in blocks if b[0] == "resource"}
+    for typ, name in set(re.findall(r"\b(oci_[a-z_]+)\.([a-z_0-9]+)\b", allt)):
+        assert (typ, name) in resources, (typ, name)
+    modules = {b[1]: None for b in blocks if b[0] == "module"}
+    for m in set(re.findall(r"\bmodule\.([a-z_0-9]+)\b", allt)):
+        assert m in modules, m
+    for src in re.findall(r'source\s*=\s*"(\.[^"]+)"', allt):
+        assert (d / src / "main.tf").exists(), src
+    # the module passes exactly the boot module's variables
+    boot_vars = {b[1] for b in _hcl_blocks((ROOT / "infrastructure/mi355x/cluster/variables.tf").read_text())}
+    for body in re.findall(r'module\s+"[^"]+"\s*\{(.*?)\n\}', allt, re.S):
+        for arg in re.findall(r"^\s*([a-z_]+)\s*=", body, re.M):
+            assert arg == "source" or arg in boot_vars, arg
+
+
+def test_oci_cluster_provisions_nodes_fabric_and_shared_fs():
+    t = "\n".join(p.read_text() for p in (ROOT / "infrastructure/mi355x/oci/cluster").glob("*.tf"))
+    kinds = {b[1] for b in _hcl_blocks(t) if b[0] == "resource"}
+    for need in ("oci_core_instance", "oci_core_compute_cluster", "oci_file_storage_file_system",
+                 "oci_file_storage_mount_target", "oci_file_storage_export", "oci_core_vcn", "oci_core_subnet"):
+        assert need in kinds, need
+    outs = {b[1] for b in _hcl_blocks(t) if b[0] == "output"}
+    assert {"master_public_ip", "master_internal_ip", "worker_public_ips", "worker_internal_ips"} <= outs
+    assert "count               = var.cluster_size - 1" in t and "depends_on = [oci_core_instance.master]" in t
