@@ -225,6 +225,12 @@ def main():
            "config": {"model": args.model, "layers": cfg.n_layer, "global_batch": args.batch * ws,
                       "seq_len": args.seq, "parallelism": f"{args.strategy}{ws}", "impl": args.impl, "tunableop": args.tunableop,
                       "activation_checkpointing": args.ckpt}}
+    if args.impl == "native":
+        from distributed_training_amd.ops import lm as _lm
+
+        # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
+        out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": (f"dta/t{v}" if v else "hipblaslt")
+                            for k, v in sorted(_lm._GEMM_CHOICE.items())}
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.json_out:

@@ -16,10 +16,11 @@
 // Structure (cdna_hip_programming.md §5): a BM x BN tile per workgroup of 8
 // waves (2 x 4), each wave (BM/2) x (BN/4) on v_mfma_f32_16x16x32_bf16; the
 // k loop streams 32-deep stages by global_load_lds_dwordx4 (LDS-DMA, no
-// staging VGPRs) into a 4-deep LDS ring, so three stages are in flight while
-// one is multiplied; the wait before each barrier is a counted vmcnt (never 0
-// inside the loop) and the barrier is a raw s_barrier, so the DMA of later
-// stages spans it.
+// staging VGPRs) into a 4-deep LDS ring; the fragments of stage k+1 are read
+// from LDS while the MFMAs of stage k run (two register sets), and up to three
+// stages of DMA are in flight; the wait before each barrier is a counted vmcnt
+// (never 0 inside the loop) and the barrier is a raw s_barrier, so the DMA of
+// later stages spans it.
 //
 // LDS images (all lane-linear for the DMA; the XOR swizzle is applied to the
 // per-lane SOURCE address and undone on the read, rule 21):
@@ -97,13 +98,16 @@ __device__ __forceinline__ void vm_wait_n() {
 // counted wait + barrier: at most `ahead` stages (of L loads each) of this wave still in flight
 template <int L>
 __device__ __forceinline__ void stage_barrier(int ahead) {
-  if (ahead >= 2) vm_wait_n<2 * L>();
+  if (ahead >= 3) vm_wait_n<3 * L>();
+  else if (ahead == 2) vm_wait_n<2 * L>();
   else if (ahead == 1) vm_wait_n<L>();
   else vm_wait_n<0>();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int BM, int BN, bool AT, bool BT>
+__device__ __forceinline__ void lds_bar() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int BM, int BN, bool AT, bool BT, bool PP>
 __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   constexpr int A_BYTES = BM * kGbBK * 2, B_BYTES = BN * kGbBK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int WTM = BM / 2, WTN = BN / 4, MT = WTM / 16, NT = WTN / 16;
@@ -167,31 +171,118 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto frag_a = [&](const char* sa, int j) {
+    if constexpr (!AT) return frag_k(sa, wm * WTM + 16 * j, lane);
+    else return frag_mn<2 * BM>(sa, wm * WTM + 16 * j, lane);
+  };
+  auto frag_b = [&](const char* sb, int i) {
+    if constexpr (!BT) return frag_k(sb, wn * WTN + 16 * i, lane);
+    else return frag_mn<2 * BN>(sb, wn * WTN + 16 * i, lane);
+  };
   const int nk = g.K / kGbBK;
-  const int pre = min(nk, kGbStages - 1);
-  for (int s = 0; s < pre; ++s) issue(s);
-  stage_barrier<L>(pre - 1);  // stage 0 landed everywhere
-  for (int kt = 0; kt < nk; ++kt) {
-    // ring slot of stage kt+3 was last read in iteration kt-1, before its barrier
-    if (kt + kGbStages - 1 < nk) issue(kt + kGbStages - 1);
-    const char* sa = lds + (kt & (kGbStages - 1)) * STAGE;
-    const char* sb = sa + A_BYTES;
+
+  if constexpr (PP) {
+    // Ping-pong (cdna_hip_programming.md §5.5 T3-T5): each stage is two phases
+    // (half of the wave's B fragments each), and every phase is a load section
+    // (ds_reads, LDS-DMA issue, counted vmcnt) and an MFMA section, separated by
+    // workgroup barriers.  Waves 4-7 (wm = 1) run ONE BARRIER BEHIND waves 0-3,
+    // and each SIMD holds one wave of each group, so while one group multiplies
+    // the other loads: the MFMA pipe alternates between the two waves of a SIMD.
+    //
+    // Barrier numbering (group 0; group 1 is +1): L(k,0) #4k+1 M(k,0) #4k+2
+    // L(k,1) #4k+3 M(k,1) #4k+4.  Stage k+1 is waited for (vmcnt) in L(k,1) by
+    // every wave -> visible after #4k+4, before any L(k+1, .) read.  Stage k+3 is
+    // DMA'd in L(k,1) into the slot of stage k-1, whose last reads (group 1,
+    // L(k-1,1)) retired before #4k+1.
+    constexpr int HN = NT / 2;
     bf16x8 af[MT], bfr[NT];
+    const int pre = min(nk, kGbStages - 1);
+    for (int s = 0; s < pre; ++s) issue(s);
+    if (pre >= 3) vm_wait_n<2 * L>();
+    else if (pre == 2) vm_wait_n<L>();
+    else vm_wait_n<0>();
+    lds_bar();
+    if (wm == 1) lds_bar();
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* sa = lds + (kt & (kGbStages - 1)) * STAGE;
+      const char* sb = sa + A_BYTES;
+      // L(kt, 0)
 #pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      if constexpr (!AT) af[j] = frag_k(sa, wm * WTM + 16 * j, lane);
-      else af[j] = frag_mn<2 * BM>(sa, wm * WTM + 16 * j, lane);
+      for (int j = 0; j < MT; ++j) af[j] = frag_a(sa, j);
+#pragma unroll
+      for (int i = 0; i < HN; ++i) bfr[i] = frag_b(sb, i);
+      lds_bar();
+      // M(kt, 0)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < HN; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      lds_bar();
+      // L(kt, 1)
+#pragma unroll
+      for (int i = HN; i < NT; ++i) bfr[i] = frag_b(sb, i);
+      if (kt + kGbStages - 1 < nk) issue(kt + kGbStages - 1);
+      if (kt + 1 < nk) {
+        const int ahead = min(nk - 1, kt + kGbStages - 1) - (kt + 1);
+        if (ahead >= 2) vm_wait_n<2 * L>();
+        else if (ahead == 1) vm_wait_n<L>();
+        else vm_wait_n<0>();
+      }
+      lds_bar();
+      // M(kt, 1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = HN; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      lds_bar();
     }
+    if (wm == 0) lds_bar();  // same barrier count for both groups
+  } else {
+    // fragments of one stage (two named sets: stage kt+1 is read while stage kt multiplies)
+    auto read = [&](int s, bf16x8 (&af)[MT], bf16x8 (&bfr)[NT]) {
+      const char* sa = lds + (s & (kGbStages - 1)) * STAGE;
+      const char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      if constexpr (!BT) bfr[i] = frag_k(sb, wn * WTN + 16 * i, lane);
-      else bfr[i] = frag_mn<2 * BN>(sb, wn * WTN + 16 * i, lane);
+      for (int j = 0; j < MT; ++j) af[j] = frag_a(sa, j);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) bfr[i] = frag_b(sb, i);
+    };
+    auto mma = [&](const bf16x8 (&af)[MT], const bf16x8 (&bfr)[NT]) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+    };
+    // Ring: stage s in slot s % 4.  Iteration kt: [wait stage kt+1, barrier] [DMA stage
+    // kt+4 into slot kt % 4 -- stage kt's fragments were read in iteration kt-1 and the
+    // barrier's lgkmcnt(0) retired those reads on every wave] [read stage kt+1] [MFMA kt].
+    const int pre = min(nk, kGbStages);
+    for (int s = 0; s < pre; ++s) issue(s);
+    stage_barrier<L>(pre - 1);  // stage 0 landed everywhere
+    bf16x8 afA[MT], bfA[NT], afB[MT], bfB[NT];
+    read(0, afA, bfA);
+    auto body = [&](int kt, const bf16x8 (&ca)[MT], const bf16x8 (&cb)[NT], bf16x8 (&na)[MT], bf16x8 (&nb)[NT]) {
+      if (kt + 1 < nk) {
+        stage_barrier<L>(min(nk - 1, kt + kGbStages - 1) - (kt + 1));
+        if (kt + kGbStages < nk) issue(kt + kGbStages);
+        read(kt + 1, na, nb);
+      }
+      mma(ca, cb);
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      body(kt, afA, bfA, afB, bfB);
+      if (kt + 1 < nk) body(kt + 1, afB, bfB, afA, bfA);
     }
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-      for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) stage_barrier<L>(min(nk - 1, kt + kGbStages - 1) - (kt + 1));
   }
 
   // epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + r (r = 0..3)
@@ -232,7 +323,8 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
 template <int BM, int BN, bool AT, bool BT>
 static hipError_t launch_bf(const GemmBfArgs& g, hipStream_t st) {
   // static LDS: 4 x (BM + BN) x 64 B (128 KiB at 256 x 256: one workgroup per CU)
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
+  constexpr bool PP = BM == 256 && BN == 256;  // ping-pong schedule for the big tile
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
   return hipGetLastError();
 }
 

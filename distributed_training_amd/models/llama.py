@@ -61,8 +61,8 @@ class Attention(nn.Module):
         super().__init__()
         self.H, self.Hkv = cfg.n_head, cfg.n_kv_head
         self.D = cfg.n_embd // cfg.n_head
-        self.wqkv = nn.Linear(cfg.n_embd, (self.H + 2 * self.Hkv) * self.D, bias=False)
-        self.wo = nn.Linear(self.H * self.D, cfg.n_embd, bias=False)
+        self.wqkv = lm.Linear(cfg.n_embd, (self.H + 2 * self.Hkv) * self.D, bias=False)
+        self.wo = lm.Linear(self.H * self.D, cfg.n_embd, bias=False)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
@@ -74,8 +74,8 @@ class Attention(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.w13 = nn.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
-        self.w2 = nn.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
+        self.w13 = lm.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
+        self.w2 = lm.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
 
     def forward(self, x):
         return self.w2(lm.swiglu(self.w13(x)))

@@ -4,13 +4,20 @@
 GPU tensors always take the HIP kernels (bf16 activations required -- the
 models run under bf16 mixed precision on GPU; anything else raises).  CPU
 tensors use the equivalent PyTorch math, which is also the numerics reference
-of the GPU tests.  Plain GEMMs (the projections) stay on ``F.linear``
-(hipBLASLt), as the build rules allow for unfused library GEMMs.
+of the GPU tests.
+
+Projection GEMMs (forward x W^T + b, input gradient dy W, weight gradient
+dy^T x, the LM head) go through :func:`gemm`: the gfx950 GEMM of
+``csrc/gemm_bf16.hip`` (bias / scale fused in its epilogue) or hipBLASLt,
+whichever measured faster for that shape on this GPU (timed once per shape
+and process, ``DTA_GEMM=auto``; ``dta`` / ``torch`` force one).  Weight
+gradients with small outputs keep the split-K kernel of ``csrc/gemm.hip``.
 """
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+import os
+from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -212,8 +219,90 @@ def rms_norm(x, w, eps: float = 1e-5):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * w
 
 
+# ------------------------------------------------------------------ GEMM dispatch
+_GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 0 = hipBLASLt
+GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0}
+
+
+def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 4) -> Dict[int, float]:
+    """Median per-call time of each candidate, rounds interleaved (clock / cache state
+    shared fairly; the first call of each -- code object load, library heuristics -- untimed)."""
+    for fn in fns.values():
+        fn()
+        fn()
+    res: Dict[int, list] = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                fn()
+            e.record()
+            e.synchronize()
+            res[k].append(s.elapsed_time(e) * 1e3 / reps)
+    return {k: sorted(v)[len(v) // 2] for k, v in res.items()}
+
+
+def _pick(kind: str, M: int, N: int, K: int, run_dta: Callable[[int], object], run_torch: Callable[[], object]) -> int:
+    """Implementation for one GEMM shape: the dta tile that measured fastest, or 0
+    (hipBLASLt) when the library is faster / the shape is not covered."""
+    key = (kind, M, N, K)
+    c = _GEMM_CHOICE.get(key)
+    if c is not None:
+        return c
+    mode = os.environ.get("DTA_GEMM", "auto")
+    C = native()
+    tiles = [t for t in (1, 2, 3) if C.gemm_tile(M, N, K, t)]
+    if mode == "torch" or not tiles:
+        c = 0
+    elif mode == "dta" or torch.cuda.is_current_stream_capturing():
+        c = C.gemm_tile(M, N, K, 0)
+    else:
+        cands = {0: run_torch}
+        for t in tiles:
+            cands[t] = (lambda t=t: run_dta(t))
+        times = _time_us(cands)
+        # the library keeps the shape unless the dta kernel is clearly faster (>2 %)
+        c = min(times, key=times.get)
+        if c and times[c] > 0.98 * times[0]:
+            c = 0
+    _GEMM_CHOICE[key] = c
+    return c
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False, bias: Optional[torch.Tensor] = None,
+         alpha: float = 1.0, kind: str = "") -> torch.Tensor:
+    """bf16 ``alpha * op(a) op(b)^T (+ bias)`` on GPU, a: [M, K] (a_t: [K, M]), b: [N, K] (b_t: [K, N]);
+    dta kernel or hipBLASLt per shape (see module doc)."""
+    M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
+    N = b.shape[1] if b_t else b.shape[0]
+    ok = (a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous()))
+    C = native()
+
+    def run_dta(tile):
+        return C.gemm(a, b, a_t, b_t, None, False, alpha, bias, 0, None, tile)
+
+    def run_torch():
+        A = a.t() if a_t else a
+        B = b if b_t else b.t()
+        if bias is not None and alpha == 1.0:
+            return torch.addmm(bias, A, B)
+        y = torch.mm(A, B)
+        if alpha != 1.0:
+            y.mul_(alpha)
+        return y if bias is None else y.add_(bias)
+
+    tile = _pick(kind + ("b" if bias is not None else ""), M, N, K, run_dta, run_torch) if ok else 0
+    if tile:
+        GEMM_STATS["dta"] += 1
+        return run_dta(tile)
+    GEMM_STATS["torch"] += 1
+    return run_torch()
+
+
 # ------------------------------------------------------------------ linear
-_WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this hipBLASLt fills the chip by itself
+_WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this the general GEMM fills the chip by itself
 
 
 def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -255,22 +344,24 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
             return dw, db
         return native().gemm_tn(dy2, x2, False, 0, -1, cw)
-    dw = torch.mm(dy2.t(), x2)
+    dw = gemm(dy2, x2, True, True, kind="wgrad")
     if with_bias:
         return dw, native().bias_grad(dy2, False, -1)
     return dw
 
 
 class _Linear(Function):
-    """y = x W^T + b: forward / input-gradient GEMMs on hipBLASLt, weight and
-    bias gradients from one native split-K kernel (see _weight_grad)."""
+    """y = x W^T (+ b): forward and input-gradient GEMMs through :func:`gemm`
+    (bias fused in the epilogue), weight (and bias) gradients from the split-K
+    kernel or :func:`gemm` (see _weight_grad)."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)  # the Parameters themselves (their .grad decides a direct write)
-        return F.linear(x, w, b)
+        x2 = x.reshape(-1, x.shape[-1])
+        return gemm(x2, w, bias=b, kind="fwd").view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
@@ -281,7 +372,7 @@ class _Linear(Function):
             dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(*x.shape[:-1], w.shape[1])
+            dx = gemm(dy2, w, False, True, kind="dgrad").view(*x.shape[:-1], w.shape[1])
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             r = _weight_grad(dy2, x.reshape(-1, x.shape[-1]), with_bias=want_b, w=pw, b=pb if want_b else None)
@@ -292,7 +383,7 @@ class _Linear(Function):
 
 
 def linear(x, w, b=None):
-    if x.is_cuda and b is not None and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+    if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
         return _Linear.apply(x, w, b)
     return F.linear(x, w, b)
@@ -416,7 +507,7 @@ class _LinearCrossEntropy(Function):
     @staticmethod
     def forward(ctx, x, w, target, ignore_index):
         x2 = x.reshape(-1, x.shape[-1])
-        logits = torch.mm(x2, w.t())
+        logits = gemm(x2, w, kind="head_fwd")
         count = (target != ignore_index).sum().clamp_min(1).float()
         loss_rows = native().cross_entropy_fwd_bwd(logits, logits, target, 1.0, ignore_index, -1)
         ctx.save_for_backward(x2, w, logits, count)
@@ -426,12 +517,12 @@ class _LinearCrossEntropy(Function):
     @staticmethod
     def backward(ctx, g):
         x2, w, dlogits, count = ctx.saved_tensors
-        s = (g / count).to(dlogits.dtype)
+        s = (g / count).to(dlogits.dtype)  # stays on the device (no host sync in backward)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dlogits, w).mul_(s).view(ctx.xshape)
+            dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dlogits.t(), x2).mul_(s)
+            dw = gemm(dlogits, x2, True, True, kind="head_wgrad").mul_(s)
         return dx, dw, None, None
 
 

@@ -92,3 +92,52 @@ def test_gemm_rejects_uncovered_shapes():
     with pytest.raises(RuntimeError):
         native().gemm(torch.zeros(128, 48, dtype=torch.bfloat16, device="cuda"),
                       torch.zeros(128, 48, dtype=torch.bfloat16, device="cuda"))  # K % 32
+
+
+@pytest.mark.parametrize("mode", ["dta", "torch", "auto"])
+@pytest.mark.parametrize("bias", [True, False])
+def test_linear_through_gemm_dispatch(mode, bias, monkeypatch):
+    """lm.linear forward + backward (dx, dW, db) through the GEMM dispatcher, each
+    implementation forced, vs fp32 PyTorch on the same bf16 inputs."""
+    from distributed_training_amd.ops import lm
+
+    monkeypatch.setenv("DTA_GEMM", mode)
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    gen = torch.Generator().manual_seed(5)
+    T, K, N = 1024, 512, 1536  # N x K output 12 x 4 tiles of 128: > split-K limit? no -> wgrad split-K
+    x = torch.randn(T, K, generator=gen).bfloat16().cuda().requires_grad_(True)
+    w = (torch.randn(N, K, generator=gen) * 0.05).bfloat16().cuda().requires_grad_(True)
+    b = torch.randn(N, generator=gen).bfloat16().cuda().requires_grad_(True) if bias else None
+    dy = torch.randn(T, N, generator=gen).bfloat16().cuda()
+    before = dict(lm.GEMM_STATS)
+    y = lm.linear(x, w, b)
+    y.backward(dy)
+    if mode == "dta":
+        assert lm.GEMM_STATS["dta"] >= before["dta"] + 2  # forward and input gradient on the dta kernel
+    if mode == "torch":
+        assert lm.GEMM_STATS["dta"] == before["dta"]
+    xf, wf = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    bf = b.detach().float().requires_grad_(True) if bias else None
+    yf = F.linear(xf, wf, bf)
+    yf.backward(dy.float())
+    _close(y, yf.detach(), K)
+    _close(x.grad, xf.grad, N)
+    _close(w.grad, wf.grad, T)
+    if bias:
+        _close(b.grad, bf.grad, T)
+
+
+def test_big_weight_gradient_uses_general_gemm(monkeypatch):
+    """Weight gradients above the split-K kernel's tile limit go through the
+    dispatcher (dta TN layout) -- Llama-size outputs."""
+    from distributed_training_amd.ops import lm
+
+    monkeypatch.setenv("DTA_GEMM", "dta")
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    gen = torch.Generator().manual_seed(9)
+    T, K, N = 512, 2048, 4096  # 32 x 16 = 512 output tiles of 128
+    x = torch.randn(T, K, generator=gen).bfloat16().cuda()
+    dy = torch.randn(T, N, generator=gen).bfloat16().cuda()
+    dw = lm._weight_grad(dy, x)
+    _close(dw, dy.float().t() @ x.float(), T)
+    assert ("wgrad", N, K, T) in lm._GEMM_CHOICE
