@@ -204,11 +204,11 @@ def main():
         # step's collectives must match across ranks); rank 0 prints the table
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as tprof:
             step()
             torch.cuda.synchronize(dev)
         if rank == 0:
-            print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40),
+            print(tprof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=70),
                   file=sys.stderr)
     tokens = args.batch * args.seq * ws * args.steps
     flops_tok = 6 * (n_params - (cfg.block_size * cfg.n_embd if is_gpt else 0)) + 12 * cfg.n_layer * cfg.n_embd * args.seq

@@ -271,24 +271,25 @@ def _pick(kind: str, M: int, N: int, K: int, run_dta: Callable[[int], object], r
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False, bias: Optional[torch.Tensor] = None,
-         alpha: float = 1.0, kind: str = "") -> torch.Tensor:
+         alpha: float = 1.0, kind: str = "", out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 ``alpha * op(a) op(b)^T (+ bias)`` on GPU, a: [M, K] (a_t: [K, M]), b: [N, K] (b_t: [K, N]);
     dta kernel or hipBLASLt per shape (see module doc)."""
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
     ok = (a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
-          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous()))
+          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous())
+          and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)))
     C = native()
 
     def run_dta(tile):
-        return C.gemm(a, b, a_t, b_t, None, False, alpha, bias, 0, None, tile)
+        return C.gemm(a, b, a_t, b_t, out, False, alpha, bias, 0, None, tile)
 
     def run_torch():
         A = a.t() if a_t else a
         B = b if b_t else b.t()
         if bias is not None and alpha == 1.0:
-            return torch.addmm(bias, A, B)
-        y = torch.mm(A, B)
+            return torch.addmm(bias, A, B) if out is None else torch.addmm(bias, A, B, out=out)
+        y = torch.mm(A, B) if out is None else torch.mm(A, B, out=out)
         if alpha != 1.0:
             y.mul_(alpha)
         return y if bias is None else y.add_(bias)
@@ -313,7 +314,13 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     use would overwrite it before autograd sums the two).  Autograd then adopts
     the returned view as ``p.grad`` and the engine's per-bucket copy kernel has
     nothing to move (parallel/ddp.py)."""
-    tag = getattr(p, "_dta_flat", None) if p is not None else None
+    if p is None:
+        return None
+    gdest = getattr(p, "_dta_gdest", None)  # FSDP unit views (parallel/fsdp.py _Unit.piece_dest)
+    if gdest is not None:
+        d = gdest()
+        return d if d is not None and d.dtype == p.dtype else None
+    tag = getattr(p, "_dta_flat", None)
     if tag is None or p.grad is not None:
         return None
     group, i = tag
@@ -344,7 +351,7 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
             return dw, db
         return native().gemm_tn(dy2, x2, False, 0, -1, cw)
-    dw = gemm(dy2, x2, True, True, kind="wgrad")
+    dw = gemm(dy2, x2, True, True, kind="wgrad", out=_grad_dest(w))
     if with_bias:
         return dw, native().bias_grad(dy2, False, -1)
     return dw
@@ -512,6 +519,7 @@ class _LinearCrossEntropy(Function):
         loss_rows = native().cross_entropy_fwd_bwd(logits, logits, target, 1.0, ignore_index, -1)
         ctx.save_for_backward(x2, w, logits, count)
         ctx.xshape = x.shape
+        ctx.wparam = w  # (its gradient may go straight into a flat gradient slice: _grad_dest)
         return loss_rows.sum() / count
 
     @staticmethod
@@ -522,7 +530,7 @@ class _LinearCrossEntropy(Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = gemm(dlogits, x2, True, True, kind="head_wgrad").mul_(s)
+            dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam)).mul_(s)
         return dx, dw, None, None
 
 

@@ -32,6 +32,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import functools
 import logging
 from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Type, Union
 
@@ -59,6 +60,41 @@ def _policy_fn(policy: WrapPolicy) -> Callable[[nn.Module], bool]:
 
 def _align(n: int, a: int) -> int:
     return (n + a - 1) // a * a
+
+
+class _SplitInto(torch.autograd.Function):
+    """A unit's flat parameter -> its per-parameter views (and padding pieces).
+
+    Backward assembles the unit's flat gradient in ONE buffer chosen by the unit
+    (:meth:`_Unit.grad_buffer`: at one rank with fresh gradients, the shard's own
+    slice of the flat gradient -- the gradient is then already where the
+    optimizer reads it).  Pieces whose backward wrote straight into their slice
+    (native Linear / norm backwards asked ``_dta_gdest`` for it) are not copied;
+    the rest are copied in; padding is zeroed.  Autograd's own split backward
+    would instead concatenate every piece into a new tensor (a full pass over
+    the unit's gradient, plus a copy into the flat gradient after it)."""
+
+    @staticmethod
+    def forward(ctx, full, unit):
+        ctx.unit = unit
+        ctx.set_materialize_grads(False)
+        return tuple(full.split(unit._split_sizes))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        u = ctx.unit
+        dest = u.grad_buffer()
+        pos = 0
+        for size, g in zip(u._split_sizes, grads):
+            sl = dest[pos:pos + size]
+            if g is None:
+                sl.zero_()
+            elif g.data_ptr() != sl.data_ptr():
+                sl.copy_(g.reshape(-1))
+            pos += size
+        # a fresh view (its own TensorImpl, referenced only here) so AccumulateGrad
+        # adopts it as full.grad instead of cloning it
+        return dest.view(-1), None
 
 
 class _Unit:
@@ -99,6 +135,8 @@ class _Unit:
         self.full.register_post_accumulate_grad_hook(self._post_backward)
         self._bwd_ready = False
         self.in_backward = False  # between this unit's pre-backward and post-backward
+        self._dest: Optional[torch.Tensor] = None  # this backward's flat gradient buffer (grad_buffer)
+        self._claimed: Set[int] = set()
         # one rank: the shard IS the whole flat parameter, so "gathering" is
         # pointing the unit at the shard's compute copy (no buffer, no copy) --
         # torch's FSDP likewise runs FULL_SHARD as NO_SHARD at world size 1
@@ -158,11 +196,39 @@ class _Unit:
         concatenation -- per-slice views would each allocate a zero-filled
         full-size gradient and add it in (O(params x unit size) traffic)."""
         aliases = self.owner._aliases
-        pieces = self.full.split(self._split_sizes)
-        for (mod, attr, name, _), k, shp in zip(self.entries, self._piece_index, self.shapes):
+        pieces = _SplitInto.apply(self.full, self)
+        for e, ((mod, attr, name, _), k, shp) in enumerate(zip(self.entries, self._piece_index, self.shapes)):
             view = pieces[k].view(shp)
+            view._dta_gdest = functools.partial(self.piece_dest, e)
             for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
                 setattr(m2, a2, view)
+
+    # ---------------------------------------------------------- gradient destination
+    def grad_buffer(self) -> torch.Tensor:
+        """The flat buffer this backward assembles the unit's gradient in: the
+        shard's flat-gradient slice when that is final (one rank, first gradient
+        since zero_grad(set_to_none)), else a temporary (reduce-scatter source /
+        accumulation input)."""
+        if self._dest is None:
+            own = self.owner
+            fg = own.shards
+            i = fg.index_of(self.shard_param)
+            if (own.world_size == 1 and own._grad_fresh and self.index not in own._written
+                    and fg.grad_dtype == self.full.dtype and fg.grad.is_cuda == self.full.is_cuda):
+                self._dest = fg.grad_view(i)
+            else:
+                self._dest = torch.empty(self.total, dtype=self.full.dtype, device=self.full.device)
+            self._claimed = set()
+        return self._dest
+
+    def piece_dest(self, e: int) -> Optional[torch.Tensor]:
+        """Slice of :meth:`grad_buffer` for parameter ``e`` -- once per backward (a
+        second use of the same weight must not overwrite it before autograd sums)."""
+        if e in self._claimed or not self.in_backward:
+            return None
+        self._claimed.add(e)
+        o, n = self.offsets[e], self.numels[e]
+        return self.grad_buffer()[o:o + n].view(self.shapes[e])
 
     # ---------------------------------------------------------- backward
     def _post_backward(self, full: torch.Tensor) -> None:
@@ -170,6 +236,8 @@ class _Unit:
         own._queue_final_callback()
         g = full.grad
         full.grad = None
+        self._dest = None
+        self._claimed = set()
         if own.world_size == 1:  # the whole gradient is this rank's shard: no collective, no copy
             own._pending_rs.append((self, CommWork(), g, g))
         else:

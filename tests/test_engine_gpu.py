@@ -90,7 +90,15 @@ def test_persistent_program_long_run():
     assert int(pa.cursor.item()) == 2500 % pa.R
     la, lb = pa.last_losses(2500).cpu(), pb.last_losses(2500).cpu()
     assert torch.isfinite(la).all()
-    torch.testing.assert_close(la[-200:].mean(), lb[-200:].mean(), rtol=5e-2, atol=1e-3)
+    # the FULL per-step loss sequence: a batch-order / index-ring / launch-boundary bug
+    # shows as a different batch's loss at that step (the two programs only differ in
+    # bf16 rounding order, which drifts slowly); early steps tightly, all steps loosely
+    torch.testing.assert_close(la[:64], lb[:64], rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(la, lb, rtol=5e-2, atol=5e-3)
+    # the per-step loss varies strongly between batches: the two sequences must move together
+    da, db = la[1:] - la[:-1], lb[1:] - lb[:-1]
+    corr = float((da * db).sum() / (da.norm() * db.norm()))
+    assert corr > 0.98, corr
     for (n, p), (_, q) in zip(model_a.named_parameters(), model_b.named_parameters()):
         assert (p - q).abs().max().item() < 3e-2 * max(1.0, q.abs().max().item()), n
 
