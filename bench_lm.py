@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ckpt", action="store_true", help="activation checkpointing")
-    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--bucket-mb", default="auto", help="DDP bucket cap in MiB, or auto (xGMI-derived)")
     ap.add_argument("--layers", type=int, default=0, help="override n_layer (0 = config)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--tunableop", action="store_true",
@@ -113,7 +113,7 @@ def main():
             from distributed_training_amd.parallel.ddp import DistributedDataParallel
 
             wrapped = DistributedDataParallel(model, comm=comm, device=dev, param_dtype=torch.bfloat16,
-                                              bucket_cap_mb=args.bucket_mb, first_bucket_mb=2.0)
+                                              bucket_cap_mb=args.bucket_mb if args.bucket_mb == "auto" else float(args.bucket_mb))
         else:
             from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
 

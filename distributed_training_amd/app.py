@@ -84,6 +84,13 @@ def _wrap_policy(name, model):
     return None
 
 
+def _mb(v):
+    """Bucket size knob: a number of MiB, or "auto" / None (derived for xGMI)."""
+    if v is None or str(v).lower() in ("auto", "none", "null"):
+        return None if v is None or str(v).lower() in ("none", "null") else "auto"
+    return float(v)
+
+
 def training_config_from(cfg, model=None) -> TrainingConfig:
     t = cfg.train
     return TrainingConfig(
@@ -97,8 +104,8 @@ def training_config_from(cfg, model=None) -> TrainingConfig:
         loss=_get(t, "loss", "cross_entropy"),
         fused_step=bool(_get(t, "fused_step", True)),
         graph_steps=int(_get(t, "graph_steps", 32)),
-        bucket_cap_mb=float(_get(t, "bucket_cap_mb", 25)),
-        first_bucket_mb=float(_get(t, "first_bucket_mb", 1)),
+        bucket_cap_mb=_mb(_get(t, "bucket_cap_mb", "auto")),
+        first_bucket_mb=_mb(_get(t, "first_bucket_mb", None)),
         mixed_precision=_get(t, "mixed_precision", None),
         fsdp_wrap=_wrap_policy(_get(t, "fsdp_wrap", None), model),
         log_throughput=bool(_get(t, "log_throughput", False)),

@@ -61,8 +61,8 @@ class TrainingConfig:
     fused_step: bool = True          # fused MLP kernel path when eligible
     fused_optimizer: bool = True     # swap torch optimizers for the HIP ones
     graph_steps: int = 32            # steps per hipGraph replay (fused path)
-    bucket_cap_mb: float = 25.0
-    first_bucket_mb: float = 1.0
+    bucket_cap_mb: Any = "auto"      # MiB, or "auto": sized for xGMI (parallel/flat.py xgmi_bucket_caps)
+    first_bucket_mb: Any = None      # MiB, or None / "auto" (with a numeric cap: 1 MiB like torch)
     mixed_precision: Optional[str] = None   # None / "bf16"
     fsdp_wrap: Optional[Any] = None          # wrap policy for FSDP
     log_throughput: bool = False

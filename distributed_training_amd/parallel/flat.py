@@ -42,7 +42,7 @@ class Bucket:
 class FlatParamGroup:
     def __init__(self, params: Sequence[torch.nn.Parameter], device: torch.device,
                  param_dtype: torch.dtype = torch.float32, grad_dtype: Optional[torch.dtype] = None,
-                 names: Optional[Sequence[str]] = None):
+                 names: Optional[Sequence[str]] = None, pad_after: Optional[Dict[int, int]] = None):
         self.params: List[torch.nn.Parameter] = list(params)
         self.names = list(names) if names is not None else [f"p{i}" for i in range(len(self.params))]
         self.device = device
@@ -52,10 +52,12 @@ class FlatParamGroup:
         self.numels = [p.numel() for p in self.params]
         self.offsets: List[int] = []
         off = 0
-        for n in self.numels:
+        pad_after = pad_after or {}
+        for i, n in enumerate(self.numels):
             self.offsets.append(off)
-            off = _align(off + n)
+            off = _align(off + n, pad_after.get(i, ALIGN_ELEMS))  # bucket ends: world_size x 64 elements
         self.total = max(off, ALIGN_ELEMS)
+        self.pad_after = dict(pad_after)
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
         with torch.no_grad():
             for p, o, n in zip(self.params, self.offsets, self.numels):
@@ -154,6 +156,15 @@ class FlatParamGroup:
         if self.mixed:
             self.master.copy_(self.compute.float())
 
+    def buckets_from_plan(self, plan: Sequence[Sequence[int]]) -> List[Bucket]:
+        """Buckets of :func:`plan_buckets` (each ends at its last parameter's padded end)."""
+        out = []
+        for ids in plan:
+            last = ids[-1]
+            end = _align(self.offsets[last] + self.numels[last], self.pad_after.get(last, ALIGN_ELEMS))
+            out.append(Bucket(len(out), self.offsets[ids[0]], end, list(ids)))
+        return out
+
     def make_buckets(self, order: Sequence[int], cap_bytes: int, first_cap_bytes: int) -> List[Bucket]:
         """Contiguous buckets over the flat buffer (params are laid out in
         ``order``, which callers choose as reverse registration order so the
@@ -207,14 +218,58 @@ def clip_flat_grad_norm_(fg: FlatParamGroup, max_norm: float, comm=None, sharded
     return norm.reshape(())
 
 
+def plan_buckets(numels: Sequence[int], esize: int, cap_bytes: int, first_cap_bytes: int) -> List[List[int]]:
+    """Bucket membership over parameters in layout order: the first bucket closes
+    at ``first_cap_bytes``, later ones at ``cap_bytes`` (torch Reducer rule)."""
+    plan: List[List[int]] = []
+    cur: List[int] = []
+    size, cap = 0, first_cap_bytes
+    for i, n in enumerate(numels):
+        cur.append(i)
+        size += _align(n) * esize
+        if size >= cap:
+            plan.append(cur)
+            cur, size, cap = [], 0, cap_bytes
+    if cur:
+        plan.append(cur)
+    return plan
+
+
+# xGMI model for DDP bucket sizing (SURVEY.md §5.8): one MI355X has 7 point-to-point
+# links of ~153 GB/s; RCCL's multi-channel ring all-reduce reaches a bus bandwidth
+# of roughly 2 links' worth, and each collective costs a fixed ~20 us (launch +
+# protocol latency).  A ring all-reduce of S bytes over N ranks moves 2 (N-1)/N S.
+XGMI_BUS_BW = 300e9
+XGMI_COLL_LATENCY = 20e-6
+
+
+def xgmi_bucket_caps(world_size: int, grad_bytes: int, min_buckets: int = 6) -> Tuple[int, int]:
+    """(first_cap_bytes, cap_bytes) for DDP buckets on one xGMI node:
+    * a steady bucket large enough that the fixed latency is <= 10 % of its
+      transfer time: S >= 10 * latency * bus_bw / (2 (N-1) / N);
+    * but at least ``min_buckets`` buckets per backward so the all-reduces
+      overlap the remaining backward; clamped to [4, 64] MiB;
+    * a first bucket of cap / 16 (>= 1 MiB) so the first collective starts after
+      the last layer's gradients, early in backward."""
+    MiB = 1 << 20
+    n = max(2, world_size)
+    s_lat = 10 * XGMI_COLL_LATENCY * XGMI_BUS_BW / (2.0 * (n - 1) / n)
+    cap = min(s_lat, grad_bytes / max(1, min_buckets))
+    cap = int(min(64 * MiB, max(4 * MiB, cap)))
+    first = max(1 * MiB, cap // 16)
+    return first, cap
+
+
 def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]], device: torch.device,
-                     param_dtype=torch.float32, grad_dtype=None, reverse: bool = True) -> FlatParamGroup:
+                     param_dtype=torch.float32, grad_dtype=None, reverse: bool = True,
+                     pad_after: Optional[Dict[int, int]] = None) -> FlatParamGroup:
     items = list(params_with_names)
     if reverse:
         items = items[::-1]
     names = [n for n, _ in items]
     params = [p for _, p in items]
-    return FlatParamGroup(params, device, param_dtype=param_dtype, grad_dtype=grad_dtype, names=names)
+    return FlatParamGroup(params, device, param_dtype=param_dtype, grad_dtype=grad_dtype, names=names,
+                          pad_after=pad_after)
 
 
 def param_flat_tags(params) -> Dict[int, Tuple[FlatParamGroup, int]]:

@@ -11,7 +11,7 @@ Design (MI355X-first):
   that become their own shard unit; every remaining parameter belongs to the
   root unit.  ``wrap_policy=None`` reproduces the reference's single unit.
 * **Flat shards.** A unit's parameters are laid out in one flat buffer padded
-  to ``world_size x 16`` elements; rank r owns the r-th slice.  All shards of
+  to ``world_size x 64`` elements; rank r owns the r-th slice.  All shards of
   all units are views into ONE flat master buffer (:class:`FlatParamGroup`),
   so the fused optimizer updates the whole sharded model in one launch and,
   under bf16 mixed precision, writes the bf16 all-gather source in the same
@@ -113,7 +113,7 @@ class _Unit:
         for n in self.numels:
             self.offsets.append(off)
             off = _align(off + n, 16)
-        self.total = _align(max(off, 16), ws * 16)
+        self.total = _align(max(off, 16), ws * 64)  # shards: multiples of 64 elements (128-B aligned collectives)
         self.shard_size = self.total // ws
         # split sizes covering [0, total): parameter pieces and padding gaps
         self._split_sizes, self._piece_index = [], []

@@ -71,7 +71,7 @@ class DistributedStrategy(ABC):
 
 
 class DDPStrategy(DistributedStrategy):
-    def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0,
+    def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb="auto", first_bucket_mb=None,
                  mixed_precision: Optional[str] = None, comm: Optional[Communicator] = None):
         self.local_rank = local_rank
         self.is_gpu = is_gpu

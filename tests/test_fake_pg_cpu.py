@@ -35,7 +35,7 @@ def test_fsdp_units_at_world_8(fake_pg):
     assert fs.world_size == 8 and len(fs.units) == cfg.n_layer + 1  # blocks + root
     covered = 0
     for u in fs.units:
-        assert u.total % (8 * 16) == 0 and u.shard_size * 8 == u.total  # 16-element aligned shards
+        assert u.total % (8 * 64) == 0 and u.shard_size * 8 == u.total  # 64-element (128-B bf16) aligned shards
         assert sum(u._split_sizes) == u.total
         assert all(o % 16 == 0 for o in u.offsets)  # every parameter 16-element aligned in the flat unit
         covered += sum(u.numels)
@@ -75,3 +75,41 @@ def test_ddp_buckets_at_world_8(fake_pg):
     lo = ddp(x[:, :-1])
     F.cross_entropy(lo.reshape(-1, lo.shape[-1]), x[:, 1:].reshape(-1)).backward()
     assert all(ddp.flat.grad_is_view(i) for i in range(len(ddp.flat.params)))
+
+
+def test_ddp_buckets_sized_for_xgmi_and_padded():
+    """bucket_cap_mb="auto": caps from the xGMI model (>= 6 buckets of overlap, latency
+    <= 10 % of a bucket), every bucket boundary a multiple of world_size x 64 elements,
+    buckets cover the parameters in reverse registration order without overlap."""
+    import torch.nn as nn
+
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.flat import xgmi_bucket_caps
+
+    class FakeComm:
+        world_size, rank = 8, 0
+
+        def all_reduce(self, t, op="sum"):
+            pass
+
+        def broadcast(self, t, src=0):
+            pass
+
+    model = nn.Sequential(*[nn.Linear(1000, 1003) for _ in range(12)])
+    ddp = DistributedDataParallel(model, comm=FakeComm(), device=torch.device("cpu"), bucket_cap_mb="auto",
+                                  init_sync=False)
+    grad_bytes = sum(p.numel() for p in model.parameters()) * 4
+    first, cap = xgmi_bucket_caps(8, grad_bytes)
+    assert ddp.bucket_bytes == (first, cap) and 4 << 20 <= cap <= 64 << 20
+    assert len(ddp.buckets) >= 3
+    prev_end = 0
+    for b in ddp.buckets:
+        assert b.start == prev_end or b.start % (8 * 64) == 0
+        assert b.end % (8 * 64) == 0, b
+        prev_end = b.end
+        for i in b.param_ids:
+            o, n = ddp.flat.offsets[i], ddp.flat.numels[i]
+            assert b.start <= o and o + n <= b.end
+    ids = [i for b in ddp.buckets for i in b.param_ids]
+    assert ids == list(range(len(ddp.flat.params)))
+    assert ddp.flat.names[0] == "11.bias"  # reverse registration order: last layer's grads fill bucket 0

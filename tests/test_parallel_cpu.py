@@ -101,7 +101,7 @@ def _fsdp_parity(rank, ws, wrap, opt_name, accum=False):
     fs = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={Block} if wrap else None)
     assert len(fs.units) == (4 if wrap else 1)
     for u in fs.units:
-        assert u.total % (ws * 16) == 0 and u.shard_size * ws == u.total
+        assert u.total % (ws * 64) == 0 and u.shard_size * ws == u.total
         assert u.alias == (ws == 1)
     if opt_name == "adamw":
         o1 = torch.optim.AdamW(ref.parameters(), lr=1e-2)
