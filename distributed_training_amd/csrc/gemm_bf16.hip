@@ -189,62 +189,74 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
     // and each SIMD holds one wave of each group, so while one group multiplies
     // the other loads: the MFMA pipe alternates between the two waves of a SIMD.
     //
+    // An MFMA section never waits for LDS reads issued in the load section right
+    // before it (that would idle the pipe for a read latency each phase): the A
+    // fragments and the first B half of stage k are read in L(k-1, 1) into one of
+    // two A register sets, the second B half in L(k, 0).
+    //
     // Barrier numbering (group 0; group 1 is +1): L(k,0) #4k+1 M(k,0) #4k+2
-    // L(k,1) #4k+3 M(k,1) #4k+4.  Stage k+1 is waited for (vmcnt) in L(k,1) by
-    // every wave -> visible after #4k+4, before any L(k+1, .) read.  Stage k+3 is
-    // DMA'd in L(k,1) into the slot of stage k-1, whose last reads (group 1,
-    // L(k-1,1)) retired before #4k+1.
+    // L(k,1) #4k+3 M(k,1) #4k+4.
+    //  * stage k+1 is waited for (vmcnt) in L(k,0) by every wave -> visible after
+    //    #4k+2 (group 1's L(k,0)), before its first reads in L(k,1);
+    //  * stage k+3 is DMA'd in L(k,1) into the slot of stage k-1, whose last reads
+    //    (group 1, L(k-1,0)) retired before group 1's M(k-1,1) ended at #4k+1.
     constexpr int HN = NT / 2;
-    bf16x8 af[MT], bfr[NT];
-    const int pre = min(nk, kGbStages - 1);
-    for (int s = 0; s < pre; ++s) issue(s);
-    if (pre >= 3) vm_wait_n<2 * L>();
-    else if (pre == 2) vm_wait_n<L>();
-    else vm_wait_n<0>();
-    lds_bar();
-    if (wm == 1) lds_bar();
-    for (int kt = 0; kt < nk; ++kt) {
-      const char* sa = lds + (kt & (kGbStages - 1)) * STAGE;
-      const char* sb = sa + A_BYTES;
-      // L(kt, 0)
+    bf16x8 afA[MT], afB[MT], b0[HN], b1[HN];
+    auto slot = [&](int s) { return lds + (s & (kGbStages - 1)) * STAGE; };
+    auto read_a_b0 = [&](int s, bf16x8 (&af)[MT]) {
+      const char* sa = slot(s);
 #pragma unroll
       for (int j = 0; j < MT; ++j) af[j] = frag_a(sa, j);
 #pragma unroll
-      for (int i = 0; i < HN; ++i) bfr[i] = frag_b(sb, i);
-      lds_bar();
-      // M(kt, 0)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int i = 0; i < HN; ++i) b0[i] = frag_b(sa + A_BYTES, i);
+    };
+    auto read_b1 = [&](int s) {
+#pragma unroll
+      for (int i = 0; i < HN; ++i) b1[i] = frag_b(slot(s) + A_BYTES, HN + i);
+    };
+    auto mma_half = [&](const bf16x8 (&af)[MT], const bf16x8 (&bh)[HN], int i0) {
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < HN; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < MT; ++j)
+          acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[i], af[j], acc[i0 + i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+    };
+    auto vm_stages = [&](int ahead) {
+      if (ahead >= 2) vm_wait_n<2 * L>();
+      else if (ahead == 1) vm_wait_n<L>();
+      else vm_wait_n<0>();
+    };
+    const int pre = min(nk, kGbStages - 1);
+    for (int s = 0; s < pre; ++s) issue(s);
+    vm_stages(pre - 1);  // stage 0 landed (this wave's part)
+    lds_bar();
+    read_a_b0(0, afA);
+    if (wm == 1) lds_bar();
+    // one stage; A fragments of stage kt in `ca`, those of kt+1 go to `na`
+    auto stage = [&](int kt, const bf16x8 (&ca)[MT], bf16x8 (&na)[MT]) {
+      // L(kt, 0)
+      if (kt + 1 < nk) vm_stages(min(nk - 1, kt + kGbStages - 2) - (kt + 1));
+      read_b1(kt);
+      lds_bar();
+      // M(kt, 0)
+      mma_half(ca, b0, 0);
       lds_bar();
       // L(kt, 1)
-#pragma unroll
-      for (int i = HN; i < NT; ++i) bfr[i] = frag_b(sb, i);
       if (kt + kGbStages - 1 < nk) issue(kt + kGbStages - 1);
-      if (kt + 1 < nk) {
-        const int ahead = min(nk - 1, kt + kGbStages - 1) - (kt + 1);
-        if (ahead >= 2) vm_wait_n<2 * L>();
-        else if (ahead == 1) vm_wait_n<L>();
-        else vm_wait_n<0>();
-      }
+      read_a_b0(kt + 1, na);  // (past the last stage: a stale slot, never multiplied; unconditional keeps
+                              //  the LDS-read count static so hipcc's lgkmcnt waits stay partial)
       lds_bar();
       // M(kt, 1)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = HN; i < NT; ++i)
-#pragma unroll
-        for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
+      mma_half(ca, b1, HN);
       lds_bar();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      stage(kt, afA, afB);
+      if (kt + 1 < nk) stage(kt + 1, afB, afA);
     }
     if (wm == 0) lds_bar();  // same barrier count for both groups
   } else {
