@@ -58,7 +58,11 @@ class ModelCheckpoint:
         logger.info("Loading snapshot")
         # tensors stay on the host: the strategy copies each into place (an 8B-parameter
         # FSDP snapshot would otherwise be materialised on every rank's GPU at once)
-        snapshot = torch.load(self.path, map_location="cpu", weights_only=True)
+        # memory-mapped: each rank pages in only what it copies (an FSDP rank reads its shard ranges)
+        try:
+            snapshot = torch.load(self.path, map_location="cpu", weights_only=True, mmap=True)
+        except RuntimeError:  # legacy (non-zip) format cannot be mapped
+            snapshot = torch.load(self.path, map_location="cpu", weights_only=True)
         model, epochs = self.strategy.load_checkpoint(model, snapshot, device)
         if optimizer is not None and "OPTIM_STATE" in snapshot:
             self.strategy.load_optim_state(model, optimizer, snapshot["OPTIM_STATE"])
