@@ -990,8 +990,10 @@ static dta::MlpPArgs make_mlp_pargs(torch::Tensor Xp, torch::Tensor T, torch::Te
     }
   }
   if (dbg && dbg->defined()) {
-    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 && dbg->numel() >= (dbg_step < 0 ? 72 : 64),
-                "dbg: int64 [64] (step stamps) or [72] (dbg_step < 0: launch timeline stamps at 64..68)");
+    TORCH_CHECK(dbg->is_cuda() && dbg->scalar_type() == torch::kInt64 &&
+                    dbg->numel() >= (dbg_step == -2 ? 80 : dbg_step < 0 ? 72 : 64),
+                "dbg: int64 [64] (step stamps), [72] (dbg_step -1: launch timeline stamps at 64..68, "
+                "s_memrealtime) or [80] (dbg_step -2: also s_memtime core-clock stamps at 72..76)");
     a.dbg = reinterpret_cast<unsigned long long*>(dbg->data_ptr<int64_t>());
     a.dbg_step = (int)dbg_step;
   }

@@ -103,20 +103,76 @@ __global__ void __launch_bounds__(kLinThreads) linear_step_kernel(LinStepArgs a)
     __syncthreads();
   }
   const int cur0 = *a.cursor;
+  // Prefetch pipeline (batch rows fit KX / KT registers per thread, e.g. 32 x 20):
+  // the next step's sampler indices load while this step's logits are formed and
+  // its feature / target rows while this step's loss and gradients are -- the two
+  // dependent global round trips of a gather leave the step's critical path.
+  constexpr int KX = 4, KT = 1;
+  const bool pf = a.B * I <= KX * kLinThreads && a.B * C <= KT * kLinThreads;
+  int rx[KX], rt[KT], nb_next = 0;
+  float xr[KX], tr[KT];
+  auto fetch_idx = [&](int s) {  // sampler rows of step s (ring rows are B wide; unused entries are 0)
+    const int slot = (cur0 + s) % a.R;
+    const int* idx = a.ring + (int64_t)slot * a.B;
+    nb_next = a.counts[slot];
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      const int e = tid + k * kLinThreads;
+      rx[k] = e < a.B * I ? idx[e / I] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int e = tid + k * kLinThreads;
+      rt[k] = e < a.B * C ? idx[e / C] : 0;
+    }
+  };
+  auto fetch_rows = [&]() {
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      const int e = tid + k * kLinThreads;
+      if (e < nb_next * I) xr[k] = a.X[(int64_t)rx[k] * I + (e % I)];
+    }
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int e = tid + k * kLinThreads;
+      if (e < nb_next * C) tr[k] = a.T[(int64_t)rt[k] * C + (e % C)];
+    }
+  };
+  if (pf && a.nsteps > 0) {
+    fetch_idx(0);
+    fetch_rows();
+  }
   for (int s = 0; s < a.nsteps; ++s) {
     const int slot = (cur0 + s) % a.R;
-    const int nb = a.counts[slot];
-    const int* idx = a.ring + (int64_t)slot * a.B;
-    // gather this step's rows (features and targets) into LDS
-    for (int e = tid; e < nb * I; e += kLinThreads) {
-      const int b = e / I, i = e - b * I;
-      x_s[e] = a.X[(int64_t)idx[b] * I + i];
-    }
-    for (int e = tid; e < nb * C; e += kLinThreads) {
-      const int b = e / C, c = e - b * C;
-      t_s[e] = a.T[(int64_t)idx[b] * C + c];
+    int nb;
+    if (pf) {
+      nb = nb_next;
+#pragma unroll
+      for (int k = 0; k < KX; ++k) {
+        const int e = tid + k * kLinThreads;
+        if (e < nb * I) x_s[e] = xr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const int e = tid + k * kLinThreads;
+        if (e < nb * C) t_s[e] = tr[k];
+      }
+    } else {
+      nb = a.counts[slot];
+      const int* idx = a.ring + (int64_t)slot * a.B;
+      // gather this step's rows (features and targets) into LDS
+      for (int e = tid; e < nb * I; e += kLinThreads) {
+        const int b = e / I, i = e - b * I;
+        x_s[e] = a.X[(int64_t)idx[b] * I + i];
+      }
+      for (int e = tid; e < nb * C; e += kLinThreads) {
+        const int b = e / C, c = e - b * C;
+        t_s[e] = a.T[(int64_t)idx[b] * C + c];
+      }
     }
     __syncthreads();
+    const bool more = pf && s + 1 < a.nsteps;
+    if (more) fetch_idx(s + 1);
     // logits
     for (int e = tid; e < nb * C; e += kLinThreads) {
       const int b = e / C, c = e - b * C;
@@ -127,6 +183,7 @@ __global__ void __launch_bounds__(kLinThreads) linear_step_kernel(LinStepArgs a)
       z_s[e] = z;
     }
     __syncthreads();
+    if (more) fetch_rows();  // (its indices arrived during the logits)
     // loss and dz (one thread per row)
     float lsum = 0.f;
     for (int b = tid; b < nb; b += kLinThreads) {

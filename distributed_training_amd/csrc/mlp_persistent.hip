@@ -78,7 +78,10 @@ __device__ __forceinline__ void lds_barrier() {
 // launch-timeline stamps (diagnostic build of one launch: dbg_step < 0), s_memrealtime (100 MHz)
 #define MP_TSTAMP(k)                                                                        \
   do {                                                                                      \
-    if (a.dbg && a.dbg_step < 0 && tid == 0) a.dbg[64 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.dbg && a.dbg_step < 0 && tid == 0) {                                              \
+      a.dbg[64 + (k)] = __builtin_amdgcn_s_memrealtime();                                   \
+      if (a.dbg_step == -2) a.dbg[72 + (k)] = __builtin_amdgcn_s_memtime();                 \
+    }                                                                                       \
   } while (0)
 
 #define MP_STAMP(k)                                                                             \

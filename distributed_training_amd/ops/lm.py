@@ -243,9 +243,52 @@ def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 
     return {k: sorted(v)[len(v) // 2] for k, v in res.items()}
 
 
+_CACHE_LOADED = [False]
+
+
+def _cache_path() -> Optional[str]:
+    return os.environ.get("DTA_GEMM_CACHE") or None
+
+
+def _load_cache() -> None:
+    """``DTA_GEMM_CACHE=file.json``: per-shape choices measured by an earlier run on this
+    kind of GPU (keys ``kind MxNxK``), so a run (or a profile) skips the timing."""
+    _CACHE_LOADED[0] = True
+    path = _cache_path()
+    if not path or not os.path.exists(path):
+        return
+    import json
+
+    try:
+        with open(path) as f:
+            for k, v in json.load(f).items():
+                kind, dims = k.rsplit(" ", 1)
+                M, N, K = (int(x) for x in dims.split("x"))
+                _GEMM_CHOICE.setdefault((kind, M, N, K), int(v))
+    except (OSError, ValueError):
+        pass
+
+
+def _save_cache() -> None:
+    path = _cache_path()
+    if not path:
+        return
+    import json
+
+    tmp = f"{path}.tmp{os.getpid()}"
+    try:
+        with open(tmp, "w") as f:
+            json.dump({f"{k[0]} {k[1]}x{k[2]}x{k[3]}": v for k, v in sorted(_GEMM_CHOICE.items())}, f, indent=0)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
 def _pick(kind: str, M: int, N: int, K: int, run_dta: Callable[[int], object], run_torch: Callable[[], object]) -> int:
     """Implementation for one GEMM shape: the dta tile that measured fastest, or 0
     (hipBLASLt) when the library is faster / the shape is not covered."""
+    if not _CACHE_LOADED[0]:
+        _load_cache()
     key = (kind, M, N, K)
     c = _GEMM_CHOICE.get(key)
     if c is not None:
@@ -267,6 +310,8 @@ def _pick(kind: str, M: int, N: int, K: int, run_dta: Callable[[int], object], r
         if c and times[c] > 0.98 * times[0]:
             c = 0
     _GEMM_CHOICE[key] = c
+    if mode == "auto":
+        _save_cache()
     return c
 
 
