@@ -113,6 +113,7 @@ def training_config_from(cfg, model=None) -> TrainingConfig:
         save_optimizer=bool(_get(t, "save_optimizer", False)),
         desync_check_every=int(_get(t, "desync_check_every", 0) or 0),
         fault_injection=_get(t, "fault_injection", None),
+        cpu_offload=bool(_get(t, "cpu_offload", False)),
     )
 
 

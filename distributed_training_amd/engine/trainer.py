@@ -70,6 +70,7 @@ class TrainingConfig:
     save_optimizer: bool = False
     desync_check_every: int = 0
     fault_injection: Optional[Dict[str, int]] = None
+    cpu_offload: bool = False        # FSDP: fp32 shards, gradients and optimizer on the host
     extra: Dict[str, Any] = field(default_factory=dict)
 
 
@@ -122,7 +123,8 @@ class Trainer:
     def _make_strategy(self) -> DistributedStrategy:
         c = self.config
         if c.parallel_strategy.lower() == "fsdp":
-            return FSDPStrategy(self.env.is_gpu, wrap_policy=c.fsdp_wrap, mixed_precision=c.mixed_precision)
+            return FSDPStrategy(self.env.is_gpu, wrap_policy=c.fsdp_wrap, mixed_precision=c.mixed_precision,
+                                cpu_offload=c.cpu_offload)
         return DDPStrategy(self.env.local_rank, self.env.is_gpu, bucket_cap_mb=c.bucket_cap_mb,
                            first_bucket_mb=c.first_bucket_mb, mixed_precision=c.mixed_precision)
 
@@ -146,7 +148,7 @@ class Trainer:
         new_params = [p for p in model.parameters() if p.requires_grad]
         same = {id(p) for p in original_params} == {id(p) for p in new_params}
         fused = isinstance(self.optimizer, (FusedSGD, FusedAdamW))
-        want_fused = self.config.fused_optimizer and self.env.is_gpu
+        want_fused = self.config.fused_optimizer and self.env.is_gpu and all(p.is_cuda for p in new_params)
         if same and (fused or not want_fused):
             return
         if want_fused or not same:

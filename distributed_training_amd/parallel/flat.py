@@ -42,7 +42,8 @@ class Bucket:
 class FlatParamGroup:
     def __init__(self, params: Sequence[torch.nn.Parameter], device: torch.device,
                  param_dtype: torch.dtype = torch.float32, grad_dtype: Optional[torch.dtype] = None,
-                 names: Optional[Sequence[str]] = None, pad_after: Optional[Dict[int, int]] = None):
+                 names: Optional[Sequence[str]] = None, pad_after: Optional[Dict[int, int]] = None,
+                 pin_memory: bool = False):
         self.params: List[torch.nn.Parameter] = list(params)
         self.names = list(names) if names is not None else [f"p{i}" for i in range(len(self.params))]
         self.device = device
@@ -59,12 +60,16 @@ class FlatParamGroup:
         self.total = max(off, ALIGN_ELEMS)
         self.pad_after = dict(pad_after)
         self.master = torch.zeros(self.total, dtype=torch.float32, device=device)
+        if pin_memory and self.master.device.type == "cpu":  # host-resident shards (FSDP cpu_offload)
+            self.master = self.master.pin_memory()
         with torch.no_grad():
             for p, o, n in zip(self.params, self.offsets, self.numels):
                 self.master[o:o + n].copy_(p.detach().reshape(-1).to(torch.float32))
         self.mixed = param_dtype != torch.float32
         self.compute = self.master if not self.mixed else self.master.to(param_dtype)
         self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=device)
+        if pin_memory and self.grad.device.type == "cpu":
+            self.grad = self.grad.pin_memory()
         # set by an engine whose backward hooks move fresh gradients into the
         # flat buffer (DDP): zero_grad(set_to_none=True) may then drop the views
         self.steal_ok = False
@@ -211,7 +216,13 @@ def clip_flat_grad_norm_(fg: FlatParamGroup, max_norm: float, comm=None, sharded
     else:
         sq = g.float().pow(2).sum().reshape(1)
     if sharded and comm is not None and comm.world_size > 1:
-        comm.all_reduce(sq, op="sum")
+        dev = getattr(comm, "device", None)
+        if dev is not None and sq.device != torch.device(dev):  # host-resident shards, device communicator
+            sq_d = sq.to(dev)
+            comm.all_reduce(sq_d, op="sum")
+            sq = sq_d.to(sq.device)
+        else:
+            comm.all_reduce(sq, op="sum")
     norm = sq.sqrt()
     coef = (float(max_norm) / (norm + 1e-6)).clamp(max=1.0)
     g.mul_(coef.to(g.dtype))

@@ -26,6 +26,13 @@ Design (MI355X-first):
 * **Full state dict** is gathered on ALL ranks (collective) and materialised
   on rank 0 only -- fixing the reference's rank-0-only deadlock (SURVEY.md
   §0 item 4, Q2).  Keys are the original, unprefixed parameter names.
+* **CPU offload** (``cpu_offload=True``; the reference passes
+  ``CPUOffload(offload_params=True)``, fsdp_strategy.py:23-25): the fp32 shards,
+  their gradients and the optimizer live in pinned host memory.  A unit's
+  shard is copied host -> device right before its all-gather, the
+  reduce-scattered gradient device -> host after backward, and the optimizer
+  (a torch optimizer over host tensors) steps on the CPU -- the GPU holds only
+  the gathered units in flight and the activations.
 * **Module-state sync.** Parameters are broadcast from rank 0 before sharding
   (the reference's FSDP has ``sync_module_states=False`` with unseeded init,
   so its replicas start different -- SURVEY.md Q7).
@@ -140,7 +147,7 @@ class _Unit:
         # one rank: the shard IS the whole flat parameter, so "gathering" is
         # pointing the unit at the shard's compute copy (no buffer, no copy) --
         # torch's FSDP likewise runs FULL_SHARD as NO_SHARD at world size 1
-        self.alias = ws == 1
+        self.alias = ws == 1 and not owner.cpu_offload
         if self.alias:
             self.full.untyped_storage().resize_(0)  # until unshard() points it at the shard
         self.free()  # storage exists only while the unit is gathered
@@ -160,10 +167,14 @@ class _Unit:
 
     # ---------------------------------------------------------- gather
     def shard_source(self) -> torch.Tensor:
-        """This rank's shard in compute dtype (the all-gather input)."""
+        """This rank's shard in compute dtype (the all-gather input; with CPU
+        offload, copied from pinned host memory onto the device first)."""
         fg: FlatParamGroup = self.owner.shards
         i = fg.index_of(self.shard_param)
-        return fg.param_view(i)
+        src = fg.param_view(i)
+        if src.device != self.full.device:
+            src = src.to(self.full.device, non_blocking=True)
+        return src
 
     def unshard(self, async_op: bool = False) -> None:
         if self.gathered or self.pending is not None:
@@ -177,6 +188,10 @@ class _Unit:
             self.gathered = True
             return
         self._alloc()
+        if self.owner.world_size == 1:  # (CPU offload at one rank) the shard is the whole unit
+            self.full.data.copy_(self.shard_source())
+            self.gathered = True
+            return
         with prof.range_(f"fsdp.unit{self.index}.allgather"):
             work = self.owner.comm.all_gather_into(self.full.data, self.shard_source(), async_op=True)
         self.pending = work
@@ -214,7 +229,7 @@ class _Unit:
             fg = own.shards
             i = fg.index_of(self.shard_param)
             if (own.world_size == 1 and own._grad_fresh and self.index not in own._written
-                    and fg.grad_dtype == self.full.dtype and fg.grad.is_cuda == self.full.is_cuda):
+                    and fg.grad_dtype == self.full.dtype and fg.grad.device == self.full.device):
                 self._dest = fg.grad_view(i)
             else:
                 self._dest = torch.empty(self.total, dtype=self.full.dtype, device=self.full.device)
@@ -245,7 +260,8 @@ class _Unit:
             # keeping: reduce-scatter straight into this unit's slice of it
             fg = own.shards
             i = fg.index_of(self.shard_param)
-            direct = own._grad_fresh and fg.grad_dtype == g.dtype and self.index not in own._written
+            direct = (own._grad_fresh and fg.grad_dtype == g.dtype and self.index not in own._written
+                      and fg.grad.device == g.device)
             out = fg.grad_view(i) if direct else torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
             if direct:
                 own._written.add(self.index)
@@ -264,8 +280,12 @@ class FullyShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Communicator] = None,
                  device: Optional[torch.device] = None, wrap_policy: WrapPolicy = None,
                  param_dtype: torch.dtype = torch.float32, reshard_after_forward: bool = True,
-                 prefetch: bool = True, sync_module_states: bool = True):
+                 prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False):
         super().__init__()
+        self.cpu_offload = bool(cpu_offload)
+        if self.cpu_offload and param_dtype != torch.float32:
+            raise NotImplementedError("FSDP cpu_offload keeps fp32 shards on the host (like the reference's "
+                                      "CPUOffload with fp32 FSDP); bf16 mixed precision is not offloaded")
         self.comm = comm or TorchComm()
         self.world_size = self.comm.world_size
         self.rank = self.comm.rank
@@ -349,7 +369,13 @@ class FullyShardedDataParallel(nn.Module):
                     # (e.g. an optimizer built before wrapping): 8B params = 32 GB of fp32
                     p.data = torch.empty(0, dtype=p.dtype, device=p.device)
                 u.entries = [(m, a, n, None) for m, a, n, _ in u.entries]
-        self.shards = FlatParamGroup(shard_params, self.device, param_dtype=param_dtype, names=names)
+        shard_dev = torch.device("cpu") if self.cpu_offload else self.device
+        if self.cpu_offload:
+            shard_params = [nn.Parameter(p.detach().cpu()) for p in shard_params]
+            for u, sp in zip(self.units, shard_params):
+                u.shard_param = sp
+        self.shards = FlatParamGroup(shard_params, shard_dev, param_dtype=param_dtype, names=names,
+                                     pin_memory=self.cpu_offload)
         self.shards.fresh_hook = self._mark_grads_fresh
         self.shard_params = nn.ParameterList(shard_params)
         if sync_module_states and self.world_size > 1:
@@ -468,15 +494,15 @@ class FullyShardedDataParallel(nn.Module):
                 if fg.params[i].grad is None or not fg.grad_is_view(i):
                     fg.params[i].grad = gv
                 if out.data_ptr() != gv.data_ptr():  # (reduce-scattered in place otherwise)
-                    gv.copy_(out)
+                    gv.copy_(out, non_blocking=True)
                 done.add(u.index)
                 self._written.add(u.index)
             elif fresh:
-                gv.add_(out.to(gv.dtype))
+                gv.add_(out.to(gv.device, gv.dtype))
             else:
                 if not fg.grad_is_view(i):
                     fg.rebind_grad(i)
-                gv.add_(out.to(gv.dtype))
+                gv.add_(out.to(gv.device, gv.dtype))
             del g
         if fresh:
             for u in self.units:  # units without a gradient this backward: zeros, as torch would accumulate
@@ -490,6 +516,8 @@ class FullyShardedDataParallel(nn.Module):
         self._cb_queued = False
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()
+        if self.cpu_offload and self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()  # host gradients complete before a CPU step
         for u in self.units:  # any unit not used in backward: drop its gathered copy
             u.in_backward = False
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):
@@ -524,7 +552,7 @@ class FullyShardedDataParallel(nn.Module):
         keep = (not rank0_only) or self.rank == 0
         for u in self.units:
             i = fg.index_of(u.shard_param)
-            shard = fg.master_view(i).contiguous()
+            shard = fg.master_view(i).contiguous().to(self.device)
             full = torch.empty(u.total, dtype=torch.float32, device=self.device)
             self.comm.all_gather_into(full, shard)
             if keep:
@@ -590,7 +618,7 @@ class FullyShardedDataParallel(nn.Module):
                 v = st[k]
                 if isinstance(v, torch.Tensor) and v.numel() == u.shard_size:
                     full = torch.empty(u.total, dtype=torch.float32, device=self.device)
-                    self.comm.all_gather_into(full, v.reshape(-1).float().contiguous())
+                    self.comm.all_gather_into(full, v.reshape(-1).float().contiguous().to(self.device))
                     if keep:
                         for (_, _, name, _), o, n, shp in zip(u.entries, u.offsets, u.numels, u.shapes):
                             out_state.setdefault(name, {})[k] = full[o:o + n].view(shp).cpu().clone()
@@ -625,7 +653,8 @@ class FullyShardedDataParallel(nn.Module):
                     full = torch.zeros(u.total, dtype=torch.float32, device=self.device)
                     for v, o, n in zip(vals, u.offsets, u.numels):
                         full[o:o + n].copy_(v.reshape(-1).to(self.device, torch.float32))
-                    ent[k] = full[self.rank * u.shard_size:(self.rank + 1) * u.shard_size].clone()
+                    ent[k] = full[self.rank * u.shard_size:(self.rank + 1) * u.shard_size].clone().to(
+                        u.shard_param.device)
                 else:
                     ent[k] = next(v for v in vals if v is not None)
             local[pid[id(u.shard_param)]] = ent

@@ -100,8 +100,12 @@ class DDPStrategy(DistributedStrategy):
 
 class FSDPStrategy(DistributedStrategy):
     def __init__(self, is_gpu: bool, wrap_policy=None, mixed_precision: Optional[str] = None,
-                 reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None):
+                 reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None,
+                 cpu_offload: bool = False):
         self.is_gpu = is_gpu
+        # the reference offloads only when there is no GPU (fsdp_strategy.py:23-25), where this
+        # engine's shards live on the host anyway; on a GPU run it is an explicit opt-in
+        self.cpu_offload = cpu_offload
         self.wrap_policy = wrap_policy
         self.param_dtype = _DTYPES[mixed_precision] if mixed_precision else torch.float32
         self.reshard_after_forward = reshard_after_forward
@@ -116,7 +120,8 @@ class FSDPStrategy(DistributedStrategy):
         comm = self.comm or default_comm(dev)
         return FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=self.wrap_policy,
                                         param_dtype=self.param_dtype,
-                                        reshard_after_forward=self.reshard_after_forward, prefetch=self.prefetch)
+                                        reshard_after_forward=self.reshard_after_forward, prefetch=self.prefetch,
+                                        cpu_offload=self.cpu_offload and dev.type == "cuda")
 
     def model_state(self, model: Module) -> Dict[str, torch.Tensor]:
         # FULL_STATE_DICT, offload_to_cpu=True, rank0_only=True (fsdp_strategy.py:31-35) -- on all ranks

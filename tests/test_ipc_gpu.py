@@ -277,3 +277,45 @@ def _engine_worker(rank, ws, strategy):
 @pytest.mark.parametrize("strategy", ["ddp", "fsdp"])
 def test_engines_multi_rank_shared_gpu(strategy, ws):
     run_gloo(_engine_worker, ws, strategy)
+
+
+def _offload_worker(rank, ws, opt_name):
+    from distributed_training_amd.parallel.comm import make_comm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    dev = _shared() if ws > 1 else torch.device("cuda", 0)
+    comm = make_comm(dev) if ws > 1 else None
+
+    def build():
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 256), torch.nn.ReLU(),
+                                torch.nn.Linear(256, 8)).to(dev)
+        return m
+
+    g = torch.Generator().manual_seed(7 + rank)
+    batches = [(torch.randn(16, 64, generator=g).to(dev), torch.randn(16, 8, generator=g).to(dev)) for _ in range(4)]
+    finals = []
+    for offload in (False, True):
+        m = build()
+        kw = {"comm": comm} if comm is not None else {}
+        f = FullyShardedDataParallel(m, device=dev, wrap_policy={torch.nn.Linear}, cpu_offload=offload, **kw)
+        assert all(p.device.type == ("cpu" if offload else "cuda") for p in f.parameters())
+        opt = (torch.optim.SGD(f.parameters(), lr=0.05, momentum=0.9) if opt_name == "sgd"
+               else torch.optim.AdamW(f.parameters(), lr=1e-2))
+        for x, y in batches:
+            opt.zero_grad(set_to_none=True)
+            torch.nn.functional.mse_loss(f(x), y).backward()
+            opt.step()
+        sd = f.full_state_dict(rank0_only=False, offload_to_cpu=True)
+        finals.append(torch.cat([v.reshape(-1).float() for v in sd.values()]))
+    torch.testing.assert_close(finals[1], finals[0], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("ws,opt_name", [(1, "sgd"), (1, "adamw"), (2, "adamw")])
+def test_fsdp_cpu_offload_matches_device_shards(ws, opt_name):
+    """FSDP with the fp32 shards, gradients and a torch optimizer in pinned host memory
+    (the reference's CPUOffload(offload_params=True)) trains exactly like device shards."""
+    if ws == 1:
+        _offload_worker(0, 1, opt_name)
+    else:
+        run_gloo(_offload_worker, ws, opt_name)
