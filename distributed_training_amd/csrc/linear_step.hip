@@ -27,6 +27,8 @@
 // global round trips between phases.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dta {
 
 struct LinStepArgs {
@@ -59,6 +61,19 @@ __device__ __forceinline__ float sgd_update(float p, float g, float* m, bool sta
   if (m) {
     const float buf = started ? a.momentum * (*m) + (1.f - a.dampening) * d : d;
     *m = buf;
+    d = a.nesterov ? d + a.momentum * buf : buf;
+  }
+  return p - a.lr * d;
+}
+
+// same update, momentum as a (register-resident) reference; `use_m` = momentum buffer present
+__device__ __forceinline__ float sgd_update_r(float p, float g, float& m, bool use_m, bool started,
+                                              const LinStepArgs& a) {
+  float d = a.maximize ? -g : g;
+  if (a.weight_decay != 0.f) d += a.weight_decay * p;
+  if (use_m) {
+    const float buf = started ? a.momentum * m + (1.f - a.dampening) * d : d;
+    m = buf;
     d = a.nesterov ? d + a.momentum * buf : buf;
   }
   return p - a.lr * d;
@@ -248,6 +263,175 @@ __global__ void __launch_bounds__(kLinThreads) linear_step_kernel(LinStepArgs a)
   }
 }
 
+// ------------------------------------------------------------------ one-wave form
+// For the reference's own shapes (Linear(20, 1), batch 32) the whole step fits
+// ONE wavefront with no LDS and no barrier: lane b owns batch row b (its
+// features in registers), every lane holds the (uniform) parameters and
+// momenta in registers, the forward is I FMAs per logit, the loss is per lane,
+// and each weight / bias gradient is one DPP wave reduction (sum over the
+// batch lanes) -- the C*I+C reductions are independent and interleave.  The
+// next step's sampler row and feature row are loaded while this step computes
+// (two named register sets).  ~20x fewer instructions on the step's critical
+// path than the workgroup form above (LDS round trips + 5 barriers).
+constexpr int kWI = 32, kWC = 1;  // register-resident limits: in_dim <= 32, out_dim 1, batch <= 64
+
+__global__ void __launch_bounds__(64) linear_step_wave_kernel(LinStepArgs a) {
+  const int lane = threadIdx.x;
+  const int I = a.I, C = a.C;
+  const bool mom = a.M != nullptr;
+  float w[kWC][kWI], bb[kWC], mw[kWC][kWI], mb[kWC];
+#pragma unroll
+  for (int c = 0; c < kWC; ++c) {
+#pragma unroll
+    for (int i = 0; i < kWI; ++i) {
+      const bool live = c < C && i < I;
+      w[c][i] = live ? a.P[c * I + i] : 0.f;
+      mw[c][i] = live && mom ? a.M[c * I + i] : 0.f;
+    }
+    bb[c] = c < C ? a.P[C * I + c] : 0.f;
+    mb[c] = c < C && mom ? a.M[C * I + c] : 0.f;
+  }
+  bool started = mom ? (a.flags[0] != 0) : false;
+  if (a.G_in != nullptr && a.flags[1] != 0) {  // per-step form: the previous step's all-reduced update
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) {
+      if (c >= C) continue;
+#pragma unroll
+      for (int i = 0; i < kWI; ++i)
+        if (i < I) w[c][i] = sgd_update_r(w[c][i], a.G_in[c * I + i], mw[c][i], mom, started, a);
+      bb[c] = sgd_update_r(bb[c], a.G_in[C * I + c], mb[c], mom, started, a);
+    }
+    started = true;
+  }
+  const int cur0 = *a.cursor;
+  int lc = *a.loss_cursor;
+  // three-stage gather pipeline: the sampler row (and batch size) of step s+2 and the
+  // feature / target row of step s+1 are in flight while step s computes, so no step
+  // waits on a dependent chain of global loads
+  auto fetch_idx = [&](int s, int& r, int& nb) {
+    const int slot = (cur0 + s) % a.R;
+    nb = a.counts[slot];
+    r = a.ring[(int64_t)slot * a.B + (lane < a.B ? lane : 0)];
+  };
+  auto fetch_row = [&](int r, int nb, float (&x)[kWI], float (&t)[kWC]) {
+    const bool live = lane < nb;
+    const float* row = a.X + (int64_t)(live ? r : 0) * I;  // I % 4 == 0: 16-byte row pieces
+#pragma unroll
+    for (int j = 0; j < kWI / 4; ++j) {
+      const float4 v = (live && 4 * j < I) ? *reinterpret_cast<const float4*>(row + 4 * j)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[4 * j] = v.x;
+      x[4 * j + 1] = v.y;
+      x[4 * j + 2] = v.z;
+      x[4 * j + 3] = v.w;
+    }
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) t[c] = (live && c < C) ? a.T[(int64_t)r * C + c] : 0.f;
+  };
+  auto step = [&](const float (&x)[kWI], const float (&t)[kWC], int nb) {
+    const bool valid = lane < nb;
+    float z[kWC], dz[kWC];
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) {
+      z[c] = bb[c];
+#pragma unroll
+      for (int i = 0; i < kWI; ++i) z[c] = fmaf(x[i], w[c][i], z[c]);
+    }
+    float lsum = 0.f;
+    if (a.loss_kind == 1) {
+      float mx = z[0];
+#pragma unroll
+      for (int c = 1; c < kWC; ++c)
+        if (c < C) mx = fmaxf(mx, z[c]);
+      float se = 0.f, ts = 0.f;
+#pragma unroll
+      for (int c = 0; c < kWC; ++c)
+        if (c < C) {
+          se += __expf(z[c] - mx);
+          ts += t[c];
+        }
+      const float lse = mx + __logf(se);
+      const float inv = 1.f / (float)nb;
+#pragma unroll
+      for (int c = 0; c < kWC; ++c) {
+        lsum -= c < C ? t[c] * (z[c] - lse) : 0.f;  // log_softmax first: one logit -> exactly 0
+        dz[c] = (valid && c < C) ? (__expf(z[c] - lse) * ts - t[c]) * inv : 0.f;
+      }
+    } else {
+      const float inv = 2.f / (float)(nb * C);
+#pragma unroll
+      for (int c = 0; c < kWC; ++c) {
+        const float d = c < C ? z[c] - t[c] : 0.f;
+        lsum += d * d;
+        dz[c] = (valid && c < C) ? d * inv : 0.f;
+      }
+    }
+    const float ltot = wave_sum(valid ? lsum : 0.f);
+    if (lane == 0) a.loss_ring[lc % a.loss_len] = a.loss_kind == 1 ? ltot / (float)nb : ltot / (float)(nb * C);
+    ++lc;
+    // gradients: one wave reduction each (uniform result in every lane)
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) {
+      if (c >= C) continue;
+#pragma unroll
+      for (int i = 0; i < kWI; ++i) {
+        if (i >= I) continue;
+        const float g = wave_sum(dz[c] * x[i]);
+        if (a.G_out) {
+          if (lane == 0) a.G_out[c * I + i] = g * a.grad_scale;
+        } else {
+          w[c][i] = sgd_update_r(w[c][i], g, mw[c][i], mom, started, a);
+        }
+      }
+      const float gb = wave_sum(dz[c]);
+      if (a.G_out) {
+        if (lane == 0) a.G_out[C * I + c] = gb * a.grad_scale;
+      } else {
+        bb[c] = sgd_update_r(bb[c], gb, mb[c], mom, started, a);
+      }
+    }
+    if (!a.G_out) started = true;
+  };
+  float x0[kWI], t0[kWC], x1[kWI], t1[kWC];
+  int r1 = 0, nb0 = 0, nb1 = 0, r2 = 0, nb2 = 0;
+  if (a.nsteps > 0) {
+    int r0;
+    fetch_idx(0, r0, nb0);
+    fetch_row(r0, nb0, x0, t0);
+  }
+  if (a.nsteps > 1) fetch_idx(1, r1, nb1);
+  for (int s = 0; s < a.nsteps; ++s) {
+    if (s + 2 < a.nsteps) fetch_idx(s + 2, r2, nb2);
+    if (s + 1 < a.nsteps) fetch_row(r1, nb1, x1, t1);
+    step(x0, t0, nb0);
+#pragma unroll
+    for (int i = 0; i < kWI; ++i) x0[i] = x1[i];
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) t0[c] = t1[c];
+    nb0 = nb1;
+    r1 = r2;
+    nb1 = nb2;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < kWC; ++c) {
+      if (c >= C) continue;
+#pragma unroll
+      for (int i = 0; i < kWI; ++i)
+        if (i < I) {
+          a.P[c * I + i] = w[c][i];
+          if (mom) a.M[c * I + i] = mw[c][i];
+        }
+      a.P[C * I + c] = bb[c];
+      if (mom) a.M[C * I + c] = mb[c];
+    }
+    *a.cursor = cur0 + a.nsteps;
+    *a.loss_cursor = lc;
+    if (mom && started) a.flags[0] = 1;
+    if (a.G_in) a.flags[1] = (a.G_out != nullptr && a.nsteps > 0) ? 1 : 0;
+  }
+}
+
 }  // namespace dta
 
 using namespace dta;
@@ -266,6 +450,12 @@ int dta_linear_step_supported(int I, int C, int B, int momentum) {
 hipError_t dta_linear_step(const LinStepArgs* a, hipStream_t st) {
   if (!dta_linear_step_supported(a->I, a->C, a->B, a->M != nullptr) || a->nsteps < 0 || a->R < 1)
     return hipErrorInvalidValue;
+  static const bool wave_off = getenv("DTA_LINEAR_WAVE") && getenv("DTA_LINEAR_WAVE")[0] == '0';
+  if (!wave_off && a->I <= kWI && a->I % 4 == 0 && a->C <= kWC && a->B <= 64 &&
+      reinterpret_cast<uintptr_t>(a->X) % 16 == 0) {  // the reference's own shapes
+    hipLaunchKernelGGL(linear_step_wave_kernel, dim3(1), dim3(64), 0, st, *a);
+    return hipGetLastError();
+  }
   const size_t lds = dta_linear_step_lds_bytes(a->I, a->C, a->B, a->M != nullptr);
   if (lds > 64 * 1024) {
     static bool raised = false;  // dynamic LDS above 64 KiB must be opted into once
