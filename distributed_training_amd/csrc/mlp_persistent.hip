@@ -97,12 +97,27 @@ __device__ __forceinline__ int img_off(int row, int col, int IMG) {
   return row * IMG + (((col >> 2) ^ ((row >> 1) & 7)) << 2) + (col & 3);
 }
 
-// bf16 W1 image [H][32] (the forward's A operand, 64-B rows): the 16-byte
-// chunk of element (h, k) is XOR-swizzled by (h >> 2) & 3, so the 16 rows one
-// ds_read_b128 lane group reads land on 16 distinct bank slots (unswizzled,
-// four rows share each slot: 4-way).
-__device__ __forceinline__ int wb_off(int h, int k) {
-  return h * 32 + ((((k >> 3) ^ ((h >> 2) & 3))) << 3) + (k & 7);
+// bf16 W1 image [32 k][WS] (k >= in zero, WS = H rounded up to 64): input
+// features as rows, so the forward reads its A operand (lane: hidden row h, 8
+// consecutive k) with transposed reads like the gradient GEMMs', and the lane
+// that owns W1[h][k] (column k of the weight-gradient accumulator, 4 consecutive
+// h per register group) writes its updated rows as one 8-byte store per group
+// instead of four 2-byte ones.  The 8-byte granule of (k, h) is XOR-swizzled
+// within its 16-granule group by (5k) & 15 (4k ^ k): both the owners' stores and
+// the transposed reads are at most 2-way (scripts/lds_banks.py model), with no
+// padding, so the image costs what the old [H][32] one did.
+__device__ __forceinline__ int wb_stride(int H) { return (H + 63) & ~63; }
+__device__ __forceinline__ int wb_off(int h, int k, int WS) {
+  return k * WS + (((h >> 2) ^ (((4 * k) ^ k) & 15)) << 2) + (h & 3);
+}
+
+__device__ __forceinline__ bf16x8 wb_trfrag(const bf16* W, int WS, int s, int h0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int k = 16 * s + 8 * (g >> 1) + (i >> 2);
+  const int h = h0 + 16 * (g & 1) + 4 * (i & 3);
+  const bf16x4 lo = mp_tr4(W + wb_off(h, k, WS));
+  const bf16x4 hi = mp_tr4(W + wb_off(h, k + 4, WS));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
 __device__ __forceinline__ bf16x8 img_trfrag(const bf16* X, int IMG, int s, int c0, int lane) {
@@ -300,7 +315,7 @@ __device__ void xreduce_sgd(const MlpPArgs& a, unsigned ep, float* Pf, float* Mf
         }
         p -= hs.lr * g;
         Pf[o] = p;
-        if (j < a.hidden * a.in_dim) Wb[wb_off(j / a.in_dim, j % a.in_dim)] = f2bf(p);
+        if (j < a.hidden * a.in_dim) Wb[wb_off(j / a.in_dim, j % a.in_dim, wb_stride(a.hidden))] = f2bf(p);
       }
     }
   }
@@ -413,10 +428,11 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     return;
   }
 
+  constexpr bool multi = XM != 0;  // DDP across ranks (a.world > 1)
   // ---- LDS carve ----
   float* Pf = reinterpret_cast<float*>(smem);                       // [total]
-  float* Mf = Pf + a.total;                                         // [total] if momentum
-  char* q = reinterpret_cast<char*>(Mf + (a.M ? a.total : 0));
+  float* Mf = Pf + a.total;  // [total] momenta, several ranks only (one rank: registers)
+  char* q = reinterpret_cast<char*>(Mf + (a.M && multi ? a.total : 0));
   bf16* Xs = reinterpret_cast<bf16*>(q);                            // [2][32][kMpXs]
   q += 2 * 32 * kMpXs * 2;
   bf16* Img = reinterpret_cast<bf16*>(q);                           // [32][IMG]
@@ -429,12 +445,12 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   q += 2 * 32 * OUT * 4;
   float* lossbuf = reinterpret_cast<float*>(q);                     // [1]
   q += 16;
-  bf16* Wb = reinterpret_cast<bf16*>(q);                            // [H][32] bf16 W1 (k >= in zero)
+  bf16* Wb = reinterpret_cast<bf16*>(q);                            // [32][WS] bf16 W1^T (k >= in zero)
+  const int WS = wb_stride(H);
 
   int c0 = *a.cursor;
   int lcur = *a.loss_cursor;
   int first = a.M ? (*a.mom_started == 0) : 0;
-  constexpr bool multi = XM != 0;  // DDP across ranks (a.world > 1)
   const unsigned xe0 = multi ? (unsigned)*a.xepoch : 0u;
 
   // ---- batch pipeline: idx two steps ahead, features one step ahead ----
@@ -490,7 +506,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
       float4 pv[kLd], mv[kLd];
 #pragma unroll
       for (int j = 0; j < kLd; ++j) pv[j] = P4[min(base + j * kMpThreads + tid, nv - 1)];
-      if (a.M) {
+      if (multi && a.M) {
 #pragma unroll
         for (int j = 0; j < kLd; ++j) mv[j] = M4[min(base + j * kMpThreads + tid, nv - 1)];
       }
@@ -499,7 +515,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         const int i = base + j * kMpThreads + tid;
         if (i < nv) {
           Pf[4 * i] = pv[j].x; Pf[4 * i + 1] = pv[j].y; Pf[4 * i + 2] = pv[j].z; Pf[4 * i + 3] = pv[j].w;
-          if (a.M) {
+          if (multi && a.M) {
             Mf[4 * i] = mv[j].x; Mf[4 * i + 1] = mv[j].y; Mf[4 * i + 2] = mv[j].z; Mf[4 * i + 3] = mv[j].w;
           }
         }
@@ -507,17 +523,18 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     }
     for (int i = 4 * nv + tid; i < a.total; i += kMpThreads) {
       Pf[i] = a.P[i];
-      if (a.M) Mf[i] = a.M[i];
+      if (multi && a.M) Mf[i] = a.M[i];
     }
   }
   __syncthreads();
   MP_TSTAMP(1);
-  for (int i = tid; i < H * 4; i += kMpThreads) {  // from the LDS copy: no second HBM pass
-    const int h = i >> 2, k0 = (i & 3) * 8;        // one 16-B chunk (8 k) of row h per iteration
-    bf16x8 v;
+  for (int i = tid; i < 32 * (WS / 4); i += kMpThreads) {  // from the LDS copy: no second HBM pass
+    const int k = i / (WS / 4), h = 4 * (i % (WS / 4));       // 4 consecutive h of input feature k
+    if (h >= H) continue;
+    bf16x4 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = f2bf(k0 + j < IN ? Pf[a.o_w1 + h * IN + k0 + j] : 0.f);
-    *reinterpret_cast<bf16x8*>(Wb + wb_off(h, k0)) = v;
+    for (int j = 0; j < 4; ++j) v[j] = f2bf(k < IN ? Pf[a.o_w1 + (h + j) * IN + k] : 0.f);
+    *reinterpret_cast<bf16x4*>(Wb + wb_off(h, k, WS)) = v;
   }
   if (gthr) store_rows(0);
   if (tid == 0) *lossbuf = 0.f;
@@ -525,12 +542,46 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   MP_TSTAMP(2);
 
   const SgdH hbase{a.lr, a.momentum, a.dampening, a.weight_decay, a.nesterov, a.maximize, 0};
+  // One rank: the fp32 master parameters (and momenta) a lane updates stay in its
+  // registers for the whole launch -- lane (column c = lane & 31) of wave w owns, for
+  // each of its tiles, the 16 accumulator rows of column c of the gradient GEMMs
+  // (W1[h][c], b1[h] or W2[h]); the LDS copy is only the forward's view of b1 / W2
+  // and the bf16 W1 image.  Written back to LDS after the loop.
+  const int own_c = r32;
+  const bool own = own_c <= IN + 1;
+  const int own_base = own_c < IN ? a.o_w1 + own_c : (own_c == IN ? a.o_b1 : a.o_w2);
+  const int own_stride = own_c < IN ? IN : 1;
+  float preg[TPW][16], mreg[TPW][16];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      preg[tt][i] = 0.f;
+      mreg[tt][i] = 0.f;
+    }
+  if constexpr (!multi) {
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int t = wave + kMpWaves * tt;
+      if (t < NT && own) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = own_base + (t * 32 + mfma32_row(i, lane)) * own_stride;
+          preg[tt][i] = Pf[off];
+          if (!PLAIN && a.M) mreg[tt][i] = a.M[off];
+        }
+      }
+    }
+  }
   const float lscale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
 
   // static priority for the younger half of the workgroup (MI355X_MICROARCH "Two waves per
   // SIMD" item 4): one s_setprio before the loop, wave-uniform guard, no per-phase flips
   if (a.prio_young && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   float dy_keep[OUT], loss_keep = 0.f;  // one rank: wave 0's dY / loss, finished after its backward
+  float mb2[OUT];                       // one rank: the output bias' momenta (wave 0, lane 0)
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) mb2[o] = (!multi && !PLAIN && a.M && tid == 0) ? a.M[a.o_b2 + o] : 0.f;
 #pragma unroll
   for (int o = 0; o < OUT; ++o) dy_keep[o] = 0.f;
   for (int s = 0; s < a.nsteps; ++s) {
@@ -566,8 +617,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           w2v[4 * g] = wv.x; w2v[4 * g + 1] = wv.y; w2v[4 * g + 2] = wv.z; w2v[4 * g + 3] = wv.w;
         }
         // A operand W1: lane (row h = h0 + r32), k = 16ks + 8hh + j: one 16-B read of the bf16 image
-        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(Wb + wb_off(h0 + r32, hh * 8)), xb0, acc);
-        acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(Wb + wb_off(h0 + r32, 16 + hh * 8)), xb1, acc);
+        acc = mfma32x32x16(wb_trfrag(Wb, WS, 0, h0, lane), xb0, acc);
+        acc = mfma32x32x16(wb_trfrag(Wb, WS, 1, h0, lane), xb1, acc);
         hpre[tt] = acc;
         // layer 2 partial: y[sample] += W2[h] * act(hpre[h][sample]) over this lane's 16 rows
 #pragma unroll
@@ -735,37 +786,35 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
               xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, from_c2 ? c2[i] : c1[i]);
           }
         } else if (upd) {
+          // one rank: register-resident parameters (see the prologue); only b1 / W2 go
+          // back to LDS (the forward's and the next backward's view), W1 to its bf16 image
+          const bool w1col = c < IN;
 #pragma unroll
-          for (int half = 0; half < 2; ++half) {  // 8 parameters at a time: all read, then all written
-            float pv[8], mv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int off = pbase + (h0 + mfma32_row(8 * half + u, lane)) * pstride;
-              pv[u] = Pf[off];
-              mv[u] = PLAIN ? 0.f : Mf[off];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int i = 8 * half + u;
-              float g = from_c2 ? c2[i] : c1[i];
-              if (!PLAIN) {
-                if (hs.maximize) g = -g;
-                if (hs.wd != 0.f) g += hs.wd * pv[u];
-                if (hs.mom != 0.f) {
-                  mv[u] = hs.first ? g : hs.mom * mv[u] + (1.f - hs.damp) * g;
-                  g = hs.nesterov ? g + hs.mom * mv[u] : mv[u];
-                }
+          for (int i = 0; i < 16; ++i) {
+            float g = from_c2 ? c2[i] : c1[i];
+            if (!PLAIN) {
+              if (hs.maximize) g = -g;
+              if (hs.wd != 0.f) g += hs.wd * preg[tt][i];
+              if (hs.mom != 0.f) {
+                mreg[tt][i] = hs.first ? g : hs.mom * mreg[tt][i] + (1.f - hs.damp) * g;
+                g = hs.nesterov ? g + hs.mom * mreg[tt][i] : mreg[tt][i];
               }
-              pv[u] -= hs.lr * g;
             }
+            preg[tt][i] -= hs.lr * g;
+          }
+          if (w1col) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int h = h0 + mfma32_row(8 * half + u, lane);
-              const int off = pbase + h * pstride;
-              Pf[off] = pv[u];
-              if (!PLAIN && hs.mom != 0.f) Mf[off] = mv[u];
-              if (c < IN) Wb[wb_off(h, c)] = f2bf(pv[u]);
-            }
+            for (int g = 0; g < 4; ++g)  // rows h0 + 8g + 4hh + 0..3
+              *reinterpret_cast<bf16x4*>(Wb + wb_off(h0 + 8 * g + 4 * hh, c, WS)) =
+                  bf16x4{f2bf(preg[tt][4 * g]), f2bf(preg[tt][4 * g + 1]), f2bf(preg[tt][4 * g + 2]),
+                         f2bf(preg[tt][4 * g + 3])};
+          } else {
+            // rows 8g + 4hh + 0..3 are consecutive: 16-byte stores
+            float* dst = Pf + pbase + h0 + 4 * hh;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              *reinterpret_cast<float4*>(dst + 8 * g) =
+                  make_float4(preg[tt][4 * g], preg[tt][4 * g + 1], preg[tt][4 * g + 2], preg[tt][4 * g + 3]);
           }
         }
         if (tt == 0) MP_STAMP(7);
@@ -836,7 +885,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
                 const int off = pbase + hrow * pstride;
                 Pf[off] = pv[u];
                 if (!PLAIN && hs2.mom != 0.f) Mf[off] = mv[u];
-                if (c < IN) Wb[wb_off(hrow, c)] = f2bf(pv[u]);
+                if (c < IN) Wb[wb_off(hrow, c, WS)] = f2bf(pv[u]);
               }
             }
           }
@@ -861,7 +910,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           if (lane == 0) {
             SgdH hb = hbase;
             hb.first = first;
-            sgd_apply(Pf + a.o_b2 + o, Mf + a.o_b2 + o, db, hb);
+            sgd_apply(Pf + a.o_b2 + o, &mb2[o], db, hb);
           }
         }
         const float lsum = wave_sum(loss_keep);
@@ -877,11 +926,29 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     // rows of W1 / b1 / W2 (updated above by this wave) and b2 / the next batch
     // tile, both published before barrier 2 of this step
   }
+  if constexpr (!multi) {  // register-resident parameters back into the LDS copy
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int t = wave + kMpWaves * tt;
+      if (t < NT && own) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = own_base + (t * 32 + mfma32_row(i, lane)) * own_stride;
+          Pf[off] = preg[tt][i];
+          if (!PLAIN && a.M) a.M[off] = mreg[tt][i];
+        }
+      }
+    }
+  }
   __syncthreads();
   MP_TSTAMP(3);
   for (int i = tid; i < a.total; i += kMpThreads) {
     a.P[i] = Pf[i];
-    if (a.M) a.M[i] = Mf[i];
+    if (multi && a.M) a.M[i] = Mf[i];
+  }
+  if (!multi && !PLAIN && a.M && tid == 0) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) a.M[a.o_b2 + o] = mb2[o];
   }
   if (tid == 0) {
     if (multi) *a.xepoch = (int)(xe0 + (unsigned)a.nsteps);
@@ -898,7 +965,8 @@ using namespace dta;
 
 size_t dta_mlp_persistent_lds_bytes(int total, int hidden, int out_dim, int has_mom) {
   return (size_t)total * 4 * (has_mom ? 2 : 1) + 2 * 32 * kMpXs * 2 + 32 * (hidden + kMpImgPad) * 2 +
-         kMpWaves * out_dim * 32 * 4 + out_dim * 32 * 4 + 2 * 32 * out_dim * 4 + 16 + (size_t)hidden * 32 * 2;
+         kMpWaves * out_dim * 32 * 4 + out_dim * 32 * 4 + 2 * 32 * out_dim * 4 + 16 +
+         (size_t)32 * ((hidden + 63) & ~63) * 2;
 }
 
 template <int ACT, int OUT, int TPW, bool PLAIN, int XM>
@@ -937,7 +1005,8 @@ hipError_t dta_mlp_persistent(const MlpPArgs* a, int act, hipStream_t st) {
       a->out_dim != 1 || a->hidden > 512 ||
       a->nsteps < 1)
     return hipErrorInvalidValue;
-  const size_t lds = dta_mlp_persistent_lds_bytes(a->total, a->hidden, a->out_dim, a->M != nullptr);
+  // momenta live in LDS only with several ranks (one rank: in the owning lanes' registers)
+  const size_t lds = dta_mlp_persistent_lds_bytes(a->total, a->hidden, a->out_dim, a->M != nullptr && a->world > 1);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   switch (act) {
     case ACT_NONE: return mp_launch_out<ACT_NONE>(*a, lds, st);

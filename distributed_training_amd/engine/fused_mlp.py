@@ -111,7 +111,7 @@ class FusedMLPProgram:
         if persistent is None:
             persistent = os.environ.get("DTA_MLP_PERSISTENT", "1") != "0"
         self.persistent = bool(persistent and full_batches and mf.persistent_supported(
-            module.input_size, H, module.output_size, self.B, momentum=bool(self.hyper()["momentum"])))
+            module.input_size, H, module.output_size, self.B, momentum=bool(self.hyper()["momentum"]), world=self.ws))
         self._p2p = None
         self._xinfo = None
         self._xinfos = {}

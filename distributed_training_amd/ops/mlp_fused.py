@@ -89,13 +89,15 @@ def supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool
     )
 
 
-def persistent_supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool = False) -> bool:
-    """Shapes served by the persistent single-workgroup loop (csrc/mlp_persistent.hip)."""
+def persistent_supported(in_dim: int, hidden: int, out_dim: int, batch: int, momentum: bool = False,
+                         world: int = 1) -> bool:
+    """Shapes served by the persistent single-workgroup loop (csrc/mlp_persistent.hip);
+    SGD momenta take LDS only with several ranks (one rank keeps them in registers)."""
     if not (1 <= in_dim and in_dim + 1 + out_dim <= 32 and out_dim == 1 and hidden % 32 == 0
             and 32 <= hidden <= 512 and 1 <= batch <= 32):
         return False
     total = make_layout(in_dim, hidden, out_dim).total
-    return native().mlp_persistent_lds_bytes(total, hidden, out_dim, int(momentum)) <= LDS_LIMIT
+    return native().mlp_persistent_lds_bytes(total, hidden, out_dim, int(momentum and world > 1)) <= LDS_LIMIT
 
 
 def pad_features(X: torch.Tensor) -> torch.Tensor:

@@ -6,7 +6,9 @@ reads (ds_read_b64_tr_b16, operand with k = token) and the register-staged
 16-byte stores (ds_write_b128).
 
     python scripts/lds_banks.py            # search swizzles for D = 64 and 128
+    python scripts/lds_banks.py w1img      # persistent-MLP W1 image (csrc/mlp_persistent.hip wb_off)
 """
+import sys
 import itertools
 
 B128_GROUPS = [
@@ -114,5 +116,28 @@ def main():
         print("  best:", best)
 
 
+def w1img():
+    """Persistent-MLP bf16 W1 image [32 k][WS]: the owners' 8-byte stores (lane l: row k = l & 31,
+    h = h0 + 8g + 4(l >> 5)) and the forward's transposed reads (16-lane group g, lane 4q + p:
+    row 16s + 8(g >> 1) + q (+4), h = h0 + 16(g & 1) + 4p); cycles per 32-lane half (1 = free)."""
+    for H in range(32, 513, 32):
+        WS = (H + 63) & ~63
+
+        def off(h, k):
+            return 2 * (k * WS + (((h >> 2) ^ (((4 * k) ^ k) & 15)) << 2) + (h & 3))
+
+        st = rd = 0
+        for h0 in range(0, H, 32):
+            for g in range(4):
+                a = [off(h0 + 8 * g + 4 * (l >> 5), l & 31) for l in range(64)]
+                st = max(st, cycles(a, HALVES, 8, 64) // 2)
+            for s_ in range(2):
+                for hi in range(2):
+                    a = [off(h0 + 16 * ((l >> 4) & 1) + 4 * (l & 3), 16 * s_ + 8 * (l >> 5) + ((l & 15) >> 2) + 4 * hi)
+                         for l in range(64)]
+                    rd = max(rd, cycles(a, HALVES, 8, 64) // 2)
+        print(f"H={H:3d} WS={WS:3d}: store {st}  tr-read {rd}")
+
+
 if __name__ == "__main__":
-    main()
+    w1img() if sys.argv[1:] == ["w1img"] else main()
