@@ -22,6 +22,22 @@ __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 // Plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) at -O3.
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// Four floats -> bf16x4 through two-wide vector conversions (one v_cvt_pk_bf16_f32
+// per pair; the scalar casts above pair their results up with an extra v_perm)
+__device__ __forceinline__ bf16x4 pk4_bf16(float a, float b, float c, float d) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+  const h2 lo = __builtin_convertvector(f2{a, b}, h2);
+  const h2 hi = __builtin_convertvector(f2{c, d}, h2);
+  return bf16x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// ReLU as one integer max on the bits (negative floats are negative int32s; -0 -> +0):
+// x > 0 ? x : 0 compiles to a canonicalising v_max_f32 pair
+__device__ __forceinline__ float relu1(float x) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
+}
+
 // 8-element vector load/store with fp32 conversion (16-byte bf16 / 32-byte fp32)
 __device__ __forceinline__ void load8(const bf16* p, float* f) {
   const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);

@@ -84,10 +84,18 @@ __device__ __forceinline__ void lds_barrier() {
     }                                                                                       \
   } while (0)
 
+// per-step phase stamps: only in a build with -DDTA_MP_PHASES (scripts/headline_clock.py
+// phases); the default build keeps their compares and branches out of the step loop
+#ifdef DTA_MP_PHASES
 #define MP_STAMP(k)                                                                             \
   do {                                                                                          \
     if (a.dbg && s == a.dbg_step && lane == 0) a.dbg[wave * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+#else
+#define MP_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
 // Activation image [32 samples][IMG]: 8-byte granules XOR-swizzled by row so
 // the per-lane column writes (32 lanes = 32 rows of one granule column) spread
@@ -622,7 +630,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         hpre[tt] = acc;
         // layer 2 partial: y[sample] += W2[h] * act(hpre[h][sample]) over this lane's 16 rows
 #pragma unroll
-        for (int i = 0; i < 16; ++i) yp[0] += w2v[i] * act_fwd(ACT, acc[i]);
+        for (int i = 0; i < 16; ++i) yp[0] += w2v[i] * (ACT == ACT_RELU ? relu1(acc[i]) : act_fwd(ACT, acc[i]));
       }
     }
 #pragma unroll
@@ -737,15 +745,20 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         for (int g = 0; g < 4; ++g) {
           const float4 wv = *reinterpret_cast<const float4*>(Pf + a.o_w2 + h0 + 8 * g + 4 * hh);  // pre-update W2
           const float w2g[4] = {wv.x, wv.y, wv.z, wv.w};
-          bf16x4 hv;
+          float av[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g + e;
             const float x = hpre[tt][i];
-            hv[e] = f2bf(act_fwd(ACT, x));
-            dh[i] = w2g[e] * dyv * act_bwd(ACT, x);
+            if constexpr (ACT == ACT_RELU) {  // max, mul, compare + select
+              av[e] = relu1(x);
+              dh[i] = x > 0.f ? w2g[e] * dyv : 0.f;
+            } else {
+              av[e] = act_fwd(ACT, x);
+              dh[i] = w2g[e] * dyv * act_bwd(ACT, x);
+            }
           }
-          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = hv;
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = pk4_bf16(av[0], av[1], av[2], av[3]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // gradient GEMMs: rows = hidden units of this tile, columns = [X | 1 | dY]
@@ -757,8 +770,8 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // act(H) reads done before dH overwrites the image
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const bf16x4 dv = {f2bf(dh[4 * g]), f2bf(dh[4 * g + 1]), f2bf(dh[4 * g + 2]), f2bf(dh[4 * g + 3])};
-          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = dv;
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) =
+              pk4_bf16(dh[4 * g], dh[4 * g + 1], dh[4 * g + 2], dh[4 * g + 3]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (tt == 0) MP_STAMP(6);
@@ -806,8 +819,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
 #pragma unroll
             for (int g = 0; g < 4; ++g)  // rows h0 + 8g + 4hh + 0..3
               *reinterpret_cast<bf16x4*>(Wb + wb_off(h0 + 8 * g + 4 * hh, c, WS)) =
-                  bf16x4{f2bf(preg[tt][4 * g]), f2bf(preg[tt][4 * g + 1]), f2bf(preg[tt][4 * g + 2]),
-                         f2bf(preg[tt][4 * g + 3])};
+                  pk4_bf16(preg[tt][4 * g], preg[tt][4 * g + 1], preg[tt][4 * g + 2], preg[tt][4 * g + 3]);
           } else {
             // rows 8g + 4hh + 0..3 are consecutive: 16-byte stores
             float* dst = Pf + pbase + h0 + 4 * hh;

@@ -66,7 +66,8 @@ if __name__ == "__main__" and len(sys.argv) == 1:
 
 
 def phases():
-    """Per-wave phase stamps (s_memtime) of one step inside a 64-step launch:
+    """Per-wave phase stamps (s_memtime) of one step inside a 64-step launch (needs an
+    extension built with -DDTA_MP_PHASES: the stamps are compiled out by default):
     0 step start, 1 forward done, 2 after barrier 1, 3 loss phase done, 4 after
     barrier 2, 6 first tile's act-grad GEMM done, 7 first tile's SGD done, 5 step end."""
     from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
