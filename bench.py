@@ -290,8 +290,11 @@ def main():
     barrier()
     t0 = time.perf_counter()
     step_fn(args.steps)
+    th = time.perf_counter()
     barrier()
     t1 = time.perf_counter()
+    if os.environ.get("DTA_BENCH_TRACE"):
+        print(f"[bench] host call {1e6 * (th - t0):.1f} us, wait {1e6 * (t1 - th):.1f} us", file=sys.stderr)
     elapsed = t1 - t0
     if ws > 1:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)

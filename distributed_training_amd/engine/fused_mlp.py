@@ -22,6 +22,8 @@ from __future__ import annotations
 import contextlib
 import logging
 import os
+import sys
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -31,6 +33,7 @@ from ..ops import mlp_fused as mf
 from ..ops import native
 
 logger = logging.getLogger(__name__)
+_TRACE = bool(os.environ.get("DTA_BENCH_TRACE"))
 
 
 def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torch.device) -> Optional[str]:
@@ -456,6 +459,7 @@ class FusedMLPProgram:
     # ------------------------------------------------------------ stepping API
     @torch.no_grad()
     def _run_persistent(self, n: int) -> None:
+        _T = [time.perf_counter()] if _TRACE else None
         end = self.launched + n
         hp = self.hyper()
         if self.launched == 0 and self._up_stream is not None:
@@ -478,12 +482,20 @@ class FusedMLPProgram:
                     self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor, self.mom_started_dev,
                     self.P[0], self.M[0], self.layout, self.B, self.act, self.loss, 1.0 / self.ws, hp,
                     xinfo=self._xinfo))
+            if _T is not None:
+                _T.append(time.perf_counter())
             self._plaunch[1].launch(k)
+            if _T is not None:
+                _T.append(time.perf_counter())
             self._last_start = self.launched
             for j in range(k):
                 self._batch_of.pop(self.launched + j, None)
             self.launched += k
             self._prefetch()
+        if _T is not None:
+            _T.append(time.perf_counter())
+            print("[fused_mlp] run_persistent us:", [round(1e6 * (b - a), 1) for a, b in zip(_T, _T[1:])],
+                  file=sys.stderr)
 
     def _prefetch(self) -> None:
         """Pipelined index loading: while a launch runs, upload the indices of

@@ -73,7 +73,7 @@ def _compile_cmds() -> List[tuple]:
     hip_flags = [
         hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC",
         "-munsafe-fp-atomics", f"-I{CSRC}",
-    ]
+    ] + os.environ.get("DTA_HIP_EXTRA_FLAGS", "").split()  # e.g. -DDTA_MP_PHASES (diagnostic builds)
     cxx = os.environ.get("CXX", "g++")
     cpp_flags = [
         cxx, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
