@@ -457,11 +457,14 @@ class FusedMLPProgram:
             self._upload_epoch()
 
     # ------------------------------------------------------------ stepping API
-    @torch.no_grad()
     def _run_persistent(self, n: int) -> None:
+        # (no autograd context: only native launches and plain copies happen here, and
+        # the timed region of a short bench call is a few dozen microseconds)
         _T = [time.perf_counter()] if _TRACE else None
         end = self.launched + n
-        hp = self.hyper()
+        g = self.opt.param_groups[0]
+        hkey = (g["lr"], g.get("momentum", 0.0), g.get("dampening", 0.0), g.get("weight_decay", 0.0),
+                g.get("nesterov", False), g.get("maximize", False))
         if self.launched == 0 and self._up_stream is not None:
             # first call (warm-up): upload two launches of indices before the first
             # launch, so later short calls find them in place and the device is not
@@ -476,8 +479,9 @@ class FusedMLPProgram:
                 if not self._up_done.query():
                     torch.cuda.current_stream(self.device).wait_event(self._up_done)
                 self._up_done = None
-            key = (id(self._xinfo), tuple(sorted(hp.items())))
+            key = (id(self._xinfo), hkey)
             if self._plaunch is None or self._plaunch[0] != key:
+                hp = self.hyper()
                 self._plaunch = (key, mf.persistent_prepare(
                     self.Xp, self.Y, self.ring, self.cursor, self.loss_ring, self.loss_cursor, self.mom_started_dev,
                     self.P[0], self.M[0], self.layout, self.B, self.act, self.loss, 1.0 / self.ws, hp,
@@ -517,12 +521,15 @@ class FusedMLPProgram:
         if ep is not None:
             sampler.set_epoch(ep)
 
-    @torch.no_grad()
     def run_steps(self, n: int) -> None:
         """Enqueue ``n`` training steps (crossing epochs as needed)."""
         if self.persistent:
             self._run_persistent(n)
             return
+        self._run_eager(n)
+
+    @torch.no_grad()
+    def _run_eager(self, n: int) -> None:
         end = self.launched + n
         while self.launched < end:
             U = self.graph_steps
