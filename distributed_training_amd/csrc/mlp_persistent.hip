@@ -729,11 +729,27 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
     //   c < IN: W1[h][c] (from dW1 = C1)   c == IN: b1[h] (C1)   c == IN + 1: W2[0][h] (C2)
     const int c = r32;
     const bool upd = c <= IN + 1;
-    const bool from_c2 = c == IN + 1;
     const int pbase = c < IN ? a.o_w1 + c : (c == IN ? a.o_b1 : a.o_w2);
     const int pstride = c < IN ? IN : 1;
     // B operand [X | 1 | dY] of both gradient GEMMs (same for every tile)
     const bf16x8 xf0 = mp_trfrag(Xb, 0, 0, lane), xf1 = mp_trfrag(Xb, 1, 0, lane);
+    // ONE accumulator per tile for both weight gradients: act(H)^T . [0 | 0 | dY] then
+    // dH^T . [X | 1 | 0] -- column c of the sum is dW2 for c == in + 1 and dW1 / db1 for
+    // c <= in, so every owner lane reads its gradient from the same registers (no
+    // per-element select between two accumulators)
+    const bool dycol = c == IN + 1;
+    bf16x8 yf0, yf1, zf0, zf1;  // (one rank; the exchange forms select between two accumulators)
+#pragma unroll
+    for (int j = 0; j < 8 && !multi; ++j) {
+      yf0[j] = dycol ? xf0[j] : f2bf(0.f);
+      yf1[j] = dycol ? xf1[j] : f2bf(0.f);
+      zf0[j] = dycol ? f2bf(0.f) : xf0[j];
+      zf1[j] = dycol ? f2bf(0.f) : xf1[j];
+    }
+    // One rank: ONE accumulator per tile for both weight gradients (masked B operands
+    // above); the exchange forms select between two (their push code needs the
+    // registers the masked operands take).
+    if constexpr (!multi) {
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
       const int t = wave + kMpWaves * tt;
@@ -750,9 +766,10 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g + e;
             const float x = hpre[tt][i];
-            if constexpr (ACT == ACT_RELU) {  // max, mul, compare + select
-              av[e] = relu1(x);
-              dh[i] = x > 0.f ? w2g[e] * dyv : 0.f;
+            if constexpr (ACT == ACT_RELU) {  // max, mul, compare + mask (a select here became a branch
+              av[e] = relu1(x);                // around the W2 load)
+              const float prod = w2g[e] * dyv;
+              dh[i] = __builtin_bit_cast(float, __builtin_bit_cast(int, prod) & (x > 0.f ? -1 : 0));
             } else {
               av[e] = act_fwd(ACT, x);
               dh[i] = w2g[e] * dyv * act_bwd(ACT, x);
@@ -761,50 +778,27 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = pk4_bf16(av[0], av[1], av[2], av[3]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // gradient GEMMs: rows = hidden units of this tile, columns = [X | 1 | dY]
-        f32x16 c2, c1;
+        f32x16 gacc;  // act(H)^T . [0 | 0 | dY], then += dH^T . [X | 1 | 0]
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c2[i] = c1[i] = 0.f;
-        c2 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c2);
-        c2 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c2);
+        for (int i = 0; i < 16; ++i) gacc[i] = 0.f;
+        gacc = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), yf0, gacc);
+        gacc = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), yf1, gacc);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // act(H) reads done before dH overwrites the image
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < 4; ++g)
           *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) =
               pk4_bf16(dh[4 * g], dh[4 * g + 1], dh[4 * g + 2], dh[4 * g + 3]);
-        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (tt == 0) MP_STAMP(6);
-        c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
-        c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
-        // SGD: all 16 parameters (and momenta) of this lane read first, then written
-        if (multi && (upd || XM == 3)) {
-          // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
-          const unsigned ep = xe0 + s + 1;
-          if (XM == 3) {
-            // fragment order: [tile][register][lane]; lanes past the parameter columns write 0
-            float* go = a.xg_out + (long long)(ep & 1) * a.xe + (long long)t * 1024 + lane;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) st_sc(go + i * 64, upd ? (from_c2 ? c2[i] : c1[i]) : 0.f);
-          } else if (XM == 2) {
-            // dense index: W1[h][c] = h * IN + c, b1[h] = H IN + h, W2[h] = H IN + H + h
-            const int jb = c < IN ? c : H * IN + (c - IN) * H;
-            const int js = c < IN ? IN : 1;
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-              xpush_owner(a, ep, jb + (h0 + mfma32_row(i, lane)) * js, from_c2 ? c2[i] : c1[i]);
-          } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-              xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, from_c2 ? c2[i] : c1[i]);
-          }
-        } else if (upd) {
+        gacc = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), zf0, gacc);
+        gacc = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), zf1, gacc);
+        if (upd) {
           // one rank: register-resident parameters (see the prologue); only b1 / W2 go
           // back to LDS (the forward's and the next backward's view), W1 to its bf16 image
           const bool w1col = c < IN;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float g = from_c2 ? c2[i] : c1[i];
+            float g = gacc[i];
             if (!PLAIN) {
               if (hs.maximize) g = -g;
               if (hs.wd != 0.f) g += hs.wd * preg[tt][i];
@@ -831,6 +825,75 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         }
         if (tt == 0) MP_STAMP(7);
       }
+    }
+    } else {
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int t = wave + kMpWaves * tt;
+      if (t < NT) {
+        const int h0 = t * 32;
+        f32x16 dh;
+        // act(H) -> image columns [h0, h0+32): lane (sample r32) writes rows 8g+4hh..+3 of its column
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 wv = *reinterpret_cast<const float4*>(Pf + a.o_w2 + h0 + 8 * g + 4 * hh);  // pre-update W2
+          const float w2g[4] = {wv.x, wv.y, wv.z, wv.w};
+          float av[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e;
+            const float x = hpre[tt][i];
+            if constexpr (ACT == ACT_RELU) {
+              av[e] = relu1(x);
+              const float prod = w2g[e] * dyv;
+              dh[i] = __builtin_bit_cast(float, __builtin_bit_cast(int, prod) & (x > 0.f ? -1 : 0));
+            } else {
+              av[e] = act_fwd(ACT, x);
+              dh[i] = w2g[e] * dyv * act_bwd(ACT, x);
+            }
+          }
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) = pk4_bf16(av[0], av[1], av[2], av[3]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // gradient GEMMs: rows = hidden units of this tile, columns = [X | 1 | dY]
+        f32x16 c2, c1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c2[i] = c1[i] = 0.f;
+        c2 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c2);
+        c2 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // act(H) reads done before dH overwrites the image
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) =
+              pk4_bf16(dh[4 * g], dh[4 * g + 1], dh[4 * g + 2], dh[4 * g + 3]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tt == 0) MP_STAMP(6);
+        c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
+        c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
+        if (multi && (upd || XM == 3)) {
+          // DDP: this rank's (1/world-scaled) gradient to every rank's slot [par][rank]
+          const unsigned ep = xe0 + s + 1;
+          if (XM == 3) {
+            // fragment order: [tile][register][lane]; lanes past the parameter columns write 0
+            float* go = a.xg_out + (long long)(ep & 1) * a.xe + (long long)t * 1024 + lane;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) st_sc(go + i * 64, upd ? ((dycol ? c2[i] : c1[i])) : 0.f);
+          } else if (XM == 2) {
+            // dense index: W1[h][c] = h * IN + c, b1[h] = H IN + h, W2[h] = H IN + H + h
+            const int jb = c < IN ? c : H * IN + (c - IN) * H;
+            const int js = c < IN ? IN : 1;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              xpush_owner(a, ep, jb + (h0 + mfma32_row(i, lane)) * js, (dycol ? c2[i] : c1[i]));
+          } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, (dycol ? c2[i] : c1[i]));
+          }
+        }
+        if (tt == 0) MP_STAMP(7);
+      }
+    }
     }
     if constexpr (XM != 0) {
       // all waves done reading the pre-update parameters before any update
