@@ -197,79 +197,172 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
 
   const int kv_end = CAUSAL ? min(qb * QB + QB, a.S) : a.S;
   const int nblk = (kv_end + BN - 1) / BN;
-  TileRegs<BN, D, NT> kr, vr;
-  tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
-  tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
-  for (int j = 0; j < nblk; ++j) {
+  // K / V tiles are register-staged (global -> registers -> swizzled LDS image).  D = 64:
+  // TWO register sets, each tile loaded two blocks before its LDS store, so a load has
+  // two blocks of compute to land in (one block -- ~1.5k cycles at D = 64 -- left the
+  // loop waiting on vmcnt ~45 % of its wave-cycles: SQ_WAIT_ANY, profiles/pmc_attention_gpt2.txt);
+  // the barrier after the store waits for LDS only (__syncthreads' fence would also wait
+  // for the loads in flight).  D = 128: one set, one block ahead (register budget: the
+  // loop below as it was).
+  if constexpr (D == 64) {
+  constexpr int AHEAD = 2;
+  TileRegs<BN, D, NT> krA, vrA, krB, vrB;
+  tile_load(krA, kbase, a.k_ss, 0, a.S, tid);
+  tile_load(vrA, vbase, a.v_ss, 0, a.S, tid);
+  if (nblk > 1) {
+    tile_load(krB, kbase, a.k_ss, BN, a.S, tid);
+    tile_load(vrB, vbase, a.v_ss, BN, a.S, tid);
+  }
+  auto block = [&](int j, TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr) {
     const int buf = j & 1;
     tile_store(kr, Ks[buf], tid);
     tile_store(vr, Vs[buf], tid);
-    __syncthreads();
-    if (j + 1 < nblk) {  // next tile's HBM latency hides behind this tile's MFMAs
-      tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
-      tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (j + AHEAD < nblk) {  // this set's next tile; its latency hides behind AHEAD blocks of MFMAs
+      tile_load(kr, kbase, a.k_ss, (j + AHEAD) * BN, a.S, tid);
+      tile_load(vr, vbase, a.v_ss, (j + AHEAD) * BN, a.S, tid);
     }
-    const int k0 = j * BN;
-    if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
-    const bf16* Kb = Ks[buf];
-    const bf16* Vb = Vs[buf];
-    // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
-    f32x16 st[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      st[t] = splat16(0.f);
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) st[t] = mfma32x32x16(row_frag<D>(Kb, t * 32 + r32, ks, hh), qf[ks], st[t]);
-    }
-    // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
-    const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
-    if (need_mask) {
-#pragma unroll
+      const int k0 = j * BN;
+      if (CAUSAL && k0 > q0w + 31) return;  // every key of the block is after this wave's queries
+      const bf16* Kb = Ks[buf];
+      const bf16* Vb = Vs[buf];
+      // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
+      f32x16 st[2];
+  #pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        st[t] = splat16(0.f);
+  #pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) st[t] = mfma32x32x16(row_frag<D>(Kb, t * 32 + r32, ks, hh), qf[ks], st[t]);
+      }
+      // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
+      const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
+      if (need_mask) {
+  #pragma unroll
+        for (int t = 0; t < 2; ++t)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + t * 32 + mfma32_row(i, lane);
+            if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
+          }
+      }
+      float mblk = st[0][0];
+  #pragma unroll
       for (int t = 0; t < 2; ++t)
-#pragma unroll
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
+      mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
+      const float mnew = fmaxf(m, mblk * c);
+      // rescale O and l only when some row's max moved (exact; no threshold)
+      if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+        const float alpha = fexp2(m - mnew);
+        l *= alpha;
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+        m = mnew;
+      }
+      float lsum = 0.f;
+  #pragma unroll
+      for (int t = 0; t < 2; ++t)
+  #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int key = k0 + t * 32 + mfma32_row(i, lane);
-          if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
+          const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
+          st[t][i] = p;
+          lsum += p;
+        }
+      l += lsum + __shfl_xor(lsum, 32, kWave);
+      // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
+  #pragma unroll
+      for (int t = 0; t < 2; ++t)
+  #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb;
+  #pragma unroll
+          for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
+  #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
+        }
+  };
+  for (int j = 0; j < nblk; j += 2) {
+    block(j, krA, vrA);
+    if (j + 1 < nblk) block(j + 1, krB, vrB);
+  }
+  } else {
+    TileRegs<BN, D, NT> kr, vr;
+    tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
+    tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
+    for (int j = 0; j < nblk; ++j) {
+      const int buf = j & 1;
+      tile_store(kr, Ks[buf], tid);
+      tile_store(vr, Vs[buf], tid);
+      __syncthreads();
+      if (j + 1 < nblk) {  // next tile's HBM latency hides behind this tile's MFMAs
+        tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
+        tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
+      }
+      const int k0 = j * BN;
+      if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
+      const bf16* Kb = Ks[buf];
+      const bf16* Vb = Vs[buf];
+      // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
+      f32x16 st[2];
+  #pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        st[t] = splat16(0.f);
+  #pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) st[t] = mfma32x32x16(row_frag<D>(Kb, t * 32 + r32, ks, hh), qf[ks], st[t]);
+      }
+      // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
+      const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
+      if (need_mask) {
+  #pragma unroll
+        for (int t = 0; t < 2; ++t)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + t * 32 + mfma32_row(i, lane);
+            if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
+          }
+      }
+      float mblk = st[0][0];
+  #pragma unroll
+      for (int t = 0; t < 2; ++t)
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
+      mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
+      const float mnew = fmaxf(m, mblk * c);
+      // rescale O and l only when some row's max moved (exact; no threshold)
+      if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+        const float alpha = fexp2(m - mnew);
+        l *= alpha;
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+        m = mnew;
+      }
+      float lsum = 0.f;
+  #pragma unroll
+      for (int t = 0; t < 2; ++t)
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
+          st[t][i] = p;
+          lsum += p;
+        }
+      l += lsum + __shfl_xor(lsum, 32, kWave);
+      // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
+  #pragma unroll
+      for (int t = 0; t < 2; ++t)
+  #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb;
+  #pragma unroll
+          for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
+  #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
         }
     }
-    float mblk = st[0][0];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
-    mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
-    const float mnew = fmaxf(m, mblk * c);
-    // rescale O and l only when some row's max moved (exact; no threshold)
-    if (__builtin_amdgcn_ballot_w64(mnew != m)) {
-      const float alpha = fexp2(m - mnew);
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-      m = mnew;
-    }
-    float lsum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
-        st[t][i] = p;
-        lsum += p;
-      }
-    l += lsum + __shfl_xor(lsum, 32, kWave);
-    // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 pb;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
-      }
   }
   // ---- epilogue: O = O^T^T / l ; LSE ----
   if (qrow < a.S) {
