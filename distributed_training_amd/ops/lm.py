@@ -221,7 +221,7 @@ def rms_norm(x, w, eps: float = 1e-5):
 
 # ------------------------------------------------------------------ GEMM dispatch
 _GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 0 = hipBLASLt
-GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0}
+GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "side_wgrad": 0}
 
 
 def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 4) -> Dict[int, float]:
@@ -375,6 +375,89 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return group.grad_view(i)
 
 
+# ------------------------------------------------------------------ side-stream weight gradients
+# Nothing on the backward's critical path reads a weight gradient: the chain is
+# dgrad -> norm / activation / attention backward -> the next layer's dgrad.  With
+# ``DTA_WGRAD_STREAM=1`` the weight (and bias) gradients that go straight into a DDP
+# flat-buffer slice run on a second HIP stream, concurrently with that chain, on the
+# general GEMM's 256 x 256 tile with little or no split-K (no fp32 slab round trip:
+# the tile is MFMA-efficient, and the chain's kernels fill the CUs it leaves free).
+# Joins: every DDP bucket launch and the end of the backward make the current
+# stream wait for the side stream (:func:`wgrad_join`).  Only a weight used ONCE
+# in the forward takes this path (a second use's gradient would be summed with
+# the side stream's result by autograd on the current stream): the DDP engine
+# opens a forward generation per call (:func:`new_forward_generation`) and the
+# native Linear counts its uses in it; without a DDP engine (no generations) no
+# weight qualifies.  Measured on the GPT-2 small DDP step (one MI355X,
+# scripts/gpu_wgrad_side.sh): 11.92 -> 11.39 ms with the 128 x 128 split-K kernel at
+# split 2 on one side stream (the default, "0:2"); the 256 x 256 tile at split 1
+# serialises on the side stream (17.9 ms).
+_SIDE: Dict[int, list] = {}
+_SIDE_PENDING: Dict[int, bool] = {}
+_SIDE_CB = [False]
+_SIDE_RR = [0]
+_FWD_GEN = [0]
+
+
+def new_forward_generation() -> None:
+    """Start counting native-Linear weight uses afresh (called per DDP forward)."""
+    _FWD_GEN[0] += 1
+    _SIDE_CB[0] = False  # (a backward that raised never ran its end-of-backward join callback)
+
+
+def _count_use(w: torch.Tensor) -> None:
+    if getattr(w, "_dta_gen", -1) != _FWD_GEN[0]:
+        w._dta_gen = _FWD_GEN[0]
+        w._dta_uses = 0
+    w._dta_uses += 1
+
+
+def _single_use(w: Optional[torch.Tensor]) -> bool:
+    return w is not None and _FWD_GEN[0] > 0 and getattr(w, "_dta_gen", -1) == _FWD_GEN[0] \
+        and getattr(w, "_dta_uses", 0) == 1
+
+
+def _side_mode() -> Tuple[bool, int, int]:
+    v = os.environ.get("DTA_WGRAD_STREAM", "0:2")
+    if v in ("", "0"):
+        return False, 0, 0
+    # "0": off; "1" (tile 1, split 1) or "tile:split" (tile 0 = the 128 x 128 split-K kernel; split 0 = own choice)
+    tile, split = (int(x) for x in v.split(":")) if ":" in v else (1, 1)
+    return True, tile, split
+
+
+def wgrad_join(device: Optional[torch.device] = None) -> None:
+    """Make the current stream wait for every weight gradient enqueued on the side stream."""
+    idx = torch.cuda.current_device() if device is None else (device.index or 0)
+    if _SIDE_PENDING.get(idx):
+        for ss in _SIDE[idx]:
+            torch.cuda.current_stream(idx).wait_stream(ss)
+        _SIDE_PENDING[idx] = False
+
+
+def _end_of_backward_join() -> None:
+    _SIDE_CB[0] = False
+    for idx in list(_SIDE_PENDING):
+        wgrad_join(torch.device("cuda", idx))
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    ss = _SIDE.get(idx)
+    if ss is None:
+        ss = _SIDE[idx] = [torch.cuda.Stream(device=idx)
+                           for _ in range(max(1, int(os.environ.get("DTA_WGRAD_STREAMS", "1"))))]
+    _SIDE_RR[0] += 1
+    s = ss[_SIDE_RR[0] % len(ss)]
+    if not _SIDE_CB[0]:
+        from torch.autograd import Variable
+
+        Variable._execution_engine.queue_callback(_end_of_backward_join)
+        _SIDE_CB[0] = True
+    _SIDE_PENDING[idx] = True
+    return s
+
+
 def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
                  b: Optional[torch.Tensor] = None):
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
@@ -391,8 +474,24 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
         x2 = x2.contiguous() if x2.stride(0) % 8 else x2
         cw = _grad_dest(w)
+        side, tile, split = _side_mode()
+        cb = _grad_dest(b) if with_bias else None
+        if side and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
+                and _single_use(w) and (tile == 0 or native().gemm_wgrad_split(M, N, K, tile)):
+            # both results land in flat-buffer slices: nothing reads them before a join
+            main = torch.cuda.current_stream(dy2.device)
+            ss = _side_stream(dy2.device)
+            ss.wait_stream(main)
+            with torch.cuda.stream(ss):
+                if with_bias:
+                    native().gemm_tn_colsum(dy2, x2, False, split, -1, cw, cb, tile)
+                else:
+                    native().gemm_tn(dy2, x2, False, split, -1, cw, tile)
+            dy2.record_stream(ss)
+            x2.record_stream(ss)
+            GEMM_STATS["side_wgrad"] += 1
+            return (cw, cb) if with_bias else cw
         if with_bias:
-            cb = _grad_dest(b)
             dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
             return dw, db
         return native().gemm_tn(dy2, x2, False, 0, -1, cw)
@@ -412,6 +511,8 @@ class _Linear(Function):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)  # the Parameters themselves (their .grad decides a direct write)
+        if ctx.needs_input_grad[1]:
+            _count_use(w)  # (a weight used once may take the side-stream weight gradient)
         x2 = x.reshape(-1, x.shape[-1])
         return gemm(x2, w, bias=b, kind="fwd").view(*x.shape[:-1], w.shape[0])
 

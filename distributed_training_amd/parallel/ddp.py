@@ -188,6 +188,10 @@ class DistributedDataParallel(nn.Module):
         scaled = self._gather_into_bucket(b, 1.0 / self.world_size if prescale and self._whole(b) else 1.0)
         if self.world_size == 1:
             return
+        if sl.is_cuda:
+            from ..ops.lm import wgrad_join
+
+            wgrad_join(sl.device)  # weight gradients still running on the side stream (ops/lm.py)
         if not prescale:
             self._works.append(self.comm.all_reduce(sl, op="avg", async_op=True))
         else:
@@ -221,6 +225,10 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self.world_size > 1 and self.require_sync:
             self._broadcast_buffers()
+        if self.flat.grad.is_cuda:
+            from ..ops.lm import new_forward_generation
+
+            new_forward_generation()  # native-Linear use counts (side-stream weight gradients)
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager

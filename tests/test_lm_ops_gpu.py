@@ -368,3 +368,65 @@ def test_gemm_tn_fused_bias_gradient(K, M, N, split):
     assert _rel(db, a.float().sum(0)) < 1e-4
     c16, db16 = native().gemm_tn_colsum(a, b, False, split)
     assert db16.dtype == torch.bfloat16 and _rel(db16, a.float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("tile,split", [(1, 1), (1, 3), (1, 0), (2, 1), (2, 5), (2, 0)])
+def test_gemm_wgrad_big_tile_split_k(tile, split):
+    """dW = dY^T X with db = column sums of dY on the general GEMM's 256 x 256 / 256 x 128
+    tiles (split-K slabs, bias gradient from an MFMA against an all-ones fragment) vs fp32 torch."""
+    from distributed_training_amd.ops import native
+
+    torch.manual_seed(10)
+    K, M, N = 2048, 512, 768
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    ref, refb = a.float().t() @ b.float(), a.float().sum(0)
+    c, db = native().gemm_tn_colsum(a, b, True, split, -1, None, None, tile)
+    assert _rel(c, ref) < 1e-3 and _rel(db, refb) < 1e-4
+    c16, db16 = native().gemm_tn_colsum(a, b, False, split, -1, None, None, tile)
+    assert c16.dtype == torch.bfloat16 and _rel(c16, ref) < 1e-2 and _rel(db16, refb) < 1e-2
+    wide = torch.randn(K, M + 256, device=DEV).bfloat16()  # A as a row-strided view
+    c2 = native().gemm_tn(wide[:, 128:128 + M], b, True, split, -1, None, tile)
+    assert _rel(c2, wide[:, 128:128 + M].float().t() @ b.float()) < 1e-3
+
+
+@pytest.mark.parametrize("mode", ["0", "0:2", "1:2", "0:0"])
+def test_ddp_side_stream_weight_gradients(mode, monkeypatch):
+    """Weight gradients on the side stream (DTA_WGRAD_STREAM): same gradients as an unwrapped
+    copy, the side path taken only by single-use weights (a weight used twice stays on the
+    current stream), and the stream joined before the gradients are read."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("DTA_WGRAD_STREAM", mode)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = lm.Linear(256, 512)
+            self.b = lm.Linear(512, 256)
+            self.shared = lm.Linear(256, 256)
+
+        def forward(self, x):
+            return self.shared(self.shared(self.b(lm.gelu(self.a(x)))))
+
+    torch.manual_seed(4)
+    dev = torch.device(DEV, 0)
+    net = Net().to(dev).bfloat16()
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    x = torch.randn(1024, 256, device=dev).bfloat16()
+    for it in range(3):
+        ddp.zero_grad(set_to_none=True)
+        n0 = lm.GEMM_STATS["side_wgrad"]
+        ddp(x).float().square().mean().backward()
+        side = lm.GEMM_STATS["side_wgrad"] - n0
+        assert side == (0 if mode == "0" else 2), side  # a and b; never `shared`
+        for p in ref.parameters():
+            p.grad = None
+        ref(x).float().square().mean().backward()
+        rp = dict(ref.named_parameters())
+        for name, p in net.named_parameters():
+            assert _rel(p.grad, rp[name].grad) < 2e-2, (mode, it, name)
