@@ -429,16 +429,6 @@ hipError_t dta_gemm_tn(const void* a, int64_t lda, const void* b, int64_t ldb, v
   return hipGetLastError();
 }
 
-// sum the split-K slabs into out (and, cout != nullptr, the [ncs][M] column-sum
-// partials into cout) in one launch
-hipError_t dta_splitk_reduce(const float* slab, int split, int64_t mn, void* out, int out_f32, const float* cs, int M,
-                             void* cout, int ncs, hipStream_t st) {
-  const unsigned cs_blocks = cout ? (unsigned)((M + 31) / 32) : 0u;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256) + cs_blocks), dim3(256), 0, st, slab,
-                     split, mn, out, out_f32, cs, M, cout, out_f32, ncs);
-  return hipGetLastError();
-}
-
 // LDS-DMA split-K form.  split = 0: pick it (dta_gemm_tn_gd_split).  slab: f32
 // [split * M * N] when split > 1.
 static int gd_wgs(int tiles, int split) { return tiles * split; }

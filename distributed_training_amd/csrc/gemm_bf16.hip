@@ -61,16 +61,6 @@ struct GemmBfArgs {
   int tiles_m, tiles_n;
   float alpha;
   int act;              // ACT_NONE / ACT_GELU_TANH
-  // split-K (weight gradients): grid = tiles x split, split s reduces k stages
-  // [s * kt_total / split, (s + 1) * kt_total / split) into fp32 slab s of c32
-  // ([split][M][ldc]); split == 1: the plain GEMM
-  int split, kt_total;
-  // CS kernels: column sums of A (the bias gradient dy summed over tokens), by an
-  // MFMA against an all-ones B fragment in the workgroups of tile column 0:
-  // split > 1 -> fp32 partials cs_part[split][M]; split == 1 -> db / db32 [M]
-  float* cs_part;
-  bf16* db;
-  float* db32;
 };
 
 __device__ __forceinline__ int kswz(int r) { return ((r >> 3) & 1) * 3; }
@@ -117,7 +107,7 @@ __device__ __forceinline__ void stage_barrier(int ahead) {
 
 __device__ __forceinline__ void lds_bar() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM, int BN, bool AT, bool BT, bool PP, bool CS>
+template <int BM, int BN, bool AT, bool BT, bool PP>
 __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   constexpr int A_BYTES = BM * kGbBK * 2, B_BYTES = BN * kGbBK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int WTM = BM / 2, WTN = BN / 4, MT = WTM / 16, NT = WTN / 16;
@@ -128,14 +118,9 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // tile: XCD remap, split-major (the workgroups of one XCD share a k range), then
-  // groups of kGbGroupM tile rows walked column-major
-  const int ntiles = g.tiles_m * g.tiles_n;
-  int t = xcd_remap(blockIdx.x, ntiles * g.split);
-  const int sp = t / ntiles;
-  t -= sp * ntiles;
-  const int kt0 = (int)((int64_t)sp * g.kt_total / g.split);
-  const int nk = (int)((int64_t)(sp + 1) * g.kt_total / g.split) - kt0;
+  // tile: XCD remap, then groups of kGbGroupM tile rows walked column-major
+  const int nwg = g.tiles_m * g.tiles_n;
+  const int t = xcd_remap(blockIdx.x, nwg);
   const int per_group = kGbGroupM * g.tiles_n;
   const int grp = t / per_group, in_g = t - grp * per_group;
   const int gm0 = grp * kGbGroupM, gh = min(kGbGroupM, g.tiles_m - gm0);
@@ -171,10 +156,6 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   }
   const int64_t stepA = AT ? (int64_t)kGbBK * g.lda : kGbBK;
   const int64_t stepB = BT ? (int64_t)kGbBK * g.ldb : kGbBK;
-#pragma unroll
-  for (int j = 0; j < AL; ++j) srcA[j] += kt0 * stepA;
-#pragma unroll
-  for (int j = 0; j < BL; ++j) srcB[j] += kt0 * stepB;
   auto issue = [&](int s) {
     char* sa = lds + (s & (kGbStages - 1)) * STAGE;
     char* sb = sa + A_BYTES;
@@ -189,27 +170,6 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // CS: wave wn sums A fragments j = wn * JPW .. + JPW - 1 (tile column 0 only)
-  constexpr int JPW = MT / 4 > 0 ? MT / 4 : 1;
-  f32x4 accb[JPW];
-#pragma unroll
-  for (int q = 0; q < JPW; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_cs = CS && tn == 0;
-  const bf16 one = f2bf(1.f);
-  const bf16x8 ones = {one, one, one, one, one, one, one, one};
-  auto mma_cs = [&](const bf16x8 (&af)[MT]) {
-    if constexpr (CS) {
-      if (do_cs) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-          if (w == wn && w * JPW < MT) {
-#pragma unroll
-            for (int q = 0; q < JPW; ++q)
-              accb[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[w * JPW + q], accb[q], 0, 0, 0);
-          }
-      }
-    }
-  };
 
   auto frag_a = [&](const char* sa, int j) {
     if constexpr (!AT) return frag_k(sa, wm * WTM + 16 * j, lane);
@@ -219,6 +179,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
     if constexpr (!BT) return frag_k(sb, wn * WTN + 16 * i, lane);
     else return frag_mn<2 * BN>(sb, wn * WTN + 16 * i, lane);
   };
+  const int nk = g.K / kGbBK;
 
   if constexpr (PP) {
     // Ping-pong (cdna_hip_programming.md §5.5 T3-T5): each stage is two phases
@@ -261,7 +222,6 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
 #pragma unroll
         for (int j = 0; j < MT; ++j)
           acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[i], af[j], acc[i0 + i][j], 0, 0, 0);
-      if (i0 == 0) mma_cs(af);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -314,7 +274,6 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
       for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
-      mma_cs(af);
     };
     // Ring: stage s in slot s % 4.  Iteration kt: [wait stage kt+1, barrier] [DMA stage
     // kt+4 into slot kt % 4 -- stage kt's fragments were read in iteration kt-1 and the
@@ -341,18 +300,6 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   // epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + r (r = 0..3)
   const int mrow = m0 + wm * WTM + (lane & 15);
   const int ncol = n0 + wn * WTN + 4 * (lane >> 4);
-  if constexpr (CS) {
-    if (do_cs && wn * JPW < MT && (lane >> 4) == 0) {  // the four columns of accb are equal
-#pragma unroll
-      for (int q = 0; q < JPW; ++q) {
-        const int m = mrow + 16 * (wn * JPW + q);
-        if (g.split > 1) g.cs_part[(int64_t)sp * g.M + m] = accb[q][0];
-        else if (g.db32) g.db32[m] = accb[q][0];
-        else g.db[m] = f2bf(accb[q][0]);
-      }
-    }
-  }
-  float* const c32 = g.c32 ? g.c32 + (int64_t)sp * g.M * g.ldc : nullptr;
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int n = ncol + 16 * i;
@@ -371,8 +318,8 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
         v[r] = fmaf(acc[i][j][r], g.alpha, bv[r]);
         if (g.act == ACT_GELU_TANH) v[r] = act_fwd(ACT_GELU_TANH, v[r]);
       }
-      if (c32) {
-        *reinterpret_cast<float4*>(c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      if (g.c32) {
+        *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
         continue;
       }
       if (g.res) {  // residual stream: y = round(round(linear) + res), as two bf16 ops would give
@@ -385,12 +332,11 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   }
 }
 
-template <int BM, int BN, bool AT, bool BT, bool CS = false>
+template <int BM, int BN, bool AT, bool BT>
 static hipError_t launch_bf(const GemmBfArgs& g, hipStream_t st) {
   // static LDS: 4 x (BM + BN) x 64 B (128 KiB at 256 x 256: one workgroup per CU)
   constexpr bool PP = BM == 256 && BN == 256;  // ping-pong schedule for the big tile
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP, CS>), dim3(g.tiles_m * g.tiles_n * g.split), dim3(512), 0,
-                     st, g);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
   return hipGetLastError();
 }
 
@@ -452,8 +398,6 @@ hipError_t dta_gemm_bf16(const void* a, int64_t lda, bool a_t, const void* b, in
   g.K = K;
   g.alpha = alpha;
   g.act = act;
-  g.split = 1;
-  g.kt_total = K / kGbBK;
   switch (tile) {
     case 1:
       g.tiles_m = M / 256;
@@ -468,67 +412,4 @@ hipError_t dta_gemm_bf16(const void* a, int64_t lda, bool a_t, const void* b, in
       g.tiles_n = N / 128;
       return launch_tile<128, 128>(g, a_t, b_t, st);
   }
-}
-
-// ---------------------------------------------------------------------------
-// Weight gradient dW = A^T B (A = dy [K][M], B = x [K][N], K = tokens) on the
-// big tiles with split-K, optionally with the bias gradient (column sums of dy)
-// from the same MFMA pipe.  Measured on the GPT-2 shapes (scripts/bench_wgrad.py,
-// profiles/wgrad_big_tile.jsonl): one 256 x 256 workgroup runs a 32-token stage in
-// ~0.86 us (~1.25 PF/s chip-equivalent), but filling 256 CUs needs ~9 splits whose
-// fp32 slabs (64 MB for 2304 x 768) cost as much as the MFMA work, so the 128 x 128
-// kernel of gemm.hip stays the choice there; fp32 atomics instead of slabs were 3-4x
-// slower still.  Large outputs (Llama) take these tiles with split 1-2.  split > 1: fp32 slabs [split][M][N] (+ bias partials
-// [split][M]) summed into c / cout by splitk_reduce (csrc/gemm.hip).
-// ---------------------------------------------------------------------------
-hipError_t dta_splitk_reduce(const float* slab, int split, int64_t mn, void* out, int out_f32, const float* cs, int M,
-                             void* cout, int ncs, hipStream_t st);
-
-// split = 0: the smallest split that puts >= 224 workgroups (one per CU) on the chip,
-// each split >= 8 stages (256 tokens) deep
-int dta_gemm_wgrad_split(int M, int N, int K, int tile) {
-  if (tile < 1 || tile > 2) return 0;
-  const int bn = tile == 1 ? 256 : 128;
-  if (M % 256 || N % bn || K % kGbBK) return 0;
-  const int tiles = (M / 256) * (N / bn), kt = K / kGbBK;
-  int sp = 1;
-  while (tiles * sp < 224 && kt / (sp + 1) >= 8) ++sp;
-  return sp;
-}
-
-hipError_t dta_gemm_wgrad(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int M, int N,
-                          int K, int tile, int split, float* slab, int out_f32, float* cs_part, void* cout,
-                          hipStream_t st) {
-  if (!dta_gemm_wgrad_split(M, N, K, tile) || split < 1 || split > K / kGbBK) return hipErrorInvalidValue;
-  if (split > 1 && (!slab || ldc != N || (cout && !cs_part))) return hipErrorInvalidValue;
-  GemmBfArgs g{};
-  g.a = static_cast<const bf16*>(a);
-  g.b = static_cast<const bf16*>(b);
-  g.lda = lda;
-  g.ldb = ldb;
-  g.M = M;
-  g.N = N;
-  g.K = K;
-  g.alpha = 1.f;
-  g.act = ACT_NONE;
-  g.split = split;
-  g.kt_total = K / kGbBK;
-  g.tiles_m = M / 256;
-  g.tiles_n = N / (tile == 1 ? 256 : 128);
-  if (split > 1) {
-    g.c32 = slab;
-    g.ldc = N;
-    g.cs_part = cs_part;
-  } else {
-    g.ldc = ldc;
-    if (out_f32) g.c32 = static_cast<float*>(c);
-    else g.c = static_cast<bf16*>(c);
-    if (out_f32) g.db32 = static_cast<float*>(cout);
-    else g.db = static_cast<bf16*>(cout);
-  }
-  hipError_t e;
-  if (tile == 1) e = cout ? launch_bf<256, 256, true, true, true>(g, st) : launch_bf<256, 256, true, true>(g, st);
-  else e = cout ? launch_bf<256, 128, true, true, true>(g, st) : launch_bf<256, 128, true, true>(g, st);
-  if (e != hipSuccess || split == 1) return e;
-  return dta_splitk_reduce(slab, split, (int64_t)M * N, c, out_f32, cout ? cs_part : nullptr, M, cout, split, st);
 }

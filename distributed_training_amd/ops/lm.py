@@ -378,10 +378,10 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # ------------------------------------------------------------------ side-stream weight gradients
 # Nothing on the backward's critical path reads a weight gradient: the chain is
 # dgrad -> norm / activation / attention backward -> the next layer's dgrad.  With
-# ``DTA_WGRAD_STREAM=1`` the weight (and bias) gradients that go straight into a DDP
+# ``DTA_WGRAD_STREAM=2`` (opt-in; 0 = off) the weight (and bias) gradients that go straight into a DDP
 # flat-buffer slice run on a second HIP stream, concurrently with that chain, on the
-# general GEMM's 256 x 256 tile with little or no split-K (no fp32 slab round trip:
-# the tile is MFMA-efficient, and the chain's kernels fill the CUs it leaves free).
+# split-K kernel at split 2 (half the fp32 slab traffic of its own chip-filling split:
+# the chain's kernels fill the CUs it leaves free).
 # Joins: every DDP bucket launch and the end of the backward make the current
 # stream wait for the side stream (:func:`wgrad_join`).  Only a weight used ONCE
 # in the forward takes this path (a second use's gradient would be summed with
@@ -389,13 +389,15 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # opens a forward generation per call (:func:`new_forward_generation`) and the
 # native Linear counts its uses in it; without a DDP engine (no generations) no
 # weight qualifies.  Measured on the GPT-2 small DDP step (one MI355X,
-# scripts/gpu_wgrad_side.sh): 11.92 -> 11.39 ms with the 128 x 128 split-K kernel at
-# split 2 on one side stream (the default, "0:2"); the 256 x 256 tile at split 1
-# serialises on the side stream (17.9 ms).
-_SIDE: Dict[int, list] = {}
+# scripts/gpu_ab_lm.sh, same-box pairs): 11.9-12.45 -> 11.4-12.2 ms with the 128 x 128
+# split-K kernel at split 2 on one side stream in 6 of 8 pairs, but 12.4 -> 15.6 / 18.2 ms
+# on one box (the hardware scheduler's interleaving of the two queues is not under
+# this code's control), so it is not the default; its own split 11.5, split 1 12.3 ms; the
+# general GEMM's 256 x 256 tile at split 1 serialises on the side stream (17.9 ms); a
+# second stream for the attention dQ kernel (concurrent with dK/dV) lost 0.1-0.25 ms.
+_SIDE: Dict[int, torch.cuda.Stream] = {}
 _SIDE_PENDING: Dict[int, bool] = {}
 _SIDE_CB = [False]
-_SIDE_RR = [0]
 _FWD_GEN = [0]
 
 
@@ -417,21 +419,18 @@ def _single_use(w: Optional[torch.Tensor]) -> bool:
         and getattr(w, "_dta_uses", 0) == 1
 
 
-def _side_mode() -> Tuple[bool, int, int]:
-    v = os.environ.get("DTA_WGRAD_STREAM", "0:2")
-    if v in ("", "0"):
-        return False, 0, 0
-    # "0": off; "1" (tile 1, split 1) or "tile:split" (tile 0 = the 128 x 128 split-K kernel; split 0 = own choice)
-    tile, split = (int(x) for x in v.split(":")) if ":" in v else (1, 1)
-    return True, tile, split
+def _side_split() -> int:
+    """``DTA_WGRAD_STREAM``: 0 = off (default); n > 0 = side stream with split n (2 measured best;
+    split 1 leaves too few workgroups, the kernel's own choice (~4-5) fills the chip the chain needs)."""
+    v = os.environ.get("DTA_WGRAD_STREAM", "0")
+    return max(0, int(v)) if v.strip() else 0
 
 
 def wgrad_join(device: Optional[torch.device] = None) -> None:
     """Make the current stream wait for every weight gradient enqueued on the side stream."""
     idx = torch.cuda.current_device() if device is None else (device.index or 0)
     if _SIDE_PENDING.get(idx):
-        for ss in _SIDE[idx]:
-            torch.cuda.current_stream(idx).wait_stream(ss)
+        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
         _SIDE_PENDING[idx] = False
 
 
@@ -443,12 +442,9 @@ def _end_of_backward_join() -> None:
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    ss = _SIDE.get(idx)
-    if ss is None:
-        ss = _SIDE[idx] = [torch.cuda.Stream(device=idx)
-                           for _ in range(max(1, int(os.environ.get("DTA_WGRAD_STREAMS", "1"))))]
-    _SIDE_RR[0] += 1
-    s = ss[_SIDE_RR[0] % len(ss)]
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
     if not _SIDE_CB[0]:
         from torch.autograd import Variable
 
@@ -474,19 +470,20 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
         x2 = x2.contiguous() if x2.stride(0) % 8 else x2
         cw = _grad_dest(w)
-        side, tile, split = _side_mode()
+        split = _side_split()
         cb = _grad_dest(b) if with_bias else None
-        if side and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
-                and _single_use(w) and (tile == 0 or native().gemm_wgrad_split(M, N, K, tile)):
+        if split and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
+                and _single_use(w):
             # both results land in flat-buffer slices: nothing reads them before a join
             main = torch.cuda.current_stream(dy2.device)
             ss = _side_stream(dy2.device)
             ss.wait_stream(main)
             with torch.cuda.stream(ss):
+                split = min(split, K // 32)
                 if with_bias:
-                    native().gemm_tn_colsum(dy2, x2, False, split, -1, cw, cb, tile)
+                    native().gemm_tn_colsum(dy2, x2, False, split, -1, cw, cb)
                 else:
-                    native().gemm_tn(dy2, x2, False, split, -1, cw, tile)
+                    native().gemm_tn(dy2, x2, False, split, -1, cw)
             dy2.record_stream(ss)
             x2.record_stream(ss)
             GEMM_STATS["side_wgrad"] += 1

@@ -370,27 +370,7 @@ def test_gemm_tn_fused_bias_gradient(K, M, N, split):
     assert db16.dtype == torch.bfloat16 and _rel(db16, a.float().sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("tile,split", [(1, 1), (1, 3), (1, 0), (2, 1), (2, 5), (2, 0)])
-def test_gemm_wgrad_big_tile_split_k(tile, split):
-    """dW = dY^T X with db = column sums of dY on the general GEMM's 256 x 256 / 256 x 128
-    tiles (split-K slabs, bias gradient from an MFMA against an all-ones fragment) vs fp32 torch."""
-    from distributed_training_amd.ops import native
-
-    torch.manual_seed(10)
-    K, M, N = 2048, 512, 768
-    a = torch.randn(K, M, device=DEV).bfloat16()
-    b = torch.randn(K, N, device=DEV).bfloat16()
-    ref, refb = a.float().t() @ b.float(), a.float().sum(0)
-    c, db = native().gemm_tn_colsum(a, b, True, split, -1, None, None, tile)
-    assert _rel(c, ref) < 1e-3 and _rel(db, refb) < 1e-4
-    c16, db16 = native().gemm_tn_colsum(a, b, False, split, -1, None, None, tile)
-    assert c16.dtype == torch.bfloat16 and _rel(c16, ref) < 1e-2 and _rel(db16, refb) < 1e-2
-    wide = torch.randn(K, M + 256, device=DEV).bfloat16()  # A as a row-strided view
-    c2 = native().gemm_tn(wide[:, 128:128 + M], b, True, split, -1, None, tile)
-    assert _rel(c2, wide[:, 128:128 + M].float().t() @ b.float()) < 1e-3
-
-
-@pytest.mark.parametrize("mode", ["0", "0:2", "1:2", "0:0"])
+@pytest.mark.parametrize("mode", ["0", "2", "1", "5"])
 def test_ddp_side_stream_weight_gradients(mode, monkeypatch):
     """Weight gradients on the side stream (DTA_WGRAD_STREAM): same gradients as an unwrapped
     copy, the side path taken only by single-use weights (a weight used twice stays on the
