@@ -140,7 +140,11 @@ torch::Tensor gemm_bf16(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t, c1
   TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm: dims too large");
   TORCH_CHECK(dta_gemm_bf16_tile((int)M, (int)N, (int)K, (int)tile) != 0,
               "gemm: shape not covered (M, N multiples of the tile, K a multiple of 32)");
-  TORCH_CHECK(act == 0 || act == 2, "gemm: act 0 (none) or 2 (gelu_tanh)");
+  // act 16: GELU backward epilogue, C = (alpha op(A) op(B)^T) * gelu_tanh'(residual) (the residual operand
+  // is the activation's input; nothing is added)
+  TORCH_CHECK(act == 0 || act == 2 || act == 16, "gemm: act 0 (none), 2 (gelu_tanh) or 16 (x gelu_tanh'(residual))");
+  TORCH_CHECK(act != 16 || (residual && residual->defined() && !(bias && bias->defined())),
+              "gemm: act 16 needs the residual operand (the GELU input) and no bias");
   torch::Tensor c;
   if (out && out->defined()) {
     c = *out;

@@ -60,8 +60,11 @@ struct GemmBfArgs {
   int M, N, K;
   int tiles_m, tiles_n;
   float alpha;
-  int act;              // ACT_NONE / ACT_GELU_TANH
+  int act;              // ACT_NONE / ACT_GELU_TANH / kEpiDGelu
 };
+
+// epilogue of an input gradient through a GELU: C = acc * gelu_tanh'(res) (res = the GELU's input)
+constexpr int kEpiDGelu = 16;
 
 __device__ __forceinline__ int kswz(int r) { return ((r >> 3) & 1) * 3; }
 __device__ __forceinline__ int mswz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
@@ -322,7 +325,11 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
         *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
         continue;
       }
-      if (g.res) {  // residual stream: y = round(round(linear) + res), as two bf16 ops would give
+      if (g.act == kEpiDGelu) {  // dgrad through the GELU: one rounding (of the product)
+        const bf16x4 h4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= act_bwd(ACT_GELU_TANH, bf2f(h4[r]));
+      } else if (g.res) {  // residual stream: y = round(round(linear) + res), as two bf16 ops would give
         const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);

@@ -82,7 +82,8 @@ class MLP(nn.Module):
         self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        return self.c_proj(lm.gelu(self.c_fc(x)))
+        # c_proj(gelu(c_fc(x))) with the GELU backward folded into c_proj's input-gradient GEMM
+        return lm.gelu_linear(self.c_fc(x), self.c_proj.weight, self.c_proj.bias)
 
 
 class Block(nn.Module):

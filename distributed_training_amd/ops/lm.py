@@ -532,6 +532,74 @@ class _Linear(Function):
         return dx, dw, db
 
 
+def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.Tensor:
+    """dh = (dy W) * gelu_tanh'(h): the input gradient of ``gelu(h) W^T + b`` -- on the general
+    GEMM with the GELU derivative in its epilogue (one pass, no dA round trip through HBM), or
+    hipBLASLt followed by the GELU-backward kernel, whichever measured faster for the shape."""
+    M, K = dy2.shape
+    N = w.shape[1]
+    C = native()
+    ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and h2.is_contiguous()
+          and h2.data_ptr() % 16 == 0 and N % 8 == 0)
+
+    def run_dta(tile):
+        return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, tile)
+
+    def run_torch():
+        return C.gelu_bwd(torch.mm(dy2, w), h2, -1)
+
+    tile = _pick("dgelu", M, N, K, run_dta, run_torch) if ok else 0
+    if tile:
+        GEMM_STATS["dta"] += 1
+        return run_dta(tile)
+    GEMM_STATS["torch"] += 1
+    return run_torch()
+
+
+class _GeluLinear(Function):
+    """y = gelu_tanh(h) W^T + b (the second half of a GPT-2 MLP).  Backward:
+    dW / db from the weight-gradient path of :class:`_Linear`, and dh through
+    :func:`_dgelu_dgrad` (the GELU backward folded into the input-gradient GEMM)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b):
+        hc = h.contiguous()
+        a = native().gelu_fwd(hc, -1)
+        ctx.save_for_backward(hc, a, w)
+        ctx.has_b = b is not None
+        ctx.params = (w, b)
+        if ctx.needs_input_grad[1]:
+            _count_use(w)
+        a2 = a.reshape(-1, a.shape[-1])
+        return gemm(a2, w, bias=b, kind="fwd").view(*h.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, a, w = ctx.saved_tensors
+        pw, pb = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dh = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dh = _dgelu_dgrad(dy2, w, h.reshape(-1, h.shape[-1])).view(h.shape)
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            r = _weight_grad(dy2, a.reshape(-1, a.shape[-1]), with_bias=want_b, w=pw, b=pb if want_b else None)
+            dw, db = r if want_b else (r, None)
+        elif want_b:
+            db = native().bias_grad(dy2, False, -1)
+        return dh, dw, db
+
+
+def gelu_linear(h, w, b=None):
+    """``linear(gelu(h), w, b)`` with the GELU backward fused into the input-gradient GEMM on GPU."""
+    if h.is_cuda and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+            and h.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
+        return _GeluLinear.apply(h, w, b)
+    return linear(gelu(h), w, b)
+
+
 def linear(x, w, b=None):
     if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:

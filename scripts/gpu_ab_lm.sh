@@ -2,7 +2,7 @@
 # A/B of GPT-2 DDP step-time knobs in one box: each line "ENV=VAL ENV2=VAL2" runs bench_lm once.
 set -euo pipefail
 cd "$(dirname "$0")/.."
-export PYTHONPATH=$PWD TMPDIR=/tmp DTA_GEMM_CACHE=/tmp/gemm_cache.json
+export PYTHONPATH=$PWD TMPDIR=/tmp DTA_GEMM_CACHE=${DTA_GEMM_CACHE:-/tmp/gemm_cache.json}
 mkdir -p gpurun_out
 while read -r cfg; do
   [ -z "$cfg" ] && continue

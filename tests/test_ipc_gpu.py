@@ -273,7 +273,7 @@ def _engine_worker(rank, ws, strategy):
     comm.destroy()
 
 
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 4, 8])
 @pytest.mark.parametrize("strategy", ["ddp", "fsdp"])
 def test_engines_multi_rank_shared_gpu(strategy, ws):
     run_gloo(_engine_worker, ws, strategy)

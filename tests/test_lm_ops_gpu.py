@@ -410,3 +410,28 @@ def test_ddp_side_stream_weight_gradients(mode, monkeypatch):
         rp = dict(ref.named_parameters())
         for name, p in net.named_parameters():
             assert _rel(p.grad, rp[name].grad) < 2e-2, (mode, it, name)
+
+
+@pytest.mark.parametrize("mode", ["dta", "torch"])
+def test_gelu_linear_fused_backward(mode, monkeypatch):
+    """gelu(h) W^T + b with the GELU backward in the input-gradient GEMM's epilogue (DTA_GEMM=dta)
+    or hipBLASLt + the GELU-backward kernel (torch) vs fp32 PyTorch."""
+    import torch.nn.functional as F
+
+    monkeypatch.setenv("DTA_GEMM", mode)
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    torch.manual_seed(11)
+    h = torch.randn(4, 128, 256, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(384, 256, device=DEV) * 0.05).bfloat16().requires_grad_()
+    b = (torch.randn(384, device=DEV) * 0.1).bfloat16().requires_grad_()
+    y = lm.gelu_linear(h, w, b)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    hf, wf, bf = (t.detach().float().requires_grad_() for t in (h, w, b))
+    yf = F.linear(F.gelu(hf, approximate="tanh"), wf, bf)
+    (yf * gy.float()).sum().backward()
+    assert _rel(y, yf) < 1e-2
+    for t, r in ((h, hf), (w, wf), (b, bf)):
+        assert _rel(t.grad, r.grad) < 2e-2
+    if mode == "dta":
+        assert lm._GEMM_CHOICE.get(("dgelu", 512, 256, 384), 0) != 0
