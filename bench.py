@@ -286,13 +286,31 @@ def main():
             dbarrier()
             torch.cuda.synchronize(dev)
 
+    # Closing bracket at ws > 1: the communicator's own barrier when it has one -- a
+    # device all-reduce of one element on its stream, ordered after this rank's steps,
+    # then a synchronize (one-shot IPC push over xGMI on a node, RCCL otherwise): a
+    # real barrier (no rank returns before every rank has finished its steps) without
+    # torch.distributed.barrier's host-side launch and bookkeeping in the timed region.
+    fast = getattr(comm, "barrier", None) if ws > 1 and comm is not None else None
+
+    def end_barrier():
+        if fast is None:
+            barrier()
+            return
+        torch.cuda.synchronize(dev)
+        fast()
+
     step_fn(args.warmup)
     barrier()
     t0 = time.perf_counter()
     step_fn(args.steps)
     th = time.perf_counter()
-    barrier()
+    end_barrier()
     t1 = time.perf_counter()
+    if fast is not None:
+        if hasattr(comm, "poll_errors"):
+            comm.poll_errors()  # a timed-out peer wait in the closing barrier raises here
+        dbarrier()
     if os.environ.get("DTA_BENCH_TRACE"):
         print(f"[bench] host call {1e6 * (th - t0):.1f} us, wait {1e6 * (t1 - th):.1f} us", file=sys.stderr)
     elapsed = t1 - t0
