@@ -34,6 +34,10 @@ struct LinStepArgs {
 
 hipError_t dta_linear_step(const dta::LinStepArgs*, hipStream_t);
 int dta_gemm_bf16_tile(int, int, int, int);
+int dta_gemm_group_max();
+hipError_t dta_gemm_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
+                                void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
+                                hipStream_t);
 hipError_t dta_gemm_bf16(const void*, int64_t, bool, const void*, int64_t, bool, void*, float*, int64_t, int, int, int,
                          float, const void*, int, const void*, int64_t, int, hipStream_t);
 size_t dta_linear_step_lds_bytes(int, int, int, int);
@@ -180,6 +184,52 @@ torch::Tensor gemm_bf16(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t, c1
   return c;
 }
 
+// Grouped weight (+ bias) gradients: dW_i = A_i^T B_i into c_i, db_i = column sums of A_i
+// (A_i = dy [K, M_i], B_i = x [K, N_i], c_i [M_i, N_i] bf16; db_i bf16 [M_i] or None).
+void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, std::vector<torch::Tensor> c,
+                      std::vector<c10::optional<torch::Tensor>> db, int64_t stream) {
+  const int n = (int)a.size();
+  TORCH_CHECK(n >= 1 && n <= dta_gemm_group_max() && (int)b.size() == n && (int)c.size() == n && (int)db.size() == n,
+              "gemm_wgrad_group: 1..", dta_gemm_group_max(), " problems, equal list lengths");
+  std::vector<const void*> ap(n), bp(n);
+  std::vector<void*> cp(n), dp(n);
+  std::vector<int64_t> lda(n), ldb(n), ldc(n);
+  std::vector<int> M(n), N(n), K(n);
+  for (int i = 0; i < n; ++i) {
+    const auto& A = a[i];
+    const auto& B = b[i];
+    const auto& Cc = c[i];
+    for (const auto* t : {&A, &B, &Cc})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->dim() == 2 && t->stride(1) == 1 &&
+                      t->stride(0) % 8 == 0 && aligned16(*t),
+                  "gemm_wgrad_group: bf16 2-D GPU tensors, unit inner stride, 16-byte aligned rows");
+    TORCH_CHECK(A.size(0) == B.size(0) && Cc.size(0) == A.size(1) && Cc.size(1) == B.size(1),
+                "gemm_wgrad_group: A [K, M], B [K, N], C [M, N]");
+    TORCH_CHECK(A.size(1) % 256 == 0 && B.size(1) % 256 == 0 && A.size(0) % 32 == 0 && A.size(0) > 0 &&
+                    A.size(0) < (1 << 30),
+                "gemm_wgrad_group: M, N multiples of 256, K a multiple of 32");
+    ap[i] = A.data_ptr();
+    bp[i] = B.data_ptr();
+    cp[i] = Cc.data_ptr();
+    lda[i] = A.stride(0);
+    ldb[i] = B.stride(0);
+    ldc[i] = Cc.stride(0);
+    M[i] = (int)A.size(1);
+    N[i] = (int)B.size(1);
+    K[i] = (int)A.size(0);
+    dp[i] = nullptr;
+    if (db[i] && db[i]->defined()) {
+      const auto& d = *db[i];
+      TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kBFloat16 && d.is_contiguous() && d.numel() == M[i],
+                  "gemm_wgrad_group: db bf16 [M]");
+      dp[i] = d.data_ptr();
+    }
+  }
+  ok(dta_gemm_wgrad_group(n, ap.data(), lda.data(), bp.data(), ldb.data(), cp.data(), ldc.data(), M.data(), N.data(),
+                          K.data(), dp.data(), stream_of(stream)),
+     "gemm_wgrad_group");
+}
+
 }  // namespace
 
 void dta_register_ext(pybind11::module_& m) {
@@ -192,6 +242,9 @@ void dta_register_ext(pybind11::module_& m) {
   m.def("gemm", &gemm_bf16, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
         py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0, py::arg("bias") = py::none(),
         py::arg("act") = 0, py::arg("residual") = py::none(), py::arg("tile") = 0, py::arg("stream") = -1);
+  m.def("gemm_wgrad_group", &gemm_wgrad_group, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("db"),
+        py::arg("stream") = -1);
+  m.def("gemm_group_max", &dta_gemm_group_max);
   m.def("gemm_tile", [](int M, int N, int K, int tile) { return dta_gemm_bf16_tile(M, N, K, tile); },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
   m.def("linear_step_supported", [](int I, int C, int B, bool mom) { return dta_linear_step_supported(I, C, B, mom) != 0; });

@@ -61,6 +61,11 @@ struct GemmBfArgs {
   int tiles_m, tiles_n;
   float alpha;
   int act;              // ACT_NONE / ACT_GELU_TANH / kEpiDGelu
+  // CS kernels (weight gradients): the bias gradient db[m] = sum_k A(m, k) (column
+  // sums of dy) from an MFMA against an all-ones B fragment in the workgroups of
+  // tile column 0 -- bf16 db or fp32 db32 (nullptr both: none)
+  bf16* db;
+  float* db32;
 };
 
 // epilogue of an input gradient through a GELU: C = acc * gelu_tanh'(res) (res = the GELU's input)
@@ -110,8 +115,11 @@ __device__ __forceinline__ void stage_barrier(int ahead) {
 
 __device__ __forceinline__ void lds_bar() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM, int BN, bool AT, bool BT, bool PP>
-__global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
+// One BM x BN output tile `t` (row-major tile index of the problem, already
+// XCD-remapped) of the problem `g`: the body of gemm_bf16_kernel and of
+// gemm_group_kernel.
+template <int BM, int BN, bool AT, bool BT, bool PP, bool CS>
+__device__ __forceinline__ void gemm_tile(const GemmBfArgs& g, const int t) {
   constexpr int A_BYTES = BM * kGbBK * 2, B_BYTES = BN * kGbBK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int WTM = BM / 2, WTN = BN / 4, MT = WTM / 16, NT = WTN / 16;
   constexpr int AL = BM / 128, BL = BN / 128, L = AL + BL;  // DMA instructions per wave per stage
@@ -121,9 +129,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // tile: XCD remap, then groups of kGbGroupM tile rows walked column-major
-  const int nwg = g.tiles_m * g.tiles_n;
-  const int t = xcd_remap(blockIdx.x, nwg);
+  // tile: groups of kGbGroupM tile rows walked column-major
   const int per_group = kGbGroupM * g.tiles_n;
   const int grp = t / per_group, in_g = t - grp * per_group;
   const int gm0 = grp * kGbGroupM, gh = min(kGbGroupM, g.tiles_m - gm0);
@@ -173,6 +179,27 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   for (int i = 0; i < NT; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // CS: wave wn sums the A fragments j = wn * JPW .. + JPW - 1 (tile column 0 only)
+  constexpr int JPW = MT / 4 > 0 ? MT / 4 : 1;
+  f32x4 accb[JPW];
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_cs = CS && tn == 0 && (g.db != nullptr || g.db32 != nullptr);
+  const bf16 one = f2bf(1.f);
+  const bf16x8 ones = {one, one, one, one, one, one, one, one};
+  auto mma_cs = [&](const bf16x8 (&af)[MT]) {
+    if constexpr (CS) {
+      if (do_cs) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          if (w == wn && w * JPW < MT) {
+#pragma unroll
+            for (int q = 0; q < JPW; ++q)
+              accb[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[w * JPW + q], accb[q], 0, 0, 0);
+          }
+      }
+    }
+  };
 
   auto frag_a = [&](const char* sa, int j) {
     if constexpr (!AT) return frag_k(sa, wm * WTM + 16 * j, lane);
@@ -225,6 +252,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
 #pragma unroll
         for (int j = 0; j < MT; ++j)
           acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[i], af[j], acc[i0 + i][j], 0, 0, 0);
+      if (i0 == 0) mma_cs(af);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -277,6 +305,7 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
       for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int j = 0; j < MT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[i], af[j], acc[i][j], 0, 0, 0);
+      mma_cs(af);
     };
     // Ring: stage s in slot s % 4.  Iteration kt: [wait stage kt+1, barrier] [DMA stage
     // kt+4 into slot kt % 4 -- stage kt's fragments were read in iteration kt-1 and the
@@ -303,6 +332,16 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
   // epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + r (r = 0..3)
   const int mrow = m0 + wm * WTM + (lane & 15);
   const int ncol = n0 + wn * WTN + 4 * (lane >> 4);
+  if constexpr (CS) {
+    if (do_cs && wn * JPW < MT && (lane >> 4) == 0) {  // the four columns of accb are equal
+#pragma unroll
+      for (int q = 0; q < JPW; ++q) {
+        const int m = mrow + 16 * (wn * JPW + q);
+        if (g.db32) g.db32[m] = accb[q][0];
+        else g.db[m] = f2bf(accb[q][0]);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int n = ncol + 16 * i;
@@ -337,6 +376,31 @@ __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
       *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
     }
   }
+}
+
+template <int BM, int BN, bool AT, bool BT, bool PP>
+__global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
+  gemm_tile<BM, BN, AT, BT, PP, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+}
+
+// Grouped weight gradients: several independent problems (dW_i = dy_i^T x_i, each with
+// its bias gradient) in ONE launch of 256 x 256 tiles over the full token reduction --
+// no split-K, no fp32 slabs.  The tiles of all problems form one list (problem-major,
+// XCD-remapped so each XCD takes a contiguous run: neighbouring tiles of one problem,
+// whose dy / x panels its L2 then shares).  Used for the GPT-2-sized weight gradients,
+// deferred and batched across Linear layers (ops/lm.py).
+constexpr int kGroupMax = 16;
+struct GemmGroupArgs {
+  int n;
+  int tile_start[kGroupMax + 1];
+  GemmBfArgs p[kGroupMax];
+};
+
+__global__ void __launch_bounds__(512) gemm_group_kernel(GemmGroupArgs ga) {
+  const int t = xcd_remap(blockIdx.x, ga.tile_start[ga.n]);
+  int q = 0;
+  while (q + 1 < ga.n && t >= ga.tile_start[q + 1]) ++q;
+  gemm_tile<256, 256, true, true, true, true>(ga.p[q], t - ga.tile_start[q]);
 }
 
 template <int BM, int BN, bool AT, bool BT>
@@ -419,4 +483,41 @@ hipError_t dta_gemm_bf16(const void* a, int64_t lda, bool a_t, const void* b, in
       g.tiles_n = N / 128;
       return launch_tile<128, 128>(g, a_t, b_t, st);
   }
+}
+
+// n problems dW_i[M_i][N_i] (bf16, row stride ldc_i) = A_i^T B_i with A_i = dy [K_i][M_i]
+// (lda_i), B_i = x [K_i][N_i] (ldb_i); db_i (bf16 [M_i], or nullptr) = column sums of A_i.
+// Every M_i, N_i a multiple of 256, K_i of 32.
+int dta_gemm_group_max() { return kGroupMax; }
+
+hipError_t dta_gemm_wgrad_group(int n, const void* const* a, const int64_t* lda, const void* const* b,
+                                const int64_t* ldb, void* const* c, const int64_t* ldc, const int* M, const int* N,
+                                const int* K, void* const* db, hipStream_t st) {
+  if (n < 1 || n > kGroupMax) return hipErrorInvalidValue;
+  GemmGroupArgs ga{};
+  ga.n = n;
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] % 256 || N[i] % 256 || K[i] % kGbBK || K[i] < kGbBK) return hipErrorInvalidValue;
+    GemmBfArgs& g = ga.p[i];
+    g.a = static_cast<const bf16*>(a[i]);
+    g.b = static_cast<const bf16*>(b[i]);
+    g.c = static_cast<bf16*>(c[i]);
+    g.lda = lda[i];
+    g.ldb = ldb[i];
+    g.ldc = ldc[i];
+    g.M = M[i];
+    g.N = N[i];
+    g.K = K[i];
+    g.tiles_m = M[i] / 256;
+    g.tiles_n = N[i] / 256;
+    g.alpha = 1.f;
+    g.act = ACT_NONE;
+    g.db = static_cast<bf16*>(db[i]);
+    ga.tile_start[i] = total;
+    total += g.tiles_m * g.tiles_n;
+  }
+  ga.tile_start[n] = total;
+  hipLaunchKernelGGL(gemm_group_kernel, dim3(total), dim3(512), 0, st, ga);
+  return hipGetLastError();
 }

@@ -221,7 +221,7 @@ def rms_norm(x, w, eps: float = 1e-5):
 
 # ------------------------------------------------------------------ GEMM dispatch
 _GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 0 = hipBLASLt
-GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "side_wgrad": 0}
+GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "side_wgrad": 0, "deferred_wgrad": 0, "group_launches": 0}
 
 
 def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 4) -> Dict[int, float]:
@@ -405,6 +405,8 @@ def new_forward_generation() -> None:
     """Start counting native-Linear weight uses afresh (called per DDP forward)."""
     _FWD_GEN[0] += 1
     _SIDE_CB[0] = False  # (a backward that raised never ran its end-of-backward join callback)
+    _DEFER.clear()  # (nor flushed what it deferred: those gradients belong to an abandoned step)
+    _DEFER_TILES[0] = 0
 
 
 def _count_use(w: torch.Tensor) -> None:
@@ -427,7 +429,9 @@ def _side_split() -> int:
 
 
 def wgrad_join(device: Optional[torch.device] = None) -> None:
-    """Make the current stream wait for every weight gradient enqueued on the side stream."""
+    """Every weight gradient of this backward written: the deferred ones launched
+    (:func:`wgrad_flush`) and the current stream made to wait for the side stream."""
+    wgrad_flush()
     idx = torch.cuda.current_device() if device is None else (device.index or 0)
     if _SIDE_PENDING.get(idx):
         torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
@@ -436,8 +440,53 @@ def wgrad_join(device: Optional[torch.device] = None) -> None:
 
 def _end_of_backward_join() -> None:
     _SIDE_CB[0] = False
+    wgrad_flush()
     for idx in list(_SIDE_PENDING):
         wgrad_join(torch.device("cuda", idx))
+
+
+def _queue_end_join() -> None:
+    if not _SIDE_CB[0]:
+        from torch.autograd import Variable
+
+        Variable._execution_engine.queue_callback(_end_of_backward_join)
+        _SIDE_CB[0] = True
+
+
+# ------------------------------------------------------------------ deferred, grouped weight gradients
+# At GPT-2 sizes one layer's weight gradients (2304x768, 768x768, 3072x768, 768x3072 over
+# 8192 tokens) are too small to fill 256 CUs on their own, which is why the per-call kernel
+# splits the token reduction (fp32 slabs, ~650 TF/s).  Nothing reads a weight gradient
+# before the DDP bucket launch / the end of the backward, so the single-use weights whose
+# gradients go straight into flat-buffer slices are DEFERRED instead: their (dy, x) pairs
+# are queued, and once the queue holds >= DTA_WGRAD_GROUP 256 x 256 output tiles (default
+# 200: two GPT-2 layers = 216 tiles) ONE grouped launch computes all of them over the full
+# token reduction -- no split, no slabs, bias gradients from the same MFMA pipe
+# (csrc/gemm_bf16.hip gemm_group_kernel).  The queue is flushed before every DDP bucket
+# launch and at the end of the backward (same stream: no further synchronisation).
+_DEFER: list = []
+_DEFER_TILES = [0]
+
+
+def _group_threshold() -> int:
+    v = os.environ.get("DTA_WGRAD_GROUP", "200")
+    return max(0, int(v)) if v.strip() else 0
+
+
+def wgrad_flush() -> None:
+    """Launch the queued weight gradients (grouped, at most gemm_group_max() per launch)."""
+    if not _DEFER:
+        return
+    items = list(_DEFER)
+    _DEFER.clear()
+    _DEFER_TILES[0] = 0
+    C = native()
+    gmax = C.gemm_group_max()
+    for i in range(0, len(items), gmax):
+        part = items[i:i + gmax]
+        C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
+                           [it[3] for it in part], -1)
+    GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -445,11 +494,7 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     s = _SIDE.get(idx)
     if s is None:
         s = _SIDE[idx] = torch.cuda.Stream(device=idx)
-    if not _SIDE_CB[0]:
-        from torch.autograd import Variable
-
-        Variable._execution_engine.queue_callback(_end_of_backward_join)
-        _SIDE_CB[0] = True
+    _queue_end_join()
     _SIDE_PENDING[idx] = True
     return s
 
@@ -472,6 +517,17 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
         cw = _grad_dest(w)
         split = _side_split()
         cb = _grad_dest(b) if with_bias else None
+        thr = _group_threshold()
+        if thr and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
+                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0:
+            # deferred: computed by a grouped launch at the next flush (see _DEFER)
+            _DEFER.append((dy2, x2, cw, cb))
+            _DEFER_TILES[0] += (M // 256) * (N // 256)
+            GEMM_STATS["deferred_wgrad"] += 1
+            _queue_end_join()
+            if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm_group_max():
+                wgrad_flush()
+            return (cw, cb) if with_bias else cw
         if split and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
                 and _single_use(w):
             # both results land in flat-buffer slices: nothing reads them before a join

@@ -381,6 +381,7 @@ def test_ddp_side_stream_weight_gradients(mode, monkeypatch):
     from distributed_training_amd.parallel.ddp import DistributedDataParallel
 
     monkeypatch.setenv("DTA_WGRAD_STREAM", mode)
+    monkeypatch.setenv("DTA_WGRAD_GROUP", "0")
 
     class Net(torch.nn.Module):
         def __init__(self):
@@ -435,3 +436,71 @@ def test_gelu_linear_fused_backward(mode, monkeypatch):
         assert _rel(t.grad, r.grad) < 2e-2
     if mode == "dta":
         assert lm._GEMM_CHOICE.get(("dgelu", 512, 256, 384), 0) != 0
+
+
+@pytest.mark.parametrize("threshold", ["0", "1", "200"])
+def test_ddp_deferred_grouped_weight_gradients(threshold, monkeypatch):
+    """Weight + bias gradients deferred and computed by grouped launches (DTA_WGRAD_GROUP tiles
+    per flush; 1 = a flush per weight, 200 = one flush at the end of the backward) match an
+    unwrapped copy; a weight used twice is never deferred."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("DTA_WGRAD_GROUP", threshold)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = lm.Linear(256, 768)
+            self.b = lm.Linear(768, 512)
+            self.c = lm.Linear(512, 256)
+            self.shared = lm.Linear(256, 256)
+
+        def forward(self, x):
+            h = lm.gelu_linear(self.a(x), self.b.weight, self.b.bias)
+            return self.shared(self.shared(self.c(h)))
+
+    torch.manual_seed(5)
+    dev = torch.device(DEV, 0)
+    net = Net().to(dev).bfloat16()
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    x = torch.randn(2, 512, 256, device=dev).bfloat16()
+    for it in range(3):
+        ddp.zero_grad(set_to_none=True)
+        n0, g0 = lm.GEMM_STATS["deferred_wgrad"], lm.GEMM_STATS["group_launches"]
+        ddp(x).float().square().mean().backward()
+        deferred = lm.GEMM_STATS["deferred_wgrad"] - n0
+        launches = lm.GEMM_STATS["group_launches"] - g0
+        assert deferred == (0 if threshold == "0" else 3), deferred  # a, b, c; never `shared`
+        assert launches == {"0": 0, "1": 3, "200": 1}[threshold], launches
+        for p in ref.parameters():
+            p.grad = None
+        ref(x).float().square().mean().backward()
+        rp = dict(ref.named_parameters())
+        for name, p in net.named_parameters():
+            assert _rel(p.grad, rp[name].grad) < 2e-2, (threshold, it, name)
+
+
+def test_gemm_wgrad_group_vs_fp32():
+    """The grouped weight-gradient launch (256 x 256 tiles, full token reduction, bias gradient
+    on the MFMA pipe) on problems of different shapes and K, strided operands, vs fp32 torch."""
+    from distributed_training_amd.ops import native
+
+    torch.manual_seed(12)
+    shapes = [(1024, 512, 256), (2048, 256, 768), (512, 768, 512), (96, 256, 256)]  # (K, M, N)
+    A, B, Cs, D = [], [], [], []
+    for K, M, N in shapes:
+        wide = torch.randn(K, M + 64, device=DEV).bfloat16()
+        A.append(wide[:, 32:32 + M])
+        B.append(torch.randn(K, N, device=DEV).bfloat16())
+        Cs.append(torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+        D.append(torch.empty(M, device=DEV, dtype=torch.bfloat16))
+    D[1] = None  # a problem without bias
+    native().gemm_wgrad_group(A, B, Cs, D)
+    for i in range(len(shapes)):
+        assert _rel(Cs[i], A[i].float().t() @ B[i].float()) < 1e-2, i
+        if D[i] is not None:
+            assert _rel(D[i], A[i].float().sum(0)) < 1e-2, i
