@@ -520,8 +520,13 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
         thr = _group_threshold()
         if thr and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
                 and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0:
-            # deferred: computed by a grouped launch at the next flush (see _DEFER)
-            _DEFER.append((dy2, x2, cw, cb))
+            # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
+            # holds ALIASES of the slices, never the tensors returned to autograd: a second
+            # reference to a returned gradient makes AccumulateGrad clone it instead of
+            # adopting it -- a copy of the slice taken BEFORE the deferred GEMM wrote it,
+            # which the DDP bucket copy then moved back over the GEMM's result whenever a
+            # flush fell between this backward and the bucket's launch (stale gradients)
+            _DEFER.append((dy2, x2, cw.view(cw.shape), None if cb is None else cb.view(cb.shape)))
             _DEFER_TILES[0] += (M // 256) * (N // 256)
             GEMM_STATS["deferred_wgrad"] += 1
             _queue_end_join()

@@ -504,3 +504,38 @@ def test_gemm_wgrad_group_vs_fp32():
         assert _rel(Cs[i], A[i].float().t() @ B[i].float()) < 1e-2, i
         if D[i] is not None:
             assert _rel(D[i], A[i].float().sum(0)) < 1e-2, i
+
+
+def test_ddp_deferred_flush_between_backward_and_bucket_launch(monkeypatch):
+    """A grouped flush that falls between a deferred weight's backward and its bucket's launch
+    (DTA_WGRAD_GROUP=8: every second 512 x 512 weight flushes; buckets span several layers):
+    every gradient is adopted as its flat-buffer view (no AccumulateGrad clone of the not yet
+    written slice) and matches an unwrapped copy on every iteration (a stale slice would carry
+    the previous iteration's gradient)."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("DTA_WGRAD_GROUP", "8")
+    torch.manual_seed(6)
+    dev = torch.device(DEV, 0)
+    net = torch.nn.Sequential(*[lm.Linear(512, 512) for _ in range(6)]).to(dev).bfloat16()
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16,
+                                  bucket_cap_mb=1.5, first_bucket_mb=1.0)
+    assert len(ddp.buckets) >= 2
+    for it in range(3):
+        x = torch.randn(2, 512, 512, device=dev).bfloat16()
+        ddp.zero_grad(set_to_none=True)
+        n0 = lm.GEMM_STATS["deferred_wgrad"]
+        (ddp(x).float().square().mean() * (it + 1)).backward()
+        assert lm.GEMM_STATS["deferred_wgrad"] - n0 == 6
+        fl = ddp.flat
+        assert all(fl.grad_is_view(i) for i in range(len(fl.params)))
+        for p in ref.parameters():
+            p.grad = None
+        (ref(x).float().square().mean() * (it + 1)).backward()
+        rp = dict(ref.named_parameters())
+        for name, p in net.named_parameters():
+            assert _rel(p.grad, rp[name].grad) < 2e-2, (it, name)
