@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--bucket-mb", default="auto", help="DDP bucket cap in MiB, or auto (xGMI-derived)")
     ap.add_argument("--layers", type=int, default=0, help="override n_layer (0 = config)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--overlap-opt", action="store_true",
+                    help="native DDP: AdamW per bucket inside the backward (DistributedDataParallel.overlap_optimizer) "
+                         "instead of after it; bit-identical, measured neutral at one rank (README)")
     ap.add_argument("--tunableop", action="store_true",
                     help="let PyTorch's TunableOp pick the hipBLASLt/rocBLAS solution per GEMM shape (tuned in warmup)")
     return ap.parse_args()
@@ -102,6 +105,7 @@ def main():
     data = torch.randint(0, V, (max(4, 64 // max(1, args.batch)) * args.batch, args.seq + 1), device=dev,
                          generator=gen)
 
+    overlap_opt = False
     if args.impl == "native":
         from distributed_training_amd.ops import lm
         from distributed_training_amd.ops.optim import FusedAdamW
@@ -120,6 +124,7 @@ def main():
             wrapped = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy={M.block_class},
                                                param_dtype=torch.bfloat16)
         opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
+        overlap_opt = args.strategy == "ddp" and args.overlap_opt and wrapped.overlap_optimizer(opt)
 
         def loss_fn(logits, y):
             return lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
@@ -229,6 +234,7 @@ def main():
         from distributed_training_amd.ops import lm as _lm
 
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
+        out["optimizer_in_backward"] = bool(overlap_opt)
         out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": (f"dta/t{v}" if v else "hipblaslt")
                             for k, v in sorted(_lm._GEMM_CHOICE.items())}
     if rank == 0:

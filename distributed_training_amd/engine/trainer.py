@@ -71,6 +71,7 @@ class TrainingConfig:
     desync_check_every: int = 0
     fault_injection: Optional[Dict[str, int]] = None
     cpu_offload: bool = False        # FSDP: fp32 shards, gradients and optimizer on the host
+    optimizer_in_backward: bool = False  # DDP on GPU: fused update per bucket inside the backward (no grad_clip)
     extra: Dict[str, Any] = field(default_factory=dict)
 
 
@@ -109,6 +110,11 @@ class Trainer:
                                           save_optimizer=config.save_optimizer)
         self._fused = None
         self._maybe_build_fused()
+        if self._fused is None and config.optimizer_in_backward and not config.grad_clip \
+                and hasattr(self.model, "overlap_optimizer"):
+            # bit-identical to backward + step(); the update of late buckets overlaps the early backward
+            if self.model.overlap_optimizer(self.optimizer):
+                logger.debug("optimizer stepped per DDP bucket inside the backward")
         self.last_epoch_stats: Dict[str, float] = {}
         logger.info(
             f"[{str(self.env.device).upper()}{self.env.global_rank}] "

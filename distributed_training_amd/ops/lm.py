@@ -466,6 +466,14 @@ def _queue_end_join() -> None:
 # launch and at the end of the backward (same stream: no further synchronisation).
 _DEFER: list = []
 _DEFER_TILES = [0]
+# called after every flush launched its groups (the DDP engine's per-bucket optimizer
+# step waits for the weight gradients of its bucket: parallel/ddp.py overlap_optimizer)
+FLUSH_LISTENERS: list = []
+
+
+def wgrad_pending() -> bool:
+    """Weight gradients are queued (their flat-buffer slices are not written yet)."""
+    return bool(_DEFER)
 
 
 def _group_threshold() -> int:
@@ -487,6 +495,8 @@ def wgrad_flush() -> None:
         C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
                            [it[3] for it in part], -1)
     GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
+    for fn in list(FLUSH_LISTENERS):
+        fn()
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:

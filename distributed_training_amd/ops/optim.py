@@ -95,6 +95,20 @@ def _restore_flat(fg, by_param: Dict[torch.nn.Parameter, dict], key: str) -> Opt
     return flat
 
 
+def _stepped_in_backward(fg) -> bool:
+    """True (once) when the DDP engine already ran this step bucket by bucket inside the
+    backward (parallel/ddp.py ``overlap_optimizer``): ``step()`` then has nothing to do."""
+    if getattr(fg, "stepped_in_backward", False):
+        fg.stepped_in_backward = False
+        return True
+    return False
+
+
+def _covers(params, fg) -> bool:
+    ids = {id(p) for p in params}
+    return len(ids) == len(fg.params) and all(id(p) in ids for p in fg.params)
+
+
 class FusedSGD(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False):
@@ -120,6 +134,8 @@ class FusedSGD(torch.optim.Optimizer):
             nest, maxi = group["nesterov"], group["maximize"]
             flats, singles = _split_params(group["params"])
             for fg, ps in flats:
+                if _stepped_in_backward(fg):
+                    continue
                 if len(ps) == len(fg.params):
                     if not fg.prepare_grads_for_step():
                         continue
@@ -153,6 +169,31 @@ class FusedSGD(torch.optim.Optimizer):
                 else:
                     _sgd_ref(p, p.grad, buf, lr, mom, damp, wd, nest, maxi, first)
         return loss
+
+    # -------------------------------------------------- step split over DDP buckets
+    def range_capable(self, fg) -> bool:
+        return len(self.param_groups) == 1 and _covers(self.param_groups[0]["params"], fg)
+
+    @torch.no_grad()
+    def step_range(self, fg, lo: int, hi: int, first: bool) -> None:
+        """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
+        current stream): the same per-element math as :meth:`step` over the whole buffer,
+        so a step split into ranges is bit-identical.  ``first``: the step's first range."""
+        g = self.param_groups[0]
+        st = self._flat_state.setdefault(id(fg), {"first": True})
+        if g["momentum"] and "mom" not in st:
+            st["mom"] = torch.zeros_like(fg.master)
+            for i, p in enumerate(fg.params):
+                self.state[p]["momentum_buffer"] = fg._view(st["mom"], i)
+        mom = st.get("mom")
+        native().flat_sgd(fg.master[lo:hi], fg.master[lo:hi], _grad32(fg.grad[lo:hi]),
+                          None if mom is None else mom[lo:hi], fg.compute[lo:hi] if fg.mixed else None,
+                          g["lr"], g["momentum"], g["dampening"], g["weight_decay"], 1.0, g["nesterov"],
+                          g["maximize"], st["first"], -1)
+
+    def end_ranges(self, fg) -> None:
+        """Every range of this step launched."""
+        self._flat_state.setdefault(id(fg), {"first": True})["first"] = False
 
     @torch.no_grad()
     def load_state_dict(self, state_dict: dict) -> None:
@@ -253,20 +294,11 @@ class FusedAdamW(torch.optim.Optimizer):
             for fg, ps in flats:
                 if len(ps) != len(fg.params):
                     raise ValueError("FusedAdamW: a FlatParamGroup must be optimised as a whole by one param group")
+                if _stepped_in_backward(fg):
+                    continue
                 if not fg.prepare_grads_for_step():
                     continue
-                st = self._flat_state.get(id(fg))
-                if st is None:
-                    st = {"m": torch.zeros_like(fg.master), "v": torch.zeros_like(fg.master),
-                          "vmax": torch.zeros_like(fg.master) if ams else None,
-                          "step": torch.zeros(1, device=fg.master.device)}
-                    self._flat_state[id(fg)] = st
-                    for i, p in enumerate(fg.params):
-                        self.state[p]["exp_avg"] = fg._view(st["m"], i)
-                        self.state[p]["exp_avg_sq"] = fg._view(st["v"], i)
-                        self.state[p]["step"] = st["step"]
-                        if ams:
-                            self.state[p]["max_exp_avg_sq"] = fg._view(st["vmax"], i)
+                st = self._flat(fg, ams)
                 pb = fg.compute if fg.mixed else None
                 native().flat_adam(fg.master, fg.grad, st["m"], st["v"], st["vmax"], pb, st["step"], lr, b1,
                                    b2, eps, wd, 1.0, adamw, maxi, ams, True, -1)
@@ -294,6 +326,40 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
     zero_grad = FusedSGD.zero_grad
+
+    def _flat(self, fg, ams: bool) -> dict:
+        st = self._flat_state.get(id(fg))
+        if st is None:
+            st = {"m": torch.zeros_like(fg.master), "v": torch.zeros_like(fg.master),
+                  "vmax": torch.zeros_like(fg.master) if ams else None,
+                  "step": torch.zeros(1, device=fg.master.device)}
+            self._flat_state[id(fg)] = st
+            for i, p in enumerate(fg.params):
+                self.state[p]["exp_avg"] = fg._view(st["m"], i)
+                self.state[p]["exp_avg_sq"] = fg._view(st["v"], i)
+                self.state[p]["step"] = st["step"]
+                if ams:
+                    self.state[p]["max_exp_avg_sq"] = fg._view(st["vmax"], i)
+        return st
+
+    # -------------------------------------------------- step split over DDP buckets
+    range_capable = FusedSGD.range_capable
+
+    @torch.no_grad()
+    def step_range(self, fg, lo: int, hi: int, first: bool) -> None:
+        """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
+        current stream); ``first`` bumps the device step counter (the step's first range).
+        Element-wise math identical to :meth:`step`: a split step is bit-identical."""
+        g = self.param_groups[0]
+        (b1, b2), ams = g["betas"], g["amsgrad"]
+        st = self._flat(fg, ams)
+        native().flat_adam(fg.master[lo:hi], fg.grad[lo:hi], st["m"][lo:hi], st["v"][lo:hi],
+                           None if st["vmax"] is None else st["vmax"][lo:hi],
+                           fg.compute[lo:hi] if fg.mixed else None, st["step"], g["lr"], b1, b2, g["eps"],
+                           g["weight_decay"], 1.0, g["adamw"], g["maximize"], ams, first, -1)
+
+    def end_ranges(self, fg) -> None:
+        pass
 
     @torch.no_grad()
     def load_state_dict(self, state_dict: dict) -> None:

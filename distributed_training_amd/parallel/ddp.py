@@ -99,6 +99,8 @@ class DistributedDataParallel(nn.Module):
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                        for i, p in enumerate(self.flat.params)]
         self.require_sync = True
+        self._ov = None  # optimizer stepped bucket by bucket inside the backward (overlap_optimizer)
+        self._ov_pending: list = []
         self._reset_iteration()
         logger.debug("DDP: %d params in %d bucket(s), %.2f MB flat", len(self.flat.params), len(self.buckets),
                      self.flat.total * self.flat.grad.element_size() / MiB)
@@ -179,7 +181,11 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, b: int) -> None:
         with prof.range_(f"ddp.bucket{b}.allreduce"):  # host enqueue; the collective runs on the comm stream
+            n = len(self._works)
             self._launch_bucket(b)
+        if self._ov is not None:
+            self._ov_pending.append((b, self._works[-1] if len(self._works) > n else None))
+            self._ov_kick()
 
     def _launch_bucket(self, b: int) -> None:
         bk = self.buckets[b]
@@ -199,6 +205,80 @@ class DistributedDataParallel(nn.Module):
                 sl.div_(self.world_size)  # pre-divide like the torch Reducer (mul_out by 1/ws)
             self._works.append(self.comm.all_reduce(sl, op="sum", async_op=True))
 
+    # ------------------------------------------------------------ optimizer in backward
+    def overlap_optimizer(self, optimizer) -> bool:
+        """Run ``optimizer``'s update bucket by bucket INSIDE the backward, on a side HIP
+        stream, as soon as a bucket's gradients are final (all-reduced across ranks; at one
+        rank: written, including deferred weight gradients) -- the update of the late layers
+        overlaps the backward of the early ones instead of following the whole backward.
+        ``optimizer.step()`` then has nothing left to do for this engine's parameters.
+
+        Valid because a bucket's parameters are read by nothing later in the same backward
+        (a parameter's gradient is final only after every use of it has been
+        differentiated), and the next forward is ordered after the side stream by the
+        end-of-backward callback.  Not for loops that modify gradients between
+        ``backward()`` and ``step()`` (clipping, unscaling): those keep the plain step.
+        The update per element is the fused kernel's, so the result is bit-identical to
+        ``step()``.  Returns False (nothing changed) when the optimizer or the engine do
+        not qualify: a fused SGD / AdamW with one param group over exactly this engine's
+        parameters, on GPU.
+        Reference: the optimizer step of src/distributed_trainer.py:165 after the DDP
+        backward of ddp_strategy.py:18 (torch's ``_apply_optimizer_in_backward`` idea)."""
+        fl = self.flat
+        if optimizer is None:
+            self._ov = None
+            return False
+        if not (fl.grad.is_cuda and hasattr(optimizer, "step_range") and optimizer.range_capable(fl)):
+            return False
+        import weakref
+
+        from ..ops import lm
+
+        self._ov = optimizer
+        self._ov_stream = torch.cuda.Stream(self.device)
+        self._ov_first = True
+        ref = weakref.ref(self)
+
+        def on_flush():
+            me = ref()
+            if me is not None and me._ov is not None:
+                me._ov_kick()
+
+        lm.FLUSH_LISTENERS.append(on_flush)
+        return True
+
+    def _ov_range(self, b: int):
+        bk = self.buckets[b]
+        end = self.flat.master.numel() if b == len(self.buckets) - 1 else bk.end
+        return bk.start, end
+
+    def _ov_kick(self, force: bool = False) -> None:
+        """Launch the update of every bucket whose gradients are final."""
+        if not self._ov_pending:
+            return
+        from ..ops import lm
+
+        if self.world_size == 1 and lm.wgrad_pending():
+            if force:
+                lm.wgrad_flush()  # (its listener comes back here with nothing pending)
+            if lm.wgrad_pending():
+                return
+            if not self._ov_pending:
+                return
+        dev = self.flat.grad.device
+        lm.wgrad_join(dev)  # side-stream weight gradients (DTA_WGRAD_STREAM) joined into the current stream
+        s = self._ov_stream
+        s.wait_stream(torch.cuda.current_stream(dev))
+        pend, self._ov_pending = self._ov_pending, []
+        with torch.cuda.stream(s):
+            for b, work in pend:
+                if work is not None:
+                    work.wait(s)
+                lo, hi = self._ov_range(b)
+                with prof.range_(f"ddp.bucket{b}.optimizer"):
+                    self._ov.step_range(self.flat, lo, hi, self._ov_first)
+                self._ov_first = False
+
     def _whole(self, b: int) -> bool:
         return len(self._pending[b]) == len(self.buckets[b].param_ids)
 
@@ -216,8 +296,15 @@ class DistributedDataParallel(nn.Module):
                     self.flat.rebind_grad(i)  # unused parameter (None -> zeros) or a foreign grad
             self._launch(b)
         self._next = len(self.buckets)
+        if self._ov is not None:
+            self._ov_kick(force=True)
         for w in self._works:
             w.wait()
+        if self._ov is not None:
+            torch.cuda.current_stream(self.flat.grad.device).wait_stream(self._ov_stream)
+            self._ov.end_ranges(self.flat)
+            self._ov_first = True
+            self.flat.stepped_in_backward = True
         self._reset_iteration()
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()  # a timed-out peer exchange raises here, not silently later

@@ -215,7 +215,7 @@ def _train(model_wrapped, opt, batches, steps):
     return losses
 
 
-def _engine_worker(rank, ws, strategy):
+def _engine_worker(rank, ws, strategy, overlap_opt=False):
     import torch.distributed as dist
 
     from distributed_training_amd.models.gpt2 import GPT2
@@ -251,6 +251,8 @@ def _engine_worker(rank, ws, strategy):
                                      param_dtype=torch.bfloat16)
         assert len(w.units) == 3
     opt = FusedSGD(w.parameters(), lr=0.05, momentum=0.9)
+    if overlap_opt:  # the SGD update per bucket on a side stream, after that bucket's all-reduce
+        assert w.overlap_optimizer(opt)
     local = [x[rank * B:(rank + 1) * B] for x in glob]
     losses = _train(w, opt, local, steps)
     comm.poll_errors()
@@ -277,6 +279,13 @@ def _engine_worker(rank, ws, strategy):
 @pytest.mark.parametrize("strategy", ["ddp", "fsdp"])
 def test_engines_multi_rank_shared_gpu(strategy, ws):
     run_gloo(_engine_worker, ws, strategy)
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_ddp_optimizer_in_backward_multi_rank_shared_gpu(ws):
+    """DDP with the optimizer stepped per bucket inside the backward (overlap_optimizer):
+    same trajectory as the one-rank reference, replicas bit-identical."""
+    run_gloo(_engine_worker, ws, "ddp", True)
 
 
 def _offload_worker(rank, ws, opt_name):

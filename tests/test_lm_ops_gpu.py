@@ -539,3 +539,41 @@ def test_ddp_deferred_flush_between_backward_and_bucket_launch(monkeypatch):
         rp = dict(ref.named_parameters())
         for name, p in net.named_parameters():
             assert _rel(p.grad, rp[name].grad) < 2e-2, (it, name)
+
+
+@pytest.mark.parametrize("opt_name,group", [("adamw", "200"), ("adamw", "8"), ("sgd", "0")])
+def test_ddp_optimizer_in_backward_bit_identical(opt_name, group, monkeypatch):
+    """DDP overlap_optimizer (the update of each bucket on a side stream inside the backward,
+    after its deferred weight gradients are written) gives the same bits as backward + step()."""
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW, FusedSGD
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("DTA_WGRAD_GROUP", group)
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    data = [torch.randint(0, 1024, (2, 257), generator=g).to(dev) for _ in range(4)]
+    finals = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=3, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        ddp = DistributedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16,
+                                      bucket_cap_mb=1.0, first_bucket_mb=0.25)
+        assert len(ddp.buckets) >= 3
+        opt = (FusedAdamW(ddp.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1) if opt_name == "adamw"
+               else FusedSGD(ddp.parameters(), lr=0.05, momentum=0.9))
+        assert ddp.overlap_optimizer(opt) if overlap else True
+        losses = []
+        for x in data:
+            opt.zero_grad(set_to_none=True)
+            loss = ddp(x[:, :-1], x[:, 1:])
+            loss.backward()
+            opt.step()
+            losses.append(loss.float())
+        torch.cuda.synchronize()
+        finals.append((torch.stack(losses).cpu(), ddp.flat.master.clone(), ddp.flat.compute.clone()))
+    assert torch.equal(finals[0][0], finals[1][0])
+    assert torch.equal(finals[0][1], finals[1][1])
+    assert torch.equal(finals[0][2], finals[1][2])
+    assert not torch.equal(finals[0][1], finals[0][1] * 0)
