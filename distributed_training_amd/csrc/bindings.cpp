@@ -31,6 +31,8 @@ hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_
                        hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
+hipError_t dta_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int, int, int64_t, int64_t,
+                             hipStream_t);
 hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
 hipError_t dta_swiglu_bwd(const void*, const void*, void*, int64_t, int, hipStream_t);
 hipError_t dta_rope(void*, const float*, const float*, int, int, int, int, int64_t, int64_t, float, hipStream_t);
@@ -572,6 +574,23 @@ torch::Tensor gelu_bwd(torch::Tensor dy, torch::Tensor x, int64_t stream) {
   hip_ok(dta_gelu_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), pick_stream(stream)), "gelu_bwd");
   return dx;
 }
+// out[sid[t]] += dy[perm[t]] over runs of equal sorted ids (in place; out bf16 [V, C], rows 16-byte aligned)
+void embedding_bwd_(torch::Tensor sid, torch::Tensor perm, torch::Tensor dy, torch::Tensor out, int64_t stream) {
+  TORCH_CHECK(sid.is_cuda() && perm.is_cuda() && dy.is_cuda() && out.is_cuda(), "embedding_bwd_: GPU tensors");
+  TORCH_CHECK(sid.scalar_type() == torch::kLong && perm.scalar_type() == torch::kLong && sid.dim() == 1 &&
+                  perm.dim() == 1 && sid.numel() == perm.numel() && sid.is_contiguous() && perm.is_contiguous(),
+              "embedding_bwd_: sorted ids / permutation must be contiguous int64 vectors of one length");
+  check_bf16_2d(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous() && dy.size(0) == sid.numel(), "embedding_bwd_: dy must be contiguous [T, C]");
+  TORCH_CHECK(out.scalar_type() == torch::kBFloat16 && out.dim() == 2 && out.stride(1) == 1 &&
+                  out.size(1) == dy.size(1) && out.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && dy.size(1) % 8 == 0,
+              "embedding_bwd_: out must be bf16 [V, C], unit column stride, 16-byte aligned rows, C % 8 == 0");
+  TORCH_CHECK(sid.numel() < (int64_t)1 << 31, "embedding_bwd_: too many tokens");
+  hip_ok(dta_embedding_bwd(sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dy.data_ptr(), out.data_ptr(),
+                           (int)sid.numel(), (int)dy.size(1), out.stride(0), out.size(0), pick_stream(stream)),
+         "embedding_bwd_");
+}
 torch::Tensor swiglu_fwd(torch::Tensor ab, int64_t stream) {
   check_bf16_2d(ab, "ab");
   const int64_t F2 = ab.size(-1), N = ab.numel() / F2;
@@ -1088,6 +1107,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("db_out") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
+  m.def("embedding_bwd_", &embedding_bwd_);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);

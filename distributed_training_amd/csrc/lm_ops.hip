@@ -495,6 +495,40 @@ static inline int egrid(int64_t n) {
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
 }
 
+
+// ---------------------------------------------------------------- embedding backward
+// dW[id] += sum of the rows of dy whose token is id -- deterministic, no atomics: the ids come
+// sorted (stable) with their source rows; the workgroup of position t works only when t starts
+// a run of equal ids and sums that run's rows in fp32, in source order, then adds the sum into
+// the bf16 row of `out` (read-modify-write of one row: `out` may already hold another use's
+// gradient, e.g. the tied LM head's, which is then accumulated rather than summed by autograd).
+// Reference: the token/position embeddings of the GPT-2 configs (SURVEY.md §2.5 N07 models).
+__global__ void __launch_bounds__(128) embedding_bwd_kernel(const int64_t* __restrict__ sid,
+                                                           const int64_t* __restrict__ perm,
+                                                           const bf16* __restrict__ dy, bf16* __restrict__ out,
+                                                           int T, int C, int64_t ldo, int64_t V) {
+  const int t = blockIdx.x;
+  const int64_t id = sid[t];
+  if ((t > 0 && sid[t - 1] == id) || id < 0 || id >= V) return;
+  int end = t + 1;
+  while (end < T && sid[end] == id) ++end;
+  for (int c = threadIdx.x * 8; c < C; c += blockDim.x * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = t; r < end; ++r) {
+      float f[8];
+      load8(dy + perm[r] * (int64_t)C + c, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    bf16* o = out + id * ldo + c;
+    float f[8];
+    load8(o, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += acc[j];
+    store8(o, f);
+  }
+}
+
 }  // namespace dta
 
 using namespace dta;
@@ -640,5 +674,13 @@ hipError_t dta_cross_entropy(const void* logits, void* dlogits, const int64_t* t
     hipLaunchKernelGGL(cross_entropy_kernel, dim3((unsigned)N), dim3(256), 0, st, L, DL, target, loss, V, grad_scale,
                        ignore_index);
   }
+  return hipGetLastError();
+}
+
+hipError_t dta_embedding_bwd(const int64_t* sid, const int64_t* perm, const void* dy, void* out, int T, int C,
+                             int64_t ldo, int64_t V, hipStream_t st) {
+  if (C % 8 || ldo % 8 || T <= 0) return T <= 0 ? hipSuccess : hipErrorInvalidValue;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(T), dim3(128), 0, st, sid, perm, (const bf16*)dy, (bf16*)out, T, C,
+                     ldo, V);
   return hipGetLastError();
 }

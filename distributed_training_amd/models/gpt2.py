@@ -145,7 +145,8 @@ class GPT2(nn.Module):
         (LM head and loss fused: the logits are never materialised twice)."""
         B, S = idx.shape
         pos = torch.arange(S, device=idx.device)
-        x = self.wte(idx) + self.wpe(pos)
+        # (the token rows' gradient is added straight into the tied head's gradient slice)
+        x = lm.embedding(idx, self.wte.weight) + lm.embedding(pos, self.wpe.weight)
         h = None
         for blk in self.h:
             if self.activation_checkpointing and torch.is_grad_enabled():

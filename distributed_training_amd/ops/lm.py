@@ -768,6 +768,69 @@ def apply_rope(x, cos, sin):
     return rope_reference(x, cos, sin)
 
 
+# ------------------------------------------------------------------ embedding
+def _claimed_slice(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The flat-buffer slice of ``p`` when another use of ``p`` in this backward already
+    wrote its gradient there (:func:`_grad_dest` claimed it; autograd has not accumulated
+    yet): a further contribution can be added into it in place."""
+    tag = getattr(p, "_dta_flat", None)
+    if tag is None or p.grad is not None or getattr(p, "_dta_gdest", None) is not None:
+        return None
+    group, i = tag
+    if not group.steal_ok or i not in group.direct_claimed or group.grad.dtype != p.dtype:
+        return None
+    return group.grad_view(i)
+
+
+def _rows16(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+
+
+class _Embedding(Function):
+    """``F.embedding`` whose backward is the deterministic sorted-run kernel of
+    ``csrc/lm_ops.hip`` (no zero-filled dense gradient + scatter + add).  When the weight's
+    gradient slice already holds another use's gradient (GPT-2's tied LM head writes there
+    first), the token rows are added into it in place and autograd gets None for the
+    weight: the two uses are summed without the [V, C] add, the zero fill and the DDP
+    bucket copy of the sum."""
+
+    @staticmethod
+    def forward(ctx, idx, w):
+        ctx.save_for_backward(idx)
+        ctx.wparam = w
+        return F.embedding(idx, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        w = ctx.wparam
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        sid, perm = torch.sort(idx.reshape(-1), stable=True)
+        dy2 = dy.reshape(-1, w.shape[1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        into = _claimed_slice(w)
+        if into is not None and _rows16(into):
+            native().embedding_bwd_(sid, perm, dy2, into, -1)
+            return None, None
+        dw = _grad_dest(w)
+        if dw is None or not _rows16(dw):  # (an unaligned slice stays claimed: autograd's result is copied in)
+            dw = torch.zeros_like(w)
+        else:
+            dw.zero_()
+        native().embedding_bwd_(sid, perm, dy2, dw, -1)
+        return None, dw
+
+
+def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Embedding lookup (the native deterministic backward on GPU for bf16 tables)."""
+    if idx.is_cuda and w.dtype == torch.bfloat16 and w.shape[1] % 8 == 0 and w.stride(1) == 1 \
+            and w.stride(0) % 8 == 0:
+        return _Embedding.apply(idx, w)
+    return F.embedding(idx, w)
+
+
 # ------------------------------------------------------------------ loss
 class _CrossEntropy(Function):
     @staticmethod
