@@ -204,6 +204,13 @@ def main():
         t = torch.tensor([el], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    if os.environ.get("DTA_SYNC_DEBUG"):
+        # diagnostics: one more (untimed) step with torch's sync debug mode -- every host
+        # synchronisation inside the step (a .item(), a read-back) prints a warning + stack
+        torch.cuda.set_sync_debug_mode("warn")
+        step()
+        torch.cuda.set_sync_debug_mode(0)
+        torch.cuda.synchronize(dev)
     if os.environ.get("DTA_PROFILE_OPS"):
         # diagnostics: one more (untimed) step under torch.profiler on EVERY rank (the
         # step's collectives must match across ranks); rank 0 prints the table

@@ -265,14 +265,6 @@ hipError_t dta_flat_adam(float* p, const void* g, int g_bf16, float* m, float* v
   const int vec = al(p, 16) && al(g, g_bf16 ? 8 : 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
   AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad, vec};
   if (g_bf16)
-      hipLaunchKernelGGL(flat_adam_x2_kernel<bf16>, dim3((int)b), dim3(256), 0, st, p,
-                         reinterpret_cast<const bf16*>(g), m, v, reinterpret_cast<bf16*>(p_bf16), n, step, h);
-    else
-      hipLaunchKernelGGL(flat_adam_x2_kernel<float>, dim3((int)b), dim3(256), 0, st, p,
-                         reinterpret_cast<const float*>(g), m, v, reinterpret_cast<bf16*>(p_bf16), n, step, h);
-    return hipGetLastError();
-  }
-  if (g_bf16)
     hipLaunchKernelGGL(flat_adam_kernel<bf16>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p,
                        reinterpret_cast<const bf16*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
   else

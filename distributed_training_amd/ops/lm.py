@@ -773,8 +773,10 @@ def _claimed_slice(p: torch.Tensor) -> Optional[torch.Tensor]:
     """The flat-buffer slice of ``p`` when another use of ``p`` in this backward already
     wrote its gradient there (:func:`_grad_dest` claimed it; autograd has not accumulated
     yet): a further contribution can be added into it in place."""
+    if getattr(p, "_dta_gdest", None) is not None:
+        return None
     tag = getattr(p, "_dta_flat", None)
-    if tag is None or p.grad is not None or getattr(p, "_dta_gdest", None) is not None:
+    if tag is None or p.grad is not None:
         return None
     group, i = tag
     if not group.steal_ok or i not in group.direct_claimed or group.grad.dtype != p.dtype:
@@ -825,8 +827,10 @@ class _Embedding(Function):
 
 def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """Embedding lookup (the native deterministic backward on GPU for bf16 tables)."""
+    # (FSDP unit views keep torch's backward: parity unpinned for the in-place form there,
+    # tests/test_lm_ops_gpu.py test_tied_embedding_gradient_fsdp_one_rank)
     if idx.is_cuda and w.dtype == torch.bfloat16 and w.shape[1] % 8 == 0 and w.stride(1) == 1 \
-            and w.stride(0) % 8 == 0:
+            and w.stride(0) % 8 == 0 and getattr(w, "_dta_gdest", None) is None:
         return _Embedding.apply(idx, w)
     return F.embedding(idx, w)
 
@@ -875,7 +879,8 @@ class _LinearCrossEntropy(Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam)).mul_(s)
+            # the scale goes on the [N, C] operand, not on the [V, C] product (GPT-2: 6.3 M vs 38.6 M elements)
+            dw = gemm(dlogits, x2 * s, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam))
         return dx, dw, None, None
 
 

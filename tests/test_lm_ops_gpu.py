@@ -621,3 +621,32 @@ def test_tied_embedding_gradient_accumulated_in_place():
         assert fl.grad_is_view(i)
         assert _rel(model.wte.weight.grad, ref.wte.weight.grad) < 2e-2
         assert _rel(model.wpe.weight.grad, ref.wpe.weight.grad) < 2e-2
+
+
+def test_tied_embedding_gradient_fsdp_one_rank():
+    """Same under the FSDP engine (one rank): the token rows go into the root unit's piece of the
+    tied weight in place; the SGD update of wte / wpe matches the unwrapped model's."""
+    import copy
+
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    dev = torch.device(DEV, 0)
+    model = GPT2(GPT2Config(n_layer=2, n_head=2, n_embd=128, vocab_size=512, block_size=128)).to(dev)
+    ref = copy.deepcopy(model).bfloat16()
+    w0 = {k: v.detach().float().clone() for k, v in model.state_dict().items()}
+    f = FullyShardedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, wrap_policy={GPT2.block_class},
+                                 param_dtype=torch.bfloat16)
+    opt = FusedSGD(f.parameters(), lr=1.0)
+    x = torch.randint(0, 64, (2, 129), device=dev)
+    opt.zero_grad(set_to_none=True)
+    f(x[:, :-1], x[:, 1:]).backward()
+    opt.step()
+    ref(x[:, :-1], x[:, 1:]).backward()
+    sd = f.full_state_dict(rank0_only=False)
+    for name in ("wte.weight", "wpe.weight"):
+        upd = w0[name].cpu() - sd[name].float().cpu()
+        assert _rel(upd, dict(ref.named_parameters())[name].grad.cpu()) < 3e-2, name
