@@ -879,8 +879,9 @@ class _LinearCrossEntropy(Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            # the scale goes on the [N, C] operand, not on the [V, C] product (GPT-2: 6.3 M vs 38.6 M elements)
-            dw = gemm(dlogits, x2 * s, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam))
+            # (the scale on the [N, C] operand instead of this [V, C] product measured no better: same-box
+            # GPT-2 pairs 11.12-12.46 vs 11.05-11.39 ms, scripts/gpu_ab_heads.sh)
+            dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam)).mul_(s)
         return dx, dw, None, None
 
 
