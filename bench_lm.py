@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--bucket-mb", default="auto", help="DDP bucket cap in MiB, or auto (xGMI-derived)")
     ap.add_argument("--layers", type=int, default=0, help="override n_layer (0 = config)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="native DDP: launch the step's kernels eagerly instead of replaying the whole step as one "
+                         "hipGraph (engine/step_graph.py)")
     ap.add_argument("--overlap-opt", action="store_true",
                     help="native DDP: AdamW per bucket inside the backward (DistributedDataParallel.overlap_optimizer) "
                          "instead of after it; bit-identical, measured neutral at one rank (README)")
@@ -179,6 +182,26 @@ def main():
         state["loss"] = loss
         prof.pop()
 
+    graphed = None
+    if args.impl == "native" and args.strategy == "ddp" and not args.no_graph:
+        # the whole step (zero_grad, forward, backward with the bucket hooks, AdamW) as ONE hipGraph;
+        # its construction runs 3 eager warm-up steps and the capture (untimed, before the warm-up below)
+        from distributed_training_amd.engine.step_graph import GraphedStep
+
+        def gstep(xb):
+            opt.zero_grad(set_to_none=True)
+            loss = wrapped(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        graphed = GraphedStep(gstep, [data[:args.batch].clone()], warmup=3)
+
+        def step():  # noqa: F811 - the graph replay replaces the eager step
+            i = state["i"] % nb
+            state["i"] += 1
+            state["loss"] = graphed(data[i * args.batch:(i + 1) * args.batch])
+
     def dbarrier():
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[local])
@@ -242,6 +265,7 @@ def main():
 
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
         out["optimizer_in_backward"] = bool(overlap_opt)
+        out["step_graph"] = graphed is not None
         out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": (f"dta/t{v}" if v else "hipblaslt")
                             for k, v in sorted(_lm._GEMM_CHOICE.items())}
     if rank == 0:

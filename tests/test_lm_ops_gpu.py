@@ -650,3 +650,46 @@ def test_tied_embedding_gradient_fsdp_one_rank():
     for name in ("wte.weight", "wpe.weight"):
         upd = w0[name].cpu() - sd[name].float().cpu()
         assert _rel(upd, dict(ref.named_parameters())[name].grad.cpu()) < 3e-2, name
+
+
+def test_graphed_ddp_step_matches_eager():
+    """The whole GPT-2 DDP step (zero_grad, forward, backward with bucket hooks and deferred
+    weight gradients, fused AdamW) captured as one hipGraph and replayed: same losses and
+    the same parameters, bit for bit, as the eager steps on the same batches."""
+    from distributed_training_amd.engine.step_graph import GraphedStep
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    data = [torch.randint(0, 1024, (2, 257), generator=g).to(dev) for _ in range(4)]
+    seq = [data[0]] * 3 + data[1:]  # GraphedStep's 3 warm-up steps train on the static batch
+    out = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        ddp = DistributedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+        opt = FusedAdamW(ddp.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+
+        def step(xb):
+            opt.zero_grad(set_to_none=True)
+            loss = ddp(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        losses = []
+        if graphed:
+            gs = GraphedStep(step, [data[0].clone()], warmup=3)
+            for xb in seq[3:]:
+                losses.append(gs(xb).float().clone())
+        else:
+            for xb in seq:
+                losses.append(step(xb).float().clone())
+            losses = losses[3:]
+        torch.cuda.synchronize()
+        out.append((torch.stack(losses).cpu(), ddp.flat.master.clone()))
+    assert torch.equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
