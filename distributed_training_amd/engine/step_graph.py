@@ -41,9 +41,10 @@ class GraphedStep:
         dev = self.static[0].device
         self.stream = torch.cuda.Stream(dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
+        self.warmup_losses = []
         with torch.cuda.stream(self.stream):
             for _ in range(max(1, warmup)):
-                step_fn(*self.static)
+                self.warmup_losses.append(step_fn(*self.static))
         torch.cuda.current_stream(dev).wait_stream(self.stream)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()

@@ -72,6 +72,7 @@ class TrainingConfig:
     fault_injection: Optional[Dict[str, int]] = None
     cpu_offload: bool = False        # FSDP: fp32 shards, gradients and optimizer on the host
     optimizer_in_backward: bool = False  # DDP on GPU: fused update per bucket inside the backward (no grad_clip)
+    step_graph: bool = False         # DDP on GPU: whole step replayed as one hipGraph (engine/step_graph.py)
     extra: Dict[str, Any] = field(default_factory=dict)
 
 
@@ -192,7 +193,27 @@ class Trainer:
             logger.debug(f"fused step programs not used: {why}; {why_lin}")
 
     # ------------------------------------------------------------------ loop
+    def _graph_eligible(self, source: torch.Tensor, targets: torch.Tensor) -> bool:
+        c = self.config
+        return (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip
+                and isinstance(self._strategy, DDPStrategy) and hasattr(self.model, "flat")
+                and not c.desync_check_every)
+
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        if self._graph_eligible(source, targets):
+            g = getattr(self, "_graphed", None)
+            if g is None:
+                from .step_graph import GraphedStep
+
+                # one eager step on this batch (the warm-up), then the capture
+                self._graphed = GraphedStep(self._run_batch_eager, [source.clone(), targets.clone()], warmup=1)
+                return self._graphed.warmup_losses[-1]
+            if all(s.shape == x.shape and s.dtype == x.dtype for s, x in zip(g.static, (source, targets))):
+                return g(source, targets)
+            # a batch of another shape (an epoch's short last batch): the eager step
+        return self._run_batch_eager(source, targets)
+
+    def _run_batch_eager(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         # roctx ranges (DTA_ROCTX=1): step phases on the rocprofv3 --marker-trace timeline
         self.optimizer.zero_grad()
         with prof.range_("forward"):

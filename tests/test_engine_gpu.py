@@ -137,3 +137,43 @@ def test_trainer_end_to_end_gpu(tmp_path):
             torch.testing.assert_close(ck["MODEL_STATE"][k].to(v.device), v)
     finally:
         env.teardown()
+
+
+def test_trainer_step_graph_matches_eager(tmp_path):
+    """train.step_graph=true (generic DDP path): the first batch runs eagerly and is captured,
+    later full batches replay the graph, an epoch's short last batch runs eagerly -- the final
+    weights equal the all-eager run's bit for bit."""
+    import os
+
+    from distributed_training_amd.app import prepare_dataloader
+    from distributed_training_amd.data.datasets import MyTrainDataset
+    from distributed_training_amd.engine.trainer import Trainer, TrainingConfig
+    from distributed_training_amd.models.mlp import MLP
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.env import DistributedEnvironment
+
+    os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": "29733"})
+    env = DistributedEnvironment("cuda")
+    env.setup()
+    try:
+        finals = []
+        for graph in (False, True):
+            torch.manual_seed(0)
+            ds = MyTrainDataset(100, 20, 1, seed=0)  # 3 full batches + one of 4 per epoch
+            model = MLP(20, 256, 1)
+            opt = FusedSGD(model.parameters(), lr=1e-2, momentum=0.9)
+            cfg = TrainingConfig(max_epochs=2, save_every=5, batch_size=32, learning_rate=1e-2,
+                                 snapshot_path=tmp_path / f"s{int(graph)}.pt", loss="mse", fused_step=False,
+                                 step_graph=graph)
+            tr = Trainer(model, prepare_dataloader(ds, 32), opt, cfg, env)
+            assert tr._fused is None
+            tr.train(2)
+            torch.cuda.synchronize()
+            if graph:
+                assert tr._graphed is not None and tr._graphed.replays == 5, tr._graphed.replays
+            finals.append({k: v.detach().clone() for k, v in tr.model.state_dict().items()})
+        for k in finals[0]:
+            assert torch.equal(finals[0][k], finals[1][k]), k
+    finally:
+        env.teardown()
