@@ -529,7 +529,8 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
         cb = _grad_dest(b) if with_bias else None
         thr = _group_threshold()
         if thr and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
-                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0:
+                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0 \
+                and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
             # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
             # holds ALIASES of the slices, never the tensors returned to autograd: a second
             # reference to a returned gradient makes AccumulateGrad clone it instead of
