@@ -774,8 +774,15 @@ def _claimed_slice(p: torch.Tensor) -> Optional[torch.Tensor]:
     """The flat-buffer slice of ``p`` when another use of ``p`` in this backward already
     wrote its gradient there (:func:`_grad_dest` claimed it; autograd has not accumulated
     yet): a further contribution can be added into it in place."""
-    if getattr(p, "_dta_gdest", None) is not None:
-        return None
+    gd = getattr(p, "_dta_gdest", None)
+    if gd is not None:  # FSDP unit view: its piece of the unit's gradient buffer (parallel/fsdp.py piece_dest)
+        unit = getattr(getattr(gd, "func", None), "__self__", None)
+        e = getattr(gd, "args", (None,))[0]
+        if unit is None or not getattr(unit, "in_backward", False) or e not in getattr(unit, "_claimed", ()):
+            return None
+        o, n = unit.offsets[e], unit.numels[e]
+        d = unit.grad_buffer()[o:o + n].view(unit.shapes[e])
+        return d if d.dtype == p.dtype else None
     tag = getattr(p, "_dta_flat", None)
     if tag is None or p.grad is not None:
         return None
@@ -828,10 +835,8 @@ class _Embedding(Function):
 
 def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """Embedding lookup (the native deterministic backward on GPU for bf16 tables)."""
-    # (FSDP unit views keep torch's backward: parity unpinned for the in-place form there,
-    # tests/test_lm_ops_gpu.py test_tied_embedding_gradient_fsdp_one_rank)
     if idx.is_cuda and w.dtype == torch.bfloat16 and w.shape[1] % 8 == 0 and w.stride(1) == 1 \
-            and w.stride(0) % 8 == 0 and getattr(w, "_dta_gdest", None) is None:
+            and w.stride(0) % 8 == 0:
         return _Embedding.apply(idx, w)
     return F.embedding(idx, w)
 

@@ -241,9 +241,10 @@ class _Unit:
         second use of the same weight must not overwrite it before autograd sums)."""
         if e in self._claimed or not self.in_backward:
             return None
-        self._claimed.add(e)
+        buf = self.grad_buffer()  # (first call of the backward: creates the buffer and resets the claims,
+        self._claimed.add(e)      # so the claim goes in after it -- else a weight used twice got its piece twice)
         o, n = self.offsets[e], self.numels[e]
-        return self.grad_buffer()[o:o + n].view(self.shapes[e])
+        return buf[o:o + n].view(self.shapes[e])
 
     # ---------------------------------------------------------- backward
     def _post_backward(self, full: torch.Tensor) -> None:

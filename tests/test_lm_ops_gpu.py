@@ -693,3 +693,41 @@ def test_graphed_ddp_step_matches_eager():
         out.append((torch.stack(losses).cpu(), ddp.flat.master.clone()))
     assert torch.equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_fsdp_weight_used_twice_first_claim():
+    """FSDP unit whose FIRST gradient piece of the backward belongs to a weight used twice: the
+    buffer creation of that first claim must not erase the claim (the second use would get the
+    same piece and overwrite the first use's gradient)."""
+    import copy
+
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = lm.Linear(256, 256)
+            self.shared = lm.Linear(256, 256)
+
+        def forward(self, x):
+            return self.shared(self.shared(self.a(x)))
+
+    torch.manual_seed(8)
+    dev = torch.device(DEV, 0)
+    net = Net().to(dev)
+    ref = copy.deepcopy(net).bfloat16()
+    w0 = {k: v.detach().float().cpu().clone() for k, v in net.state_dict().items()}
+    f = FullyShardedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    opt = FusedSGD(f.parameters(), lr=1.0)
+    x = torch.randn(512, 256, device=dev).bfloat16()
+    opt.zero_grad(set_to_none=True)
+    f(x).float().square().mean().backward()
+    opt.step()
+    ref(x).float().square().mean().backward()
+    sd = f.full_state_dict(rank0_only=False)
+    rp = dict(ref.named_parameters())
+    for name in rp:
+        upd = w0[name] - sd[name].float().cpu()
+        assert _rel(upd, rp[name].grad.float().cpu()) < 3e-2, name
