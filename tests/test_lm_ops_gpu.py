@@ -731,3 +731,4 @@ def test_fsdp_weight_used_twice_first_claim():
     for name in rp:
         upd = w0[name] - sd[name].float().cpu()
         assert _rel(upd, rp[name].grad.float().cpu()) < 3e-2, name
+
