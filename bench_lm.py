@@ -195,8 +195,14 @@ def main():
             opt.step()
             return loss
 
-        graphed = GraphedStep(gstep, [data[:args.batch].clone()], warmup=3)
+        try:
+            graphed = GraphedStep(gstep, [data[:args.batch].clone()], warmup=3)
+        except RuntimeError as e:  # a step that cannot be captured here keeps the eager launches
+            print(f"[bench_lm] step graph unavailable ({e}); eager step", file=sys.stderr)
+            torch.cuda.synchronize(dev)
+            graphed = None
 
+    if graphed is not None:
         def step():  # noqa: F811 - the graph replay replaces the eager step
             i = state["i"] % nb
             state["i"] += 1
