@@ -114,6 +114,8 @@ def training_config_from(cfg, model=None) -> TrainingConfig:
         desync_check_every=int(_get(t, "desync_check_every", 0) or 0),
         fault_injection=_get(t, "fault_injection", None),
         cpu_offload=bool(_get(t, "cpu_offload", False)),
+        optimizer_in_backward=bool(_get(t, "optimizer_in_backward", False)),
+        step_graph=bool(_get(t, "step_graph", False)),
     )
 
 
