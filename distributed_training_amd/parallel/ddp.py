@@ -226,7 +226,7 @@ class DistributedDataParallel(nn.Module):
         backward of ddp_strategy.py:18 (torch's ``_apply_optimizer_in_backward`` idea)."""
         fl = self.flat
         if optimizer is None:
-            self._ov = None
+            self._ov = None  # (its flush listener stays registered but does nothing)
             return False
         if not (fl.grad.is_cuda and hasattr(optimizer, "step_range") and optimizer.range_capable(fl)):
             return False
@@ -241,7 +241,10 @@ class DistributedDataParallel(nn.Module):
 
         def on_flush():
             me = ref()
-            if me is not None and me._ov is not None:
+            if me is None:  # engine gone: drop this listener
+                if on_flush in lm.FLUSH_LISTENERS:
+                    lm.FLUSH_LISTENERS.remove(on_flush)
+            elif me._ov is not None:
                 me._ov_kick()
 
         lm.FLUSH_LISTENERS.append(on_flush)
