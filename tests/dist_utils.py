@@ -1,6 +1,7 @@
 """Helpers for multi-process CPU (gloo) tests."""
 import os
 import socket
+import time
 import traceback
 
 import torch.distributed as dist
@@ -29,23 +30,42 @@ def _entry(rank, ws, port, fn, args, errq):
             dist.destroy_process_group()
 
 
-def run_gloo(fn, ws: int = 2, *args):
-    """Run ``fn(rank, ws, *args)`` in ``ws`` gloo processes; re-raise failures."""
+def run_gloo(fn, ws: int = 2, *args, timeout: float = 300.0, attempts: int = 3):
+    """Run ``fn(rank, ws, *args)`` in ``ws`` gloo processes; re-raise failures.
+
+    The first failing rank ends the run at once (its peers would otherwise wait in a
+    collective until the timeout).  A rendezvous port taken between :func:`free_port`
+    and rank 0's bind (EADDRINUSE on a busy host) is retried on a fresh port."""
     ctx = mp.get_context("spawn")
-    errq = ctx.SimpleQueue()
-    port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, ws, port, fn, args, errq)) for r in range(ws)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join(300)
-    errs = []
-    while not errq.empty():
-        errs.append(errq.get())
-    for p in procs:
-        if p.is_alive():
-            p.kill()
-    if errs:
-        raise AssertionError("\n".join(f"rank {r}:\n{tb}" for r, tb in errs))
-    bad = [p.exitcode for p in procs if p.exitcode != 0]
-    assert not bad, f"worker exit codes {bad}"
+    for attempt in range(attempts):
+        errq = ctx.SimpleQueue()
+        port = free_port()
+        procs = [ctx.Process(target=_entry, args=(r, ws, port, fn, args, errq)) for r in range(ws)]
+        for p in procs:
+            p.start()
+        deadline = time.monotonic() + timeout
+        errs = []
+        while time.monotonic() < deadline:
+            while not errq.empty():
+                errs.append(errq.get())
+            if errs or not any(p.is_alive() for p in procs) \
+                    or any(p.exitcode not in (None, 0) for p in procs):
+                break
+            time.sleep(0.05)
+        if errs:  # (give the failing rank's peers no time to write more)
+            time.sleep(0.5)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        for p in procs:
+            p.join(10)
+        while not errq.empty():
+            errs.append(errq.get())
+        if errs and attempt + 1 < attempts and any("EADDRINUSE" in tb or "address already in use" in tb
+                                                   for _, tb in errs):
+            continue
+        if errs:
+            raise AssertionError("\n".join(f"rank {r}:\n{tb}" for r, tb in errs))
+        bad = [p.exitcode for p in procs if p.exitcode != 0]
+        assert not bad, f"worker exit codes {bad} (timeout {timeout:.0f} s)"
+        return

@@ -114,8 +114,10 @@ def test_trainer_end_to_end_gpu(tmp_path):
     from distributed_training_amd.ops.optim import FusedSGD
     from distributed_training_amd.parallel.env import DistributedEnvironment
 
+    from dist_utils import free_port
+
     os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": "29731"})
+                       "MASTER_PORT": str(free_port())})
     env = DistributedEnvironment("cuda")
     env.setup()
     try:
@@ -152,8 +154,10 @@ def test_trainer_step_graph_matches_eager(tmp_path):
     from distributed_training_amd.ops.optim import FusedSGD
     from distributed_training_amd.parallel.env import DistributedEnvironment
 
+    from dist_utils import free_port
+
     os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": "29733"})
+                       "MASTER_PORT": str(free_port())})
     env = DistributedEnvironment("cuda")
     env.setup()
     try:
