@@ -122,9 +122,10 @@ def main():
             wrapped = DistributedDataParallel(model, comm=comm, device=dev, param_dtype=torch.bfloat16,
                                               bucket_cap_mb=args.bucket_mb if args.bucket_mb == "auto" else float(args.bucket_mb))
         else:
-            from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+            from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
 
-            wrapped = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy={M.block_class},
+            # blocks + (Llama) the embedding and the output head as units of their own
+            wrapped = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=lm_wrap_policy(model),
                                                param_dtype=torch.bfloat16)
         opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
         overlap_opt = args.strategy == "ddp" and args.overlap_opt and wrapped.overlap_optimizer(opt)
@@ -195,11 +196,9 @@ def main():
             opt.step()
             return loss
 
-        try:
-            graphed = GraphedStep(gstep, [data[:args.batch].clone()], warmup=3)
-        except RuntimeError as e:  # a step that cannot be captured here keeps the eager launches
-            print(f"[bench_lm] step graph unavailable ({e}); eager step", file=sys.stderr)
-            torch.cuda.synchronize(dev)
+        graphed = GraphedStep(gstep, [data[:args.batch].clone()], warmup=3, engine=wrapped)
+        if not graphed.ok:  # a step that cannot be captured (all ranks agreed) keeps the eager launches
+            print(f"[bench_lm] step graph unavailable ({graphed.error}); eager step", file=sys.stderr)
             graphed = None
 
     if graphed is not None:
@@ -261,6 +260,7 @@ def main():
            "samples_per_s": round(args.batch * ws * args.steps / el, 2), "mfu": round(mfu, 4),
            "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(peak_mem / 1e9, 2),
            "final_loss": float(state["loss"].item()),
+           "fsdp_units": (len(wrapped.units) if args.impl == "native" and args.strategy == "fsdp" else None),
            "comm": ("none: one rank (DDP skips the all-reduce, FSDP runs NO_SHARD)" if ws == 1 else
                     type(getattr(wrapped, "comm", None)).__name__ if args.impl == "native" else "torch"),
            "config": {"model": args.model, "layers": cfg.n_layer, "global_batch": args.batch * ws,
@@ -324,6 +324,7 @@ def _patch_torch_ops():
     lm.linear = F.linear
     lm.linear_cross_entropy = linear_ce
     lm.gelu = lambda x: F.gelu(x, approximate="tanh")
+    lm.embedding = F.embedding
     lm.swiglu = lambda ab: F.silu(ab.chunk(2, -1)[0]) * ab.chunk(2, -1)[1]
     lm.apply_rope = lm.rope_reference
 

@@ -79,7 +79,13 @@ def prepare_dataloader(dataset: Dataset, batch_size: int) -> DeviceDataLoader:
 def _wrap_policy(name, model):
     if not name:
         return None
-    if name == "block":
+    if name == "block":  # blocks + the model's extra units (Llama: embedding, output head)
+        if getattr(model, "block_class", None) is None:
+            return None
+        from .parallel.fsdp import lm_wrap_policy
+
+        return lm_wrap_policy(model)
+    if name == "block_only":  # blocks only (embedding / head in the root unit)
         return getattr(model, "block_class", None) and {model.block_class}
     return None
 

@@ -49,8 +49,12 @@ def linear_eligible(module: nn.Module, optimizer, loader, loss: str, device: tor
     g = optimizer.param_groups[0]
     if "momentum" not in g or "betas" in g:
         return "optimizer is not SGD"
+    if g.get("momentum", 0):
+        # the program keeps its momentum in its own buffer, which the optimizer's state (and so a
+        # checkpoint's OPTIM_STATE) would never see; the reference's SGD has none (distributed_trainer.py:200)
+        return "SGD with momentum runs on the generic engine path"
     C, I = module.weight.shape
-    if not native().linear_step_supported(I, C, loader.batch_size, bool(g.get("momentum", 0))):
+    if not native().linear_step_supported(I, C, loader.batch_size, False):
         return "shape outside the fused kernel's limits"
     return None
 

@@ -17,28 +17,55 @@ What makes the native step capturable:
   the same overwrites), and the fused optimizers keep their step count on the device;
 * the per-shape GEMM choice (``ops/lm.py`` ``_pick``, which times candidates with a
   synchronize) is made during the eager warm-up steps, before capture.
-Collectives inside the step are captured too (RCCL and the IPC push kernels are
-graph-capturable); the FSDP engine is not (it frees and re-allocates unit storage
-between units), so it keeps the eager step.
+The bucket collectives of the DDP engine are captured too (RCCL and the IPC push
+kernels are graph-capturable; tests/test_ipc_gpu.py replays a captured multi-rank
+step against the eager one); the FSDP engine is not (it frees and re-allocates unit
+storage between units), so it keeps the eager step.
+
+Host logic that the replay skips is redone around it:
+* the communicator's error poll of the engine's end-of-backward finalize (a peer
+  exchange that timed out must raise, not leave partial sums): :meth:`__call__`
+  polls after every replay (a host-mapped flag, no device sync);
+* a capture that fails (an op that cannot be recorded) leaves the engine mid-step:
+  its hook state and the deferred weight-gradient queue are reset, and all ranks
+  agree (MIN over the engine's communicator) before any of them falls back to the
+  eager step -- one rank replaying while another runs eagerly would issue different
+  collectives and hang.  ``ok`` is False then and the caller runs eagerly.
 
 The static inputs are the tensors the step reads; :meth:`__call__` copies a new
 batch into them (device-to-device) before the replay.
 """
 from __future__ import annotations
 
-from typing import Callable, Sequence
+import logging
+from typing import Any, Callable, Optional, Sequence
 
 import torch
+
+logger = logging.getLogger(__name__)
+
+
+def _agree_all_ok(engine: Any, ok: bool, device: torch.device) -> bool:
+    """MIN of ``ok`` over the engine's ranks (eager collective, outside any capture)."""
+    comm = getattr(engine, "comm", None)
+    if comm is None or getattr(comm, "world_size", 1) <= 1:
+        return ok
+    t = torch.tensor([1.0 if ok else 0.0], device=device if comm.device.type == "cuda" else "cpu")
+    comm.all_reduce(t, op="min")
+    return float(t.item()) >= 1.0
 
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[..., torch.Tensor], static_inputs: Sequence[torch.Tensor],
-                 warmup: int = 3):
+                 warmup: int = 3, engine: Optional[Any] = None):
         """``step_fn(*static_inputs)`` runs one full training step (zero_grad, forward,
         backward, optimizer step) and returns the loss tensor.  ``warmup`` eager steps
-        run first on the capture stream (they are real training steps)."""
+        run first on the capture stream (they are real training steps).  ``engine``:
+        the DDP engine of the step (error polls, capture-failure reset, rank agreement)."""
         self.static = list(static_inputs)
+        self.engine = engine
         dev = self.static[0].device
+        self.device = dev
         self.stream = torch.cuda.Stream(dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
         self.warmup_losses = []
@@ -47,15 +74,56 @@ class GraphedStep:
                 self.warmup_losses.append(step_fn(*self.static))
         torch.cuda.current_stream(dev).wait_stream(self.stream)
         torch.cuda.synchronize(dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.stream):
-            self.loss = step_fn(*self.static)
+        self.graph: Optional[torch.cuda.CUDAGraph] = torch.cuda.CUDAGraph()
+        self.error: Optional[BaseException] = None
+        self.loss: Optional[torch.Tensor] = None
+        try:
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.loss = step_fn(*self.static)
+        except Exception as e:  # noqa: BLE001 - reported through .ok / .error after the agreement
+            self.error = e
+            self._abandon()
+        torch.cuda.synchronize(dev)
+        if not _agree_all_ok(engine, self.error is None, dev):
+            if self.error is None:
+                self.error = RuntimeError("step capture failed on another rank")
+            logger.warning("step graph disabled, eager step used: %s", self.error)
+            self.graph = None
+            self.loss = None
         self.replays = 0
 
+    @property
+    def ok(self) -> bool:
+        return self.graph is not None
+
+    def _abandon(self) -> None:
+        """Undo the host state a half-captured step left behind."""
+        from ..ops import lm
+
+        lm.abandon_step()
+        reset = getattr(self.engine, "reset_iteration", None)
+        if reset is not None:
+            reset()
+
+    def poll(self) -> None:
+        comm = getattr(self.engine, "comm", None)
+        if comm is None or getattr(self.engine, "world_size", 1) <= 1:
+            return
+        watch = getattr(comm, "watch_stream", None)
+        if watch is not None:  # the replay's captured collectives under the communicator's deadline
+            watch(torch.cuda.current_stream(self.device), "step graph replay")
+        poll = getattr(comm, "poll_errors", None)
+        if poll is not None:
+            poll()
+
     def __call__(self, *inputs: torch.Tensor) -> torch.Tensor:
+        if self.graph is None:
+            raise RuntimeError(f"step graph unavailable ({self.error}); run the eager step")
         for s, x in zip(self.static, inputs):
             if x is not s:
                 s.copy_(x, non_blocking=True)
         self.graph.replay()
         self.replays += 1
+        self.poll()  # the engine finalize's error check, which the replay does not run
+        assert self.loss is not None
         return self.loss

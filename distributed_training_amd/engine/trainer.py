@@ -194,10 +194,15 @@ class Trainer:
 
     # ------------------------------------------------------------------ loop
     def _graph_eligible(self, source: torch.Tensor, targets: torch.Tensor) -> bool:
+        from ..ops.optim import FusedAdamW, FusedSGD
+
         c = self.config
+        # only the fused optimizers keep their step count on the device (torch's AdamW keeps it on the
+        # host and cannot be captured)
         return (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip
                 and isinstance(self._strategy, DDPStrategy) and hasattr(self.model, "flat")
-                and not c.desync_check_every)
+                and isinstance(self.optimizer, (FusedSGD, FusedAdamW))
+                and not c.desync_check_every and getattr(self, "_graphed", None) is not False)
 
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         if self._graph_eligible(source, targets):
@@ -205,9 +210,12 @@ class Trainer:
             if g is None:
                 from .step_graph import GraphedStep
 
-                # one eager step on this batch (the warm-up), then the capture
-                self._graphed = GraphedStep(self._run_batch_eager, [source.clone(), targets.clone()], warmup=1)
-                return self._graphed.warmup_losses[-1]
+                # one eager step on this batch (the warm-up), then the capture; a failed capture
+                # (agreed on by every rank) leaves the eager step for the rest of the run
+                g = GraphedStep(self._run_batch_eager, [source.clone(), targets.clone()], warmup=1,
+                                engine=self.model)
+                self._graphed = g if g.ok else False
+                return g.warmup_losses[-1]
             if all(s.shape == x.shape and s.dtype == x.dtype for s, x in zip(g.static, (source, targets))):
                 return g(source, targets)
             # a batch of another shape (an epoch's short last batch): the eager step

@@ -103,10 +103,10 @@ class Llama(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.vocab_size = cfg.vocab_size
-        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.tok_embeddings = lm.Embedding(cfg.vocab_size, cfg.n_embd)
         self.layers = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
         self.norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
-        self.output = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+        self.output = lm.LMHead(cfg.n_embd, cfg.vocab_size, bias=False)
         if cfg.tie_weights:
             self.output.weight = self.tok_embeddings.weight
         cos, sin = lm.rope_tables(cfg.block_size, cfg.n_embd // cfg.n_head, cfg.rope_theta)
@@ -122,6 +122,13 @@ class Llama(nn.Module):
     def enable_activation_checkpointing(self, on: bool = True):
         self.activation_checkpointing = on
 
+    def fsdp_extra_units(self):
+        """Modules that are FSDP units of their own besides the blocks (parallel/fsdp.py
+        ``lm_wrap_policy``): the embedding and the output head, 525 M parameters each at 8B --
+        in the root unit they would be gathered synchronously before the forward and held
+        through the whole backward.  Tied (one weight, used first and last): kept in the root."""
+        return [] if self.cfg.tie_weights else [self.tok_embeddings, self.output]
+
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
@@ -136,9 +143,7 @@ class Llama(nn.Module):
             else:
                 x, h = blk(x, cos, sin, h)
         _, y = self.norm.add_forward(x, h)
-        if targets is not None:
-            return lm.linear_cross_entropy(y, self.output.weight, targets)
-        return self.output(y)
+        return self.output(y, targets)
 
     def flops_per_token(self, seq_len: int) -> float:
         c = self.cfg

@@ -401,19 +401,49 @@ _SIDE_CB = [False]
 _FWD_GEN = [0]
 
 
+_CLOSED_GEN = [0]  # every forward generation <= this one has had its backward finalized
+_GEN_USES = [0]    # weight uses (that will be differentiated) counted in the current generation
+
+
 def new_forward_generation() -> None:
     """Start counting native-Linear weight uses afresh (called per DDP forward)."""
+    if _GEN_USES[0] == 0:  # (a no-grad forward: no backward will close it)
+        _CLOSED_GEN[0] = _FWD_GEN[0]
+    if _CLOSED_GEN[0] == _FWD_GEN[0]:  # the previous step's backward ran to its end
+        _SIDE_CB[0] = False  # (a backward that raised never ran its end-of-backward join callback)
+        _DEFER.clear()  # (nor flushed what it deferred: those gradients belong to an abandoned step)
+        _DEFER_TILES[0] = 0
     _FWD_GEN[0] += 1
-    _SIDE_CB[0] = False  # (a backward that raised never ran its end-of-backward join callback)
-    _DEFER.clear()  # (nor flushed what it deferred: those gradients belong to an abandoned step)
+    _GEN_USES[0] = 0
+
+
+def abandon_step() -> None:
+    """A step stopped midway (a failed graph capture): drop what its backward queued."""
+    _SIDE_CB[0] = False
+    _DEFER.clear()
     _DEFER_TILES[0] = 0
+    _GEN_USES[0] = 0
+    _CLOSED_GEN[0] = _FWD_GEN[0]
+
+
+def close_forward_generations() -> None:
+    """The backward of every forward so far is finished (the DDP engine's end-of-backward
+    finalize): a weight's uses in those generations no longer count against a later one."""
+    _CLOSED_GEN[0] = _FWD_GEN[0]
 
 
 def _count_use(w: torch.Tensor) -> None:
-    if getattr(w, "_dta_gen", -1) != _FWD_GEN[0]:
+    g = getattr(w, "_dta_gen", -1)
+    if g != _FWD_GEN[0]:
+        # two forwards before one backward (e.g. a loss summed over two calls): a use in an
+        # earlier generation whose backward has not run yet is a second use of the weight in
+        # that coming backward, so the weight is not single-use (no deferred / side-stream
+        # gradient: its returned slice would be summed before the deferred GEMM wrote it)
+        prev_open = g > _CLOSED_GEN[0] and getattr(w, "_dta_uses", 0) > 0
         w._dta_gen = _FWD_GEN[0]
-        w._dta_uses = 0
+        w._dta_uses = 1 if prev_open else 0
     w._dta_uses += 1
+    _GEN_USES[0] += 1
 
 
 def _single_use(w: Optional[torch.Tensor]) -> bool:
@@ -684,6 +714,30 @@ class Linear(torch.nn.Linear):
 
     def forward(self, x):
         return linear(x, self.weight, self.bias)
+
+
+class LMHead(torch.nn.Linear):
+    """The untied output projection as a module of its own (same parameter / state-dict key as
+    ``nn.Linear``): ``head(y, targets)`` is the fused head + token cross-entropy
+    (:func:`linear_cross_entropy`), ``head(y)`` the logits.  Being a module call makes it an
+    FSDP unit of its own (parallel/fsdp.py ``lm_wrap_policy``): gathered by a prefetch during the
+    last blocks, its gradient reduce-scattered as soon as the head's backward -- the first of
+    the backward -- is done."""
+
+    def forward(self, y, targets=None):
+        if targets is not None:
+            return linear_cross_entropy(y, self.weight, targets)
+        return linear(y, self.weight, self.bias)
+
+
+class Embedding(torch.nn.Embedding):
+    """``nn.Embedding`` (same parameter / key) through :func:`embedding` (the native backward).
+    Its backward reads no weight values, so as an FSDP unit it is never re-gathered for backward."""
+
+    fsdp_backward_needs_params = False
+
+    def forward(self, idx):
+        return embedding(idx, self.weight)
 
 
 # ------------------------------------------------------------------ activations

@@ -19,10 +19,13 @@ Reference parity: replaces the implicit c10d NCCL/Gloo process group of
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 import sys
-from typing import List, Optional
+import threading
+import time
+from typing import Callable, Deque, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -163,16 +166,111 @@ class TorchComm(Communicator):
             dist.barrier(group=self.group)
 
 
+def comm_timeout_s() -> float:
+    """``DTA_COMM_TIMEOUT_S``: deadline of one device collective (default 600 s; <= 0: no watchdog)."""
+    v = os.environ.get("DTA_COMM_TIMEOUT_S", "600").strip()
+    return float(v) if v else 600.0
+
+
+class CommWatchdog:
+    """Host-side deadline on device collectives -- what c10d ProcessGroupNCCL's watchdog
+    gives the reference's ``init_process_group`` (src/distributed_trainer.py:61-62).
+
+    Every collective the communicator enqueues registers the event recorded behind it on
+    the comm stream (:meth:`track`); a daemon thread queries the oldest pending event
+    every ``poll_s``.  One that is still pending ``timeout_s`` after its enqueue means a
+    peer never joined: the thread calls ``on_timeout`` (RcclComm: ``ncclCommAbort``, which
+    also ends the kernels spinning on the dead peer), records the error, and the next
+    :meth:`raise_if_error` on the training thread -- every ``CommWork.wait``, the DDP
+    finalize / graph-replay poll, ``barrier`` -- raises ``RuntimeError``.  If the training
+    thread does not get there within ``exit_grace_s`` (blocked in a host sync that the
+    abort did not release), the process exits with status 3 (``DTA_COMM_TIMEOUT_EXIT=0``
+    disables that), so a hung rank ends the job instead of holding the node.  No
+    device synchronisation: tracking is a deque append per collective."""
+
+    def __init__(self, name: str, timeout_s: float, on_timeout: Callable[[], None], poll_s: float = 0.0,
+                 exit_grace_s: float = 60.0):
+        self.name = name
+        self.timeout_s = float(timeout_s)
+        self.poll_s = float(poll_s) if poll_s > 0 else max(0.05, min(2.0, self.timeout_s / 20))
+        self.exit_grace_s = float(exit_grace_s)
+        self.on_timeout = on_timeout
+        self.error: Optional[str] = None
+        self._pending: Deque[Tuple[object, float, str]] = collections.deque()
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._reported = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+
+    def track(self, event, desc: str) -> None:
+        """``event``: anything with ``query() -> bool`` (a ``torch.cuda.Event`` recorded after the collective)."""
+        if self.timeout_s <= 0:
+            return
+        with self._lock:
+            self._pending.append((event, time.monotonic(), desc))
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name=f"dta-comm-watchdog-{self.name}", daemon=True)
+            self._thread.start()
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._pending)
+
+    def check(self) -> bool:
+        """One watchdog pass; True if the deadline expired (now or before)."""
+        if self.error is not None:
+            return True
+        now = time.monotonic()
+        with self._lock:
+            while self._pending and self._pending[0][0].query():
+                self._pending.popleft()
+            head = self._pending[0] if self._pending else None
+        if head is None or now - head[1] <= self.timeout_s:
+            return False
+        self.error = (f"{self.name}: collective '{head[2]}' not complete {now - head[1]:.1f} s after its enqueue "
+                      f"(DTA_COMM_TIMEOUT_S={self.timeout_s:g}); communicator aborted")
+        print(f"[dta watchdog] {self.error}", file=sys.stderr, flush=True)
+        try:
+            self.on_timeout()
+        except Exception as e:  # noqa: BLE001 - the error is reported either way
+            print(f"[dta watchdog] abort failed: {e}", file=sys.stderr, flush=True)
+        return True
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.poll_s):
+            if self.check():
+                break
+        if self.error is None or self._stop.is_set():
+            return
+        if os.environ.get("DTA_COMM_TIMEOUT_EXIT", "1") != "0" and not self._reported.wait(self.exit_grace_s):
+            print(f"[dta watchdog] training thread did not observe the timeout within {self.exit_grace_s:g} s; "
+                  "exiting", file=sys.stderr, flush=True)
+            os._exit(3)
+
+    def raise_if_error(self) -> None:
+        if self.error is not None:
+            self._reported.set()
+            raise RuntimeError(self.error)
+
+    def stop(self) -> None:
+        self._stop.set()
+
+
 class _StreamComm(Communicator):
     """Collectives enqueued on the communicator's own HIP stream: the stream
     first waits on the caller's (compute) stream, the returned work's event
     makes a consumer stream wait in turn -- no host synchronisation, and the
     caching allocator is told (``record_stream``) that the tensors are in use
-    on the comm stream."""
+    on the comm stream.  With a :class:`CommWatchdog` (``self.watchdog``) every
+    eager collective is put under its deadline (captured ones are covered by the
+    graph replay's own tracked event: :meth:`watch_stream`)."""
 
     stream: torch.cuda.Stream
+    watchdog: Optional[CommWatchdog] = None
 
-    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor]) -> Optional[CommWork]:
+    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor], desc: str = "collective"
+                 ) -> Optional[CommWork]:
+        self.raise_if_error()
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)
         fn(int(self.stream.cuda_stream))
@@ -180,14 +278,29 @@ class _StreamComm(Communicator):
             t.record_stream(self.stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
-        work = CommWork(event=ev)
+        if self.watchdog is not None and not torch.cuda.is_current_stream_capturing():
+            self.watchdog.track(ev, desc)
+        work = CommWork(event=ev, post=self.raise_if_error)
         if async_op:
             return work
         work.wait(cur)
         return None
 
+    def watch_stream(self, stream: torch.cuda.Stream, desc: str) -> None:
+        """Put the work enqueued so far on ``stream`` (e.g. a replayed step graph holding
+        captured collectives) under the watchdog's deadline."""
+        if self.watchdog is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.watchdog.track(ev, desc)
+
+    def raise_if_error(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.raise_if_error()
+
     def poll_errors(self) -> None:
         """Raise if a bounded peer wait timed out (cheap: no device sync)."""
+        self.raise_if_error()
 
 
 class RcclComm(_StreamComm):
@@ -196,7 +309,7 @@ class RcclComm(_StreamComm):
     name = "rccl"
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
-                 stream_priority: int = -1):
+                 stream_priority: int = -1, timeout_s: Optional[float] = None):
         from ..ops import ensure_rccl
 
         C = ensure_rccl()
@@ -216,6 +329,12 @@ class RcclComm(_StreamComm):
             self._comm = C.RcclComm(uid, world_size, rank, device.index if device.index is not None else 0)
         # dedicated high-priority stream for collectives (lower number = higher priority)
         self.stream = torch.cuda.Stream(device=device, priority=stream_priority)
+        # deadline per collective (c10d watchdog semantics); at one rank nothing waits for a peer, so only
+        # an explicit timeout_s (tests) arms it there
+        t = comm_timeout_s() if timeout_s is None else float(timeout_s)
+        self.aborted = False
+        if t > 0 and (world_size > 1 or timeout_s is not None):
+            self.watchdog = CommWatchdog(f"rccl rank {rank}/{world_size}", t, self.abort)
         # one-shot xGMI all-reduce for small fp32 buckets (intra-node, self-tested)
         self._p2p = None
         if world_size > 1 and store is not None:
@@ -234,24 +353,33 @@ class RcclComm(_StreamComm):
         if self._p2p_ok(t, op):
             sc = 1.0 / self.world_size if op == "avg" else 1.0
             h, it = self._p2p._h, self._p2p.timeout_iters
-            return self._enqueue(lambda s: h.all_reduce(t, sc, it, s), async_op, [t])
-        return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t])
+            return self._enqueue(lambda s: h.all_reduce(t, sc, it, s), async_op, [t], "p2p all_reduce")
+        return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t],
+                             f"all_reduce {t.numel()} x {t.dtype}")
 
     def all_gather_into(self, out, inp, async_op=False):
         if self.world_size == 1:  # single rank: a device copy on the current stream
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
             return CommWork() if async_op else None
-        return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp])
+        return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp],
+                             f"all_gather {inp.numel()} x {inp.dtype}")
 
     def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
-        return self._enqueue(lambda s: self._comm.reduce_scatter(out, inp, op, s), async_op, [out, inp])
+        return self._enqueue(lambda s: self._comm.reduce_scatter(out, inp, op, s), async_op, [out, inp],
+                             f"reduce_scatter {out.numel()} x {out.dtype}")
 
     def broadcast(self, t, src=0, async_op=False):
-        return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t])
+        return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t],
+                             f"broadcast {t.numel()} x {t.dtype}")
 
     def all_to_all_single(self, out, inp):
-        self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp])
+        self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp], "all_to_all")
+
+    def abort(self) -> None:
+        """``ncclCommAbort``: ends this rank's pending RCCL kernels; every later collective raises."""
+        self.aborted = True
+        self._comm.abort()
 
     def _p2p_ok(self, t: torch.Tensor, op: str) -> bool:
         return self._p2p is not None and op in ("sum", "avg") and self._p2p.supports(t)
@@ -274,8 +402,9 @@ class RcclComm(_StreamComm):
             self._p2p.check()
 
     def poll_errors(self) -> None:
-        """Per-step check of the p2p path's sticky timeout flag (no device sync): a peer
-        that never delivered leaves a partial sum, so training must not go on silently."""
+        """Per-step check of the watchdog and of the p2p path's sticky timeout flag (no device
+        sync): a peer that never delivered leaves a partial sum, so training must not go on silently."""
+        self.raise_if_error()
         if self._p2p is not None:
             self._p2p.poll()
 
@@ -283,8 +412,11 @@ class RcclComm(_StreamComm):
         x = torch.zeros(1, device=self.device)
         self.all_reduce(x)
         torch.cuda.current_stream(self.device).synchronize()
+        self.raise_if_error()
 
     def destroy(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
         self._comm.destroy()
 
 

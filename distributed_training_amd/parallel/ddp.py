@@ -79,7 +79,7 @@ class DistributedDataParallel(nn.Module):
             first_b, cap_b = xgmi_bucket_caps(self.world_size, grad_bytes)
         else:
             cap_b = int(float(bucket_cap_mb) * MiB)
-            first_b = int((1.0 if first_bucket_mb is None else float(first_bucket_mb)) * MiB)
+            first_b = MiB  # torch's dist._DEFAULT_FIRST_BUCKET_BYTES (also for first_bucket_mb="auto")
         if first_bucket_mb not in (None, "auto"):
             first_b = int(float(first_bucket_mb) * MiB)
         self.bucket_bytes = (first_b, cap_b)
@@ -128,6 +128,12 @@ class DistributedDataParallel(nn.Module):
                 self.comm.broadcast(b.data, src=0)
 
     # ------------------------------------------------------------ per step
+    def reset_iteration(self) -> None:
+        """Forget a step that stopped midway (e.g. a failed graph capture): hook counts,
+        queued buckets and pending optimizer ranges."""
+        self._ov_pending = []
+        self._reset_iteration()
+
     def _reset_iteration(self) -> None:
         self.flat.direct_claimed.clear()
         self._ready = [0] * len(self.buckets)
@@ -309,6 +315,10 @@ class DistributedDataParallel(nn.Module):
             self._ov_first = True
             self.flat.stepped_in_backward = True
         self._reset_iteration()
+        if self.flat.grad.is_cuda:
+            from ..ops.lm import close_forward_generations
+
+            close_forward_generations()
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()  # a timed-out peer exchange raises here, not silently later
 

@@ -65,6 +65,18 @@ def _policy_fn(policy: WrapPolicy) -> Callable[[nn.Module], bool]:
     return lambda m: isinstance(m, classes)
 
 
+def lm_wrap_policy(model: nn.Module) -> Callable[[nn.Module], bool]:
+    """The transformer wrap policy: every block (``model.block_class``) is a unit, and so is each
+    module of ``model.fsdp_extra_units()`` (Llama: the embedding and the untied output head --
+    SURVEY.md §7.2 step 8 "embed/lm_head as their own units"), leaving the root unit with the
+    small leftovers (final norm).  Reference: the FSDP wrap of src/dist_strategy/fsdp_strategy.py:20-26
+    (there: no policy, one unit)."""
+    block = getattr(model, "block_class", None)
+    extra_fn = getattr(model, "fsdp_extra_units", None)
+    extra = {id(m) for m in (extra_fn() if extra_fn is not None else [])}
+    return lambda m: (block is not None and isinstance(m, block)) or id(m) in extra
+
+
 def _align(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
@@ -148,6 +160,10 @@ class _Unit:
         # pointing the unit at the shard's compute copy (no buffer, no copy) --
         # torch's FSDP likewise runs FULL_SHARD as NO_SHARD at world size 1
         self.alias = ws == 1 and not owner.cpu_offload
+        # an embedding's backward reads only the token ids: its unit is not re-gathered for backward
+        # (unless a weight is tied to another use, e.g. an output head, that does read it)
+        self.bwd_needs_params = (bool(getattr(module, "fsdp_backward_needs_params", True)) or is_root
+                                 or any(name in owner._aliases for _, _, name, _ in entries))
         if self.alias:
             self.full.untyped_storage().resize_(0)  # until unshard() points it at the shard
         self.free()  # storage exists only while the unit is gathered
@@ -433,7 +449,11 @@ class FullyShardedDataParallel(nn.Module):
                 # activation-checkpoint recomputation inside this unit's backward:
                 # the recomputed graph still needs the gathered parameters
                 return output
-            if self.reshard_after_forward:
+            # the last unit of the forward is the first of the backward: kept gathered rather than
+            # freed and re-gathered synchronously at the start of the backward (the output head at 8B)
+            last = (not self._record_order and self._fwd_order and u is self._fwd_order[-1]
+                    and torch.is_grad_enabled() and u.bwd_needs_params)
+            if self.reshard_after_forward and not last:
                 u.free()
             self._register_pre_backward(u, output)
             return output
@@ -449,10 +469,11 @@ class FullyShardedDataParallel(nn.Module):
             if not u._bwd_ready:
                 u._bwd_ready = True
                 u.in_backward = True
-                u.unshard(async_op=False)
+                if u.bwd_needs_params:
+                    u.unshard(async_op=False)
                 if self.prefetch:
                     prv = self._next_in_order(u, -1)
-                    if prv is not None and prv.full.grad is None:
+                    if prv is not None and prv.full.grad is None and prv.bwd_needs_params:
                         prv.unshard(async_op=True)
             return grad
 
@@ -461,6 +482,8 @@ class FullyShardedDataParallel(nn.Module):
                 t.register_hook(hook)
 
     def forward(self, *args, **kwargs):
+        if self.prefetch and not self._record_order and self._fwd_order:
+            self._fwd_order[0].unshard(async_op=True)  # the first unit (the embedding) in flight with the root's
         if self.root_unit is not None:
             self.root_unit.unshard(async_op=False)
             self.root_unit.set_views()

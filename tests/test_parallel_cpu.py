@@ -361,3 +361,91 @@ def _resume_parity(rank, ws, strategy, opt_name, tmpdir):
                                                ("ddp", "sgd")])
 def test_resume_restores_optimizer_state(strategy, opt_name, tmp_path):
     run_gloo(_resume_parity, 2, strategy, opt_name, str(tmp_path))
+
+
+@pytest.mark.parametrize("cap, first, want_first", [(25, "auto", 1.0), (25, None, 1.0), (25, 2, 2.0),
+                                                    ("auto", "auto", None)])
+def test_ddp_bucket_caps_numeric_cap_with_auto_first(cap, first, want_first):
+    """A numeric ``bucket_cap_mb`` with ``first_bucket_mb: auto`` (the shipped default of
+    conf/train/default.yaml) keeps torch's 1 MiB first bucket instead of failing on float("auto")."""
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.ddp import MiB, DistributedDataParallel
+
+    model = nn.Sequential(nn.Linear(20, 64), nn.ReLU(), nn.Linear(64, 1))
+    ddp = DistributedDataParallel(model, comm=TorchComm(), bucket_cap_mb=cap, first_bucket_mb=first)
+    first_b, cap_b = ddp.bucket_bytes
+    if want_first is not None:
+        assert first_b == int(want_first * MiB) and cap_b == int(float(cap) * MiB)
+
+
+def test_forward_generation_two_forwards_one_backward():
+    """Two forwards before one backward: a weight used once in each is NOT single-use for the
+    coming backward (its gradient must not be deferred)."""
+    from distributed_training_amd.ops import lm
+
+    w = torch.zeros(4, requires_grad=True)
+    lm.new_forward_generation()
+    lm._count_use(w)
+    assert lm._single_use(w)
+    lm.new_forward_generation()  # second forward, first backward not run yet
+    lm._count_use(w)
+    assert not lm._single_use(w)
+    lm.close_forward_generations()  # the backward finished
+    lm.new_forward_generation()
+    lm._count_use(w)
+    assert lm._single_use(w)
+    lm.new_forward_generation()  # a no-grad forward in between counts nothing and closes itself
+    lm.close_forward_generations()
+    lm.new_forward_generation()
+    lm._count_use(w)
+    assert lm._single_use(w)
+    lm.abandon_step()
+
+
+def _tiny_llama():
+    from distributed_training_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(0)
+    return Llama(LlamaConfig(n_layer=2, n_head=4, n_kv_head=2, n_embd=32, ffn_hidden=64, vocab_size=96,
+                             block_size=16))
+
+
+def _fsdp_llama_units(rank, ws, steps):
+    """lm_wrap_policy: blocks, the embedding and the output head are units of their own (the
+    root keeps only the final norm); training matches one process on the global batch."""
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    ref = _tiny_llama()
+    model = _tiny_llama()
+    fs = FullyShardedDataParallel(model, comm=TorchComm(), wrap_policy=lm_wrap_policy(model))
+    names = [[n for _, _, n, _ in u.entries] for u in fs.units]
+    assert names[0] == ["tok_embeddings.weight"] and names[-2] == ["output.weight"], names
+    assert names[-1] == ["norm.weight"] and fs.units[-1].is_root
+    assert len(fs.units) == 2 + 2 + 1
+    assert not fs.units[0].bwd_needs_params and fs.units[-2].bwd_needs_params
+    o_ref = FusedAdamW(ref.parameters(), lr=1e-2)
+    o_fs = FusedAdamW(fs.parameters(), lr=1e-2)
+    B, S = 2, 8
+    for it in range(steps):
+        g = torch.Generator().manual_seed(300 + it)
+        X = torch.randint(0, 96, (B * ws, S + 1), generator=g)
+        o_ref.zero_grad()
+        ref(X[:, :-1], X[:, 1:]).backward()
+        o_ref.step()
+        o_fs.zero_grad()
+        xb = X[rank * B:(rank + 1) * B]
+        fs(xb[:, :-1], xb[:, 1:]).backward()
+        o_fs.step()
+        # after backward no unit is left gathered (the head kept for backward was freed)
+        assert ws == 1 or not any(u.gathered for u in fs.units)
+    sd = fs.full_state_dict(rank0_only=False)
+    for k, v in ref.state_dict().items():
+        if k in sd:
+            torch.testing.assert_close(sd[k], v, rtol=2e-4, atol=2e-5, msg=k)
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_native_fsdp_llama_embedding_head_units(ws):
+    run_gloo(_fsdp_llama_units, ws, 3)
