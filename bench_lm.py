@@ -272,7 +272,9 @@ def main():
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
         out["optimizer_in_backward"] = bool(overlap_opt)
         out["step_graph"] = graphed is not None
-        out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": (f"dta/t{v}" if v else "hipblaslt")
+        out["gemm_calls"] = {"dta": _lm.GEMM_STATS["dta"], "hipblaslt": _lm.GEMM_STATS["torch"]}
+        out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": ("hipblaslt" if not v else
+                                                             f"k64/t{v - _lm.K64}" if v >= _lm.K64 else f"r2/t{v}")
                             for k, v in sorted(_lm._GEMM_CHOICE.items())}
     if rank == 0:
         print(json.dumps(out), flush=True)

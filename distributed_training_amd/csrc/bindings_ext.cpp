@@ -40,6 +40,9 @@ hipError_t dta_gemm_wgrad_group(int, const void* const*, const int64_t*, const v
                                 hipStream_t);
 hipError_t dta_gemm_bf16(const void*, int64_t, bool, const void*, int64_t, bool, void*, float*, int64_t, int, int, int,
                          float, const void*, int, const void*, int64_t, int, hipStream_t);
+int dta_gemm_k64_tile(int, int, int, int);
+hipError_t dta_gemm_k64(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, void*, int64_t, float*,
+                        int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t);
 size_t dta_linear_step_lds_bytes(int, int, int, int);
 int dta_linear_step_supported(int, int, int, int);
 
@@ -230,6 +233,73 @@ void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b
      "gemm_wgrad_group");
 }
 
+void check_out2d(const torch::Tensor& c, int64_t M, int64_t N, c10::ScalarType dt, const char* what) {
+  TORCH_CHECK(c.is_cuda() && c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 &&
+                  c.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
+              what, ": must be [M, N], unit inner stride, 16-byte aligned rows");
+  TORCH_CHECK(c.scalar_type() == dt, what, ": wrong dtype");
+}
+
+// The 64-deep-stage GEMM (csrc/gemm_k64.hip).  C[M, N] = alpha * op(A) op(B)^T (+ bias) with epilogue
+// epi: 0 none, 2 GELU (out2 given: out = pre-activation h, out2 = gelu(h) -- both returned), 16 x gelu'(res),
+// 32 + res.  a: [M, K] (a_t: [K, M]); b: [N, K] (b_t: [K, N]).  Returns (out, out2 or None).
+std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t,
+                                    c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> out2,
+                                    bool out_f32, double alpha, c10::optional<torch::Tensor> bias, int64_t epi,
+                                    c10::optional<torch::Tensor> res, int64_t tile, int64_t stream) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm64: GPU tensors");
+  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm64: bf16 operands");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm64: 2-D, unit inner stride");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && aligned16(a) && aligned16(b),
+              "gemm64: row strides multiples of 8 elements, 16-byte aligned bases");
+  const int64_t M = a_t ? a.size(1) : a.size(0), K = a_t ? a.size(0) : a.size(1);
+  const int64_t N = b_t ? b.size(1) : b.size(0), Kb = b_t ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm64: inner dimensions differ");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm64: dims too large");
+  TORCH_CHECK(dta_gemm_k64_tile((int)M, (int)N, (int)K, (int)tile) != 0,
+              "gemm64: shape not covered (M, N multiples of the tile, K a multiple of 64)");
+  TORCH_CHECK(epi == 0 || epi == 2 || epi == 16 || epi == 32, "gemm64: epi 0, 2 (gelu), 16 (x gelu'(res)), 32 (+res)");
+  TORCH_CHECK(!out_f32 || epi == 0, "gemm64: fp32 output without epilogue only");
+  const bool two = out2 && out2->defined();
+  TORCH_CHECK(!two || epi == 2, "gemm64: out2 (dual store) with the GELU epilogue only");
+  torch::Tensor c, c2;
+  if (out && out->defined()) {
+    c = *out;
+    check_out2d(c, M, N, out_f32 ? torch::kFloat32 : torch::kBFloat16, "gemm64 out");
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+  }
+  if (two) {
+    c2 = *out2;
+    check_out2d(c2, M, N, torch::kBFloat16, "gemm64 out2");
+  }
+  const void* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() &&
+                    bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm64: bias bf16 [N]");
+    bp = bias->data_ptr();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  TORCH_CHECK((epi == 16 || epi == 32) == (res && res->defined()), "gemm64: res exactly with epi 16 / 32");
+  if (res && res->defined()) {
+    TORCH_CHECK(res->is_cuda() && res->scalar_type() == torch::kBFloat16 && res->dim() == 2 && res->size(0) == M &&
+                    res->size(1) == N && res->stride(1) == 1 && res->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(res->data_ptr()) % 8 == 0,
+                "gemm64: res bf16 [M, N]");
+    rp = res->data_ptr();
+    ldr = res->stride(0);
+  }
+  ok(dta_gemm_k64(a.data_ptr(), a.stride(0), a_t, b.data_ptr(), b.stride(0), b_t, out_f32 ? nullptr : c.data_ptr(),
+                  c.stride(0), two ? c2.data_ptr() : nullptr, two ? c2.stride(0) : 0,
+                  out_f32 ? c.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (float)alpha, bp, (int)epi, rp, ldr,
+                  (int)tile, stream_of(stream)),
+     "gemm64");
+  if (two) return {c, c2};
+  return {c};
+}
+
 }  // namespace
 
 void dta_register_ext(pybind11::module_& m) {
@@ -244,6 +314,12 @@ void dta_register_ext(pybind11::module_& m) {
         py::arg("act") = 0, py::arg("residual") = py::none(), py::arg("tile") = 0, py::arg("stream") = -1);
   m.def("gemm_wgrad_group", &gemm_wgrad_group, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("db"),
         py::arg("stream") = -1);
+  m.def("gemm64", &gemm_k64, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
+        py::arg("out") = py::none(), py::arg("out2") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0,
+        py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("res") = py::none(), py::arg("tile") = 0,
+        py::arg("stream") = -1);
+  m.def("gemm64_tile", [](int M, int N, int K, int tile) { return dta_gemm_k64_tile(M, N, K, tile); },
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
   m.def("gemm_group_max", &dta_gemm_group_max);
   m.def("gemm_tile", [](int M, int N, int K, int tile) { return dta_gemm_bf16_tile(M, N, K, tile); },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);

@@ -1,0 +1,436 @@
+// bf16 GEMM for gfx950 with 64-deep k stages, a phase-interleaved half-tile
+// DMA pipeline and fused epilogues -- the transformer projections' forward
+// (y = x W^T + b [, GELU with a dual store of pre-activation and activation]
+// [, + residual]), input gradient (dx = dy W [, * gelu'(h)]) and weight
+// gradient (dW = dy^T x): SURVEY.md N07, the GEMMs of nn.Linear at
+// src/distributed_trainer.py:162,164 scaled to the GPT-2 / Llama configs.
+//
+//   C[M, N] = alpha * sum_k A(m, k) B(n, k)   (+ bias[n], epilogue)
+//
+// Operand storage (bf16, unit inner stride):
+//   A: K-major [M][K] (lda)  or  M-major [K][M] (AT)
+//   B: K-major [N][K] (ldb)  or  N-major [K][N] (BT)
+//
+// Structure (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5):
+//  * BM x BN tile per workgroup of 2 x WC waves; waves are laid out so that
+//    the A operand's two HALF-TILES (rows [0, BM/2) and [BM/2, BM)) and B's two
+//    half-tiles each feed ONE quadrant phase of every wave: wave (wr, wc) owns
+//    rows {mh * BM/2 + wr * BM/4 + [0, BM/4)} and columns
+//    {nh * BN/2 + wc * BN/(2 WC) + [0, BN/(2 WC))} for mh, nh in {0, 1}.
+//  * A K-tile (64 deep) is four phases; phase = [ds_read of the quadrant's
+//    fragments | LDS-DMA (global_load_lds_dwordx4) of ONE half-tile of a later
+//    K-tile | counted vmcnt] -> s_barrier -> lgkmcnt(0) -> 16 MFMAs -> s_barrier:
+//      P1 read A-top, B-left   DMA right (t+1)     MFMA top x left
+//      P2 read B-right         DMA bottom (t+1)    vmcnt(2LA+2LB)  MFMA top x right
+//      P3 read A-bottom        DMA top (t+2)       MFMA bottom x right
+//      P4 (registers)          DMA left (t+2)      vmcnt(2LA+LB)   MFMA bottom x left
+//    Two LDS buffers (K-tile t in buffer t & 1).  Every half-tile is restaged
+//    two or more phases after its last read (safe with the wave-group stagger
+//    below: a phase's reads are retired by its lgkmcnt(0) before its second
+//    barrier); every wait retires the half-tiles read one phase later or
+//    more, and leaves three half-tiles in flight -- vmcnt is never 0 in the
+//    loop, barriers are raw s_barrier (the LDS-DMA spans them).
+//  * Waves 4-7 run one barrier behind waves 0-3 (stagger, MI355X_MICROARCH.md
+//    "Two waves per SIMD" item 9): while one wave of a SIMD multiplies, its
+//    partner loads.  MFMA clusters are pinned between the barriers with
+//    s_setprio / sched_barrier (T5).
+//  * LDS images are lane-linear for the DMA; the XOR swizzle goes on the
+//    per-lane SOURCE address and is undone on the read (rule 21):
+//      K-major (128-B rows of 64 k):  chunk c of row r at c ^ (r & 7)
+//        -> ds_read_b128 fragment reads conflict-free;
+//      M/N-major (64 k-rows of 2 x BM/2 bytes): chunk ch of k-row k at
+//        ch ^ ((k&3)<<2 | (k>>2)&3) (256-B rows) or ch ^ ((k>>1&1)<<1 | (k>>3&1)<<2)
+//        (128-B rows) -> ds_read_b64_tr_b16 reads conflict-free (verified with
+//        scripts/lds_banks.py's bank model).
+//  * v_mfma_f32_16x16x32_bf16 (on random data it holds a higher clock than
+//    32x32x16 at equal cycles per FLOP: MI355X_MICROARCH.md "DVFS give-back"
+//    item 7), issued as mfma(B, A) so each lane's four accumulators are four
+//    consecutive output COLUMNS: the epilogue stores bf16x4 pieces.
+//  * Out-of-range K-tiles of the pipeline's tail are DMA'd from the last
+//    K-tile (never read): the vmcnt counts stay static; drained before exit.
+//    (A persistent variant -- each workgroup walking several tiles with the
+//    DMA running across tile boundaries -- measured slower at every GPT-2 and
+//    Llama shape: 51 vs 46 us on the GPT-2 qkv forward, 136 vs 92 us on its
+//    weight gradient; the epilogue inside the K loop costs registers and
+//    scheduling freedom.)
+//  * Tile order: XCD-aware bijective remap, then groups of 8 tile rows walked
+//    column by column (L2 panel reuse on each XCD).
+#include "common.h"
+
+namespace dta {
+namespace k64 {
+
+constexpr int BK = 64;
+constexpr int kGroupM = 8;
+
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 2, EPI_DGELU = 16, EPI_RES = 32 };
+
+struct Args {
+  const bf16* a;
+  const bf16* b;
+  bf16* c;          // bf16 output (EPI_GELU with c2: the pre-activation)
+  bf16* c2;         // EPI_GELU: the activation gelu(c) (nullptr: c holds the activation)
+  float* c32;       // fp32 output instead of c (EPI_NONE only)
+  const bf16* bias; // [N] or nullptr
+  const bf16* res;  // EPI_DGELU: the GELU input; EPI_RES: added after rounding
+  int64_t lda, ldb, ldc, ldc2, ldr;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  float alpha;
+  int epi;
+};
+
+// GELU (tanh form) as x * sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of tanhf
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __frcp_rn(1.f + __expf(-2.f * u));
+}
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float s = __frcp_rn(1.f + __expf(-2.f * u));  // sigmoid(2u) = (1 + tanh u) / 2
+  // d/dx [x s] = s + x s (1 - s) 2 du/dx
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
+
+__device__ __forceinline__ bf16x4 tr4(const char* lds, int byte_off) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lds + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// chunk swizzle of an M/N-major image with RB-byte k-rows
+template <int RB>
+__device__ __forceinline__ int mswz(int k) {
+  if constexpr (RB == 256) return ((k & 3) << 2) | ((k >> 2) & 3);
+  else return (((k >> 1) & 1) << 1) | (((k >> 3) & 1) << 2);
+}
+
+// fragment (16 rows r0.., k 32 kk .. +31) of a K-major half image: lane l -> row r0 + (l & 15), k 8 (l >> 4) ..
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int r0, int kk, int lane) {
+  const int r = r0 + (lane & 15), c = 4 * kk + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(img + r * 128 + 16 * (c ^ (r & 7)));
+}
+
+// the same fragment (16 indices i0.., k 32 kk ..) of an M/N-major half image with RB-byte k-rows
+template <int RB>
+__device__ __forceinline__ bf16x8 frag_mn(const char* img, int i0, int kk, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int k = 32 * kk + 8 * g + q;
+  const int col = i0 + 4 * p, ch = col >> 3, w = (col & 7) * 2;
+  const bf16x4 lo = tr4(img, k * RB + 16 * (ch ^ mswz<RB>(k)) + w);
+  const bf16x4 hi = tr4(img, (k + 4) * RB + 16 * (ch ^ mswz<RB>(k + 4)) + w);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BM, int BN, int WC, bool AT, bool BT>
+struct Cfg {
+  static constexpr int NW = 2 * WC, NTHR = 64 * NW;
+  static constexpr int HA = BM / 2, HB = BN / 2;                  // half-tile rows / columns
+  static constexpr int A_HALF = HA * BK * 2, B_HALF = HB * BK * 2;  // bytes
+  static constexpr int LA = A_HALF / (NTHR * 16), LB = B_HALF / (NTHR * 16);  // DMA per thread per half
+  static constexpr int BUF = 2 * A_HALF + 2 * B_HALF;
+  static constexpr int MTH = HA / 32, NTH = HB / (16 * WC);       // fragments per wave per half
+  static constexpr int RBA = 2 * HA, RBB = 2 * HB;                 // M/N-major image row bytes
+  static_assert(LA >= 1 && LB >= 1 && MTH >= 1 && NTH >= 1, "tile too small for the workgroup");
+  static_assert(!AT || RBA == 256 || RBA == 128, "M-major A: BM 256 or 128");
+  static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
+};
+
+template <int BM, int BN, int WC, bool AT, bool BT>
+__global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
+  using C = Cfg<BM, BN, WC, AT, BT>;
+  constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
+  constexpr bool STAG = WC == 4;  // two waves per SIMD: stagger the halves
+  __shared__ __attribute__((aligned(1024))) char lds[2 * C::BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+
+  // ---- tile ----
+  const int t = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
+  const int per_group = kGroupM * g.tiles_n;
+  const int grp = t / per_group, in_g = t - grp * per_group;
+  const int gm0 = grp * kGroupM, gh = min(kGroupM, g.tiles_m - gm0);
+  const int m0 = (gm0 + in_g % gh) * BM, n0 = (in_g / gh) * BN;
+  const int nk = g.K / BK;
+
+  // ---- per-lane DMA sources of K-tile 0 (half h: rows / columns [h * H, (h+1) * H)) ----
+  // half index: 0 top, 1 bottom, 2 left, 3 right; LDS: buffer b at b * BUF, [top|bottom|left|right]
+  const bf16* srcA[2][LA];
+  const bf16* srcB[2][LB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      const int i = j * NW + wave;  // 1 KiB piece of the half image
+      if constexpr (!AT) {
+        const int r = 8 * i + (lane >> 3), c = (lane & 7) ^ (r & 7);
+        srcA[h][j] = g.a + (int64_t)(m0 + h * HA + r) * g.lda + 8 * c;
+      } else {
+        constexpr int CPR = C::RBA / 16, RPI = 64 / CPR;
+        const int k = RPI * i + lane / CPR, ch = (lane % CPR) ^ mswz<C::RBA>(k);
+        srcA[h][j] = g.a + (int64_t)k * g.lda + m0 + h * HA + 8 * ch;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      const int i = j * NW + wave;
+      if constexpr (!BT) {
+        const int r = 8 * i + (lane >> 3), c = (lane & 7) ^ (r & 7);
+        srcB[h][j] = g.b + (int64_t)(n0 + h * HB + r) * g.ldb + 8 * c;
+      } else {
+        constexpr int CPR = C::RBB / 16, RPI = 64 / CPR;
+        const int k = RPI * i + lane / CPR, ch = (lane % CPR) ^ mswz<C::RBB>(k);
+        srcB[h][j] = g.b + (int64_t)k * g.ldb + n0 + h * HB + 8 * ch;
+      }
+    }
+  }
+  const int64_t stepA = AT ? (int64_t)BK * g.lda : BK;
+  const int64_t stepB = BT ? (int64_t)BK * g.ldb : BK;
+  auto dma_a = [&](int h, int kt) {  // A half h of K-tile kt (past the end: the last K-tile, never read)
+    const int ks = min(kt, nk - 1);
+    char* dst = lds + (kt & 1) * C::BUF + h * C::A_HALF;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
+  };
+  auto dma_b = [&](int h, int kt) {
+    const int ks = min(kt, nk - 1);
+    char* dst = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) glds16(srcB[h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
+  };
+
+  // ---- fragment reads: the wave's quadrant of a half ----
+  auto read_a = [&](bf16x8 (&af)[MTH][2], int kt, int h) {
+    const char* img = lds + (kt & 1) * C::BUF + h * C::A_HALF;
+#pragma unroll
+    for (int jj = 0; jj < MTH; ++jj)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int r0 = wr * (HA / 2) + 16 * jj;
+        if constexpr (!AT) af[jj][kk] = frag_k(img, r0, kk, lane);
+        else af[jj][kk] = frag_mn<C::RBA>(img, r0, kk, lane);
+      }
+  };
+  auto read_b = [&](bf16x8 (&bf)[NTH][2], int kt, int h) {
+    const char* img = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+#pragma unroll
+    for (int ii = 0; ii < NTH; ++ii)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c0 = wc * (HB / WC) + 16 * ii;
+        if constexpr (!BT) bf[ii][kk] = frag_k(img, c0, kk, lane);
+        else bf[ii][kk] = frag_mn<C::RBB>(img, c0, kk, lane);
+      }
+  };
+
+  f32x4 acc[2 * NTH][2 * MTH];
+#pragma unroll
+  for (int i = 0; i < 2 * NTH; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * MTH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8 (&af)[MTH][2], const bf16x8 (&bf)[NTH][2], int mh, int nh) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ii = 0; ii < NTH; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < MTH; ++jj)
+          acc[nh * NTH + ii][mh * MTH + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ii][kk], af[jj][kk], acc[nh * NTH + ii][mh * MTH + jj], 0,
+                                                      0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- prologue: K-tile 0 whole + top / left of K-tile 1; retire top, left, right of 0 ----
+  dma_a(0, 0);
+  dma_b(0, 0);
+  dma_b(1, 0);
+  dma_a(1, 0);
+  dma_a(0, 1);
+  dma_b(0, 1);
+  vm_wait<2 * LA + LB>();
+  bar();
+  if constexpr (STAG) {
+    if (wr == 1) bar();
+  }
+
+  bf16x8 af[MTH][2], b0[NTH][2], b1[NTH][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    // P1
+    read_a(af, kt, 0);
+    read_b(b0, kt, 0);
+    dma_b(1, kt + 1);
+    bar();
+    lgkm0();
+    mma(af, b0, 0, 0);
+    bar();
+    // P2
+    read_b(b1, kt, 1);
+    dma_a(1, kt + 1);
+    vm_wait<2 * LA + 2 * LB>();
+    bar();
+    lgkm0();
+    mma(af, b1, 0, 1);
+    bar();
+    // P3
+    read_a(af, kt, 1);
+    dma_a(0, kt + 2);
+    bar();
+    lgkm0();
+    mma(af, b1, 1, 1);
+    bar();
+    // P4
+    dma_b(0, kt + 2);
+    vm_wait<2 * LA + LB>();
+    bar();
+    mma(af, b0, 1, 0);
+    bar();
+  }
+  vm_wait<0>();  // the tail's dummy DMAs land before the workgroup's LDS is released
+  if constexpr (STAG) {
+    if (wr == 0) bar();  // equal barrier counts for both halves
+  }
+
+  // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment ----
+#pragma unroll
+  for (int i = 0; i < 2 * NTH; ++i) {
+    const int nh = i / NTH, ii = i % NTH;
+    const int n = n0 + nh * HB + wc * (HB / WC) + 16 * ii + 4 * (lane >> 4);
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias) {
+      const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * MTH; ++j) {
+      const int mh = j / MTH, jj = j % MTH;
+      const int m = m0 + mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[i][j][r], g.alpha, bv[r]);
+      if (g.c32) {
+        *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
+      if (g.epi == EPI_GELU) {
+        if (g.c2) {  // dual store: pre-activation h (for the backward) and gelu(h) (the next GEMM's input)
+          const bf16x4 h4 = pk4_bf16(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = h4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_fast(bf2f(h4[r]));  // gelu of the stored (rounded) h
+          *reinterpret_cast<bf16x4*>(g.c2 + (int64_t)m * g.ldc2 + n) = pk4_bf16(v[0], v[1], v[2], v[3]);
+          continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
+      } else if (g.epi == EPI_DGELU) {  // dgrad through the GELU: one rounding (of the product)
+        const bf16x4 h4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_fast(bf2f(h4[r]));
+      } else if (g.epi == EPI_RES) {  // residual stream: round(round(linear) + res), as two bf16 ops give
+        const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);
+      }
+      *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = pk4_bf16(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+template <int BM, int BN, int WC, bool AT, bool BT>
+static hipError_t launch(const Args& g, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st, g);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int WC>
+static hipError_t launch_t(const Args& g, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch<BM, BN, WC, false, false>(g, st);
+  if (!at && bt) return launch<BM, BN, WC, false, true>(g, st);
+  if (at && bt) return launch<BM, BN, WC, true, true>(g, st);
+  return launch<BM, BN, WC, true, false>(g, st);
+}
+
+// tile ids: 1 = 256x256 (8 waves), 2 = 256x128 (8 waves), 3 = 128x128 (4 waves), 4 = 128x256 (8 waves)
+constexpr int kTiles = 4;
+__host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
+__host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
+
+}  // namespace k64
+}  // namespace dta
+
+using namespace dta;
+
+// 0 if the tile does not cover the problem, else the tile id.  tile = 0: the fewest rounds of
+// resident workgroups weighted by the tile's relative efficiency (bigger tiles reuse more per byte).
+int dta_gemm_k64_tile(int M, int N, int K, int tile) {
+  if (K % k64::BK || K < k64::BK) return 0;
+  auto fits = [&](int t) { return M % k64::tile_bm(t) == 0 && N % k64::tile_bn(t) == 0; };
+  if (tile) return (tile >= 1 && tile <= k64::kTiles && fits(tile)) ? tile : 0;
+  static const double eff[5] = {0, 1.0, 0.88, 0.74, 0.88};
+  static const int per_cu[5] = {0, 1, 1, 2, 1};
+  int best = 0;
+  double best_t = 1e30;
+  for (int t = 1; t <= k64::kTiles; ++t) {
+    if (!fits(t)) continue;
+    const int tiles = (M / k64::tile_bm(t)) * (N / k64::tile_bn(t));
+    const int slots = 256 * per_cu[t];
+    const int rounds = (tiles + slots - 1) / slots;
+    const double tt = rounds * (double)k64::tile_bm(t) * k64::tile_bn(t) * per_cu[t] / eff[t];
+    if (tt < best_t * 0.999) {
+      best_t = tt;
+      best = t;
+    }
+  }
+  return best;
+}
+
+// epi: 0 none, 2 GELU (c2 != nullptr: c = pre-activation, c2 = gelu), 16 x gelu'(res), 32 + res
+hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
+                        int64_t ldc, void* c2, int64_t ldc2, float* c32, int M, int N, int K, float alpha,
+                        const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st) {
+  tile = dta_gemm_k64_tile(M, N, K, tile);
+  if (!tile || (!c && !c32)) return hipErrorInvalidValue;
+  if (c32 && epi != k64::EPI_NONE) return hipErrorInvalidValue;
+  k64::Args g{};
+  g.a = static_cast<const bf16*>(a);
+  g.b = static_cast<const bf16*>(b);
+  g.c = static_cast<bf16*>(c);
+  g.c2 = static_cast<bf16*>(c2);
+  g.c32 = c32;
+  g.bias = static_cast<const bf16*>(bias);
+  g.res = static_cast<const bf16*>(res);
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.ldc2 = ldc2;
+  g.ldr = ldr;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.alpha = alpha;
+  g.epi = epi;
+  g.tiles_m = M / k64::tile_bm(tile);
+  g.tiles_n = N / k64::tile_bn(tile);
+  switch (tile) {
+    case 1: return k64::launch_t<256, 256, 4>(g, a_t, b_t, st);
+    case 2: return k64::launch_t<256, 128, 4>(g, a_t, b_t, st);
+    case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, st);
+    default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, st);
+  }
+}

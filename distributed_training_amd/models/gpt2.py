@@ -82,8 +82,10 @@ class MLP(nn.Module):
         self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
-        # c_proj(gelu(c_fc(x))) with the GELU backward folded into c_proj's input-gradient GEMM
-        return lm.gelu_linear(self.c_fc(x), self.c_proj.weight, self.c_proj.bias)
+        # c_proj(gelu(c_fc(x))): the GELU in c_fc's GEMM epilogue (pre-activation and activation stored
+        # in one pass), its backward folded into c_proj's input-gradient GEMM
+        h, a = lm.linear_gelu(x, self.c_fc.weight, self.c_fc.bias)
+        return lm.gelu_linear(h, self.c_proj.weight, self.c_proj.bias, a=a)
 
 
 class Block(nn.Module):

@@ -284,50 +284,77 @@ def _save_cache() -> None:
         pass
 
 
-def _pick(kind: str, M: int, N: int, K: int, run_dta: Callable[[int], object], run_torch: Callable[[], object]) -> int:
-    """Implementation for one GEMM shape: the dta tile that measured fastest, or 0
-    (hipBLASLt) when the library is faster / the shape is not covered."""
+# implementation ids in _GEMM_CHOICE: 0 = hipBLASLt (torch), 1..3 = csrc/gemm_bf16.hip tile (round-2
+# kernel, 32-deep stages; kept for K % 64 != 0), 10 + t = csrc/gemm_k64.hip tile t (64-deep stages)
+K64 = 10
+# the hand-written kernel keeps a shape unless the library is clearly faster: ties go to the kernel
+# whose epilogue the caller can fuse further (and whose behaviour this repository controls)
+_PREFER_DTA = 1.02
+
+
+def _k64_on() -> bool:
+    """``DTA_GEMM_K64=0``: leave csrc/gemm_k64.hip out of the candidates (A/B against round 2)."""
+    return os.environ.get("DTA_GEMM_K64", "1") != "0"
+
+
+def gemm_candidates(M: int, N: int, K: int) -> list:
+    """Hand-written GEMM implementations that cover an M x N x K problem (ids as in _GEMM_CHOICE)."""
+    C = native()
+    k64 = [K64 + t for t in (1, 2, 3, 4) if _k64_on() and C.gemm64_tile(M, N, K, t)]
+    if k64:
+        return k64
+    return [t for t in (1, 2, 3) if C.gemm_tile(M, N, K, t)]
+
+
+def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]]) -> int:
+    """Implementation for one (possibly fused) GEMM shape: ``cands`` maps implementation ids to
+    callables computing the SAME fused result (0 = hipBLASLt + separate epilogue kernels); the
+    fastest by interleaved timing (median of rounds), hand-written on near-ties (_PREFER_DTA).
+    Memoised per (kind, M, N, K) and process; ``DTA_GEMM_CACHE`` persists it."""
     if not _CACHE_LOADED[0]:
         _load_cache()
     key = (kind, M, N, K)
     c = _GEMM_CHOICE.get(key)
-    if c is not None:
+    if c is not None and (c in cands or c == 0):
         return c
     mode = os.environ.get("DTA_GEMM", "auto")
-    C = native()
-    tiles = [t for t in (1, 2, 3) if C.gemm_tile(M, N, K, t)]
-    if mode == "torch" or not tiles:
+    dta = [k for k in cands if k != 0]
+    if mode == "torch" or not dta:
         c = 0
     elif mode == "dta" or torch.cuda.is_current_stream_capturing():
-        c = C.gemm_tile(M, N, K, 0)
+        c = max(dta)  # (k64 ids sort after the round-2 tiles; the k64 auto tile is listed first below)
+        auto = native().gemm64_tile(M, N, K, 0)
+        if K64 + auto in dta:
+            c = K64 + auto
     else:
-        cands = {0: run_torch}
-        for t in tiles:
-            cands[t] = (lambda t=t: run_dta(t))
         times = _time_us(cands)
-        # the library keeps the shape unless the dta kernel is clearly faster (>2 %)
-        c = min(times, key=times.get)
-        if c and times[c] > 0.98 * times[0]:
-            c = 0
+        best = min(dta, key=times.get)
+        c = best if 0 not in times or times[best] <= _PREFER_DTA * times[0] else 0
     _GEMM_CHOICE[key] = c
     if mode == "auto":
         _save_cache()
     return c
 
 
+def _run_gemm(impl: int, a, b, a_t: bool, b_t: bool, out=None, alpha: float = 1.0, bias=None):
+    C = native()
+    if impl >= K64:
+        return C.gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
+    return C.gemm(a, b, a_t, b_t, out, False, alpha, bias, 0, None, impl)
+
+
+def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias=None, out=None) -> bool:
+    return (a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous())
+            and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)))
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False, bias: Optional[torch.Tensor] = None,
          alpha: float = 1.0, kind: str = "", out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 ``alpha * op(a) op(b)^T (+ bias)`` on GPU, a: [M, K] (a_t: [K, M]), b: [N, K] (b_t: [K, N]);
-    dta kernel or hipBLASLt per shape (see module doc)."""
+    hand-written kernel or hipBLASLt per shape (see module doc)."""
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
-    ok = (a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
-          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous())
-          and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)))
-    C = native()
-
-    def run_dta(tile):
-        return C.gemm(a, b, a_t, b_t, out, False, alpha, bias, 0, None, tile)
 
     def run_torch():
         A = a.t() if a_t else a
@@ -339,10 +366,46 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
             y.mul_(alpha)
         return y if bias is None else y.add_(bias)
 
-    tile = _pick(kind + ("b" if bias is not None else ""), M, N, K, run_dta, run_torch) if ok else 0
-    if tile:
+    impl = 0
+    if _gemm_ok(a, b, bias, out):
+        cands: Dict[int, Callable[[], object]] = {0: run_torch}
+        for t in gemm_candidates(M, N, K):
+            cands[t] = (lambda t=t: _run_gemm(t, a, b, a_t, b_t, out, alpha, bias))
+        impl = _pick(kind + ("b" if bias is not None else ""), M, N, K, cands)
+    if impl:
         GEMM_STATS["dta"] += 1
-        return run_dta(tile)
+        return _run_gemm(impl, a, b, a_t, b_t, out, alpha, bias)
+    GEMM_STATS["torch"] += 1
+    return run_torch()
+
+
+def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``h = x W^T + b`` and ``a = gelu_tanh(h)`` (of the rounded h) -- the GPT-2 MLP up-projection
+    with its activation: the 64-deep GEMM with the GELU in its epilogue storing BOTH (one pass, no
+    re-read of h), or hipBLASLt + the GELU kernel, whichever measured faster for the shape (the
+    FUSED costs are compared)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    C = native()
+
+    def run_torch():
+        h = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        return h, C.gelu_fwd(h, -1)
+
+    def run_k64(t):
+        h = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+        return tuple(C.gemm64(x2, w, False, False, h, torch.empty_like(h), False, 1.0, b, 2, None, t))
+
+    impl = 0
+    if _gemm_ok(x2, w, b) and N % 8 == 0:
+        cands: Dict[int, Callable[[], object]] = {0: run_torch}
+        for t in (1, 2, 3, 4):
+            if _k64_on() and C.gemm64_tile(M, N, K, t):
+                cands[K64 + t] = (lambda t=t: run_k64(t))
+        impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands)
+    if impl:
+        GEMM_STATS["dta"] += 1
+        return run_k64(impl - K64)
     GEMM_STATS["torch"] += 1
     return run_torch()
 
@@ -635,7 +698,7 @@ class _Linear(Function):
 
 
 def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.Tensor:
-    """dh = (dy W) * gelu_tanh'(h): the input gradient of ``gelu(h) W^T + b`` -- on the general
+    """dh = (dy W) * gelu_tanh'(h): the input gradient of ``gelu(h) W^T + b`` -- on a hand-written
     GEMM with the GELU derivative in its epilogue (one pass, no dA round trip through HBM), or
     hipBLASLt followed by the GELU-backward kernel, whichever measured faster for the shape."""
     M, K = dy2.shape
@@ -644,16 +707,23 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and h2.is_contiguous()
           and h2.data_ptr() % 16 == 0 and N % 8 == 0)
 
-    def run_dta(tile):
-        return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, tile)
+    def run(impl):
+        if impl >= K64:
+            return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
+        return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, impl)
 
     def run_torch():
         return C.gelu_bwd(torch.mm(dy2, w), h2, -1)
 
-    tile = _pick("dgelu", M, N, K, run_dta, run_torch) if ok else 0
-    if tile:
+    impl = 0
+    if ok:
+        cands: Dict[int, Callable[[], object]] = {0: run_torch}
+        for t in gemm_candidates(M, N, K):
+            cands[t] = (lambda t=t: run(t))
+        impl = _pick("dgelu", M, N, K, cands)
+    if impl:
         GEMM_STATS["dta"] += 1
-        return run_dta(tile)
+        return run(impl)
     GEMM_STATS["torch"] += 1
     return run_torch()
 
@@ -664,9 +734,10 @@ class _GeluLinear(Function):
     :func:`_dgelu_dgrad` (the GELU backward folded into the input-gradient GEMM)."""
 
     @staticmethod
-    def forward(ctx, h, w, b):
+    def forward(ctx, h, w, b, a=None):
         hc = h.contiguous()
-        a = native().gelu_fwd(hc, -1)
+        if a is None:
+            a = native().gelu_fwd(hc, -1)
         ctx.save_for_backward(hc, a, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)
@@ -691,14 +762,50 @@ class _GeluLinear(Function):
             dw, db = r if want_b else (r, None)
         elif want_b:
             db = native().bias_grad(dy2, False, -1)
-        return dh, dw, db
+        return dh, dw, db, None
 
 
-def gelu_linear(h, w, b=None):
-    """``linear(gelu(h), w, b)`` with the GELU backward fused into the input-gradient GEMM on GPU."""
+class _LinearGelu(Function):
+    """(h, a) = (x W^T + b, gelu_tanh(h)): the GPT-2 MLP up-projection with its activation
+    computed in the GEMM's epilogue (:func:`gemm_gelu_dual`).  ``a`` is the input of the
+    down-projection (:class:`_GeluLinear` with ``a`` given), which differentiates through
+    the GELU itself and returns the gradient of ``h`` -- so ``a`` carries no gradient here
+    and backward is exactly :class:`_Linear`'s."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        ctx.params = (w, b)
+        if ctx.needs_input_grad[1]:
+            _count_use(w)
+        x2 = x.reshape(-1, x.shape[-1])
+        h, a = gemm_gelu_dual(x2, w, b)
+        shp = (*x.shape[:-1], w.shape[0])
+        h, a = h.view(shp), a.view(shp)
+        ctx.mark_non_differentiable(a)
+        return h, a
+
+    @staticmethod
+    def backward(ctx, dh, da):
+        return _Linear.backward(ctx, dh)
+
+
+def linear_gelu(x, w, b=None):
+    """``(h, gelu(h))`` for ``h = linear(x, w, b)``; feed both to :func:`gelu_linear` (``a=``)."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+            and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
+        return _LinearGelu.apply(x, w, b)
+    h = linear(x, w, b)
+    return h, gelu(h).detach()
+
+
+def gelu_linear(h, w, b=None, a=None):
+    """``linear(gelu(h), w, b)`` with the GELU backward fused into the input-gradient GEMM on GPU;
+    ``a``: gelu(h) already computed (by :func:`linear_gelu`'s epilogue)."""
     if h.is_cuda and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and h.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
-        return _GeluLinear.apply(h, w, b)
+        return _GeluLinear.apply(h, w, b, a)
     return linear(gelu(h), w, b)
 
 

@@ -1,0 +1,130 @@
+"""The 64-deep-stage GEMM (csrc/gemm_k64.hip) against an fp32 PyTorch reference of
+the same op on the same bf16 inputs: every operand layout (forward NT, input-gradient
+NN, weight-gradient TN, and TT) x every tile, pipelines shorter than the DMA
+look-ahead (K = 64, 128), exact small-integer checks that catch any fragment /
+swizzle / transposition mistake, and the fused epilogues (bias, alpha, GELU with the
+dual store of pre-activation and activation, x gelu'(h), + residual, fp32 out)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+LAYOUTS = [(False, False), (False, True), (True, True), (True, False)]
+TILES = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 256)}
+
+
+def _ops(M, N, K, a_t, b_t, gen, scale=1.0):
+    a = (torch.randn(K, M, generator=gen) if a_t else torch.randn(M, K, generator=gen)) * scale
+    b = (torch.randn(K, N, generator=gen) if b_t else torch.randn(N, K, generator=gen)) * scale
+    a, b = a.bfloat16().cuda(), b.bfloat16().cuda()
+    A = a.float().t() if a_t else a.float()
+    B = b.float() if b_t else b.float().t()
+    return a, b, A @ B
+
+
+def _close(got, want, K):
+    tol = 4e-3 * want.abs().max().item() + 1e-3 * K ** 0.5
+    err = (got.float() - want).abs().max().item()
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_gemm64_exact_small_integers(a_t, b_t, tile):
+    """Small integers: every product and partial sum is exact in fp32 -- any fragment-order,
+    swizzle or pipeline-staging mistake shows as a mismatch (asymmetric operands)."""
+    from distributed_training_amd.ops import native
+
+    bm, bn = TILES[tile]
+    gen = torch.Generator().manual_seed(tile * 10 + 2 * a_t + b_t)
+    for M, N, K in ((2 * bm, 3 * bn, 64), (bm, bn, 128), (3 * bm, 2 * bn, 640)):
+        a = torch.randint(-3, 4, (K, M) if a_t else (M, K), generator=gen).float()
+        b = torch.randint(-3, 4, (K, N) if b_t else (N, K), generator=gen).float()
+        want = (a.t() if a_t else a) @ (b if b_t else b.t())
+        got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out_f32=True, tile=tile)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), want), (a_t, b_t, tile, M, N, K)
+
+
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+@pytest.mark.parametrize("tile,M,N,K", [(1, 512, 512, 256), (2, 512, 384, 192), (3, 384, 256, 1088),
+                                        (4, 256, 768, 768), (0, 1024, 768, 768)])
+def test_gemm64_random(a_t, b_t, tile, M, N, K):
+    from distributed_training_amd.ops import native
+
+    if tile and (M % TILES[tile][0] or N % TILES[tile][1]):
+        pytest.skip("shape not a multiple of the tile")
+    gen = torch.Generator().manual_seed(M + N + K + 7 * a_t + 3 * b_t)
+    a, b, want = _ops(M, N, K, a_t, b_t, gen)
+    got, = native().gemm64(a, b, a_t, b_t, tile=tile)
+    torch.cuda.synchronize()
+    _close(got, want, K)
+
+
+@pytest.mark.parametrize("tile", [1, 3])
+def test_gemm64_epilogues(tile):
+    from distributed_training_amd.ops import native
+
+    gen = torch.Generator().manual_seed(5 + tile)
+    M, N, K = 512, 768, 384
+    xs = torch.randn(M, K + 64, generator=gen).bfloat16().cuda()[:, 16:16 + K]  # row stride K + 64
+    w = (torch.randn(N, K, generator=gen) * 0.1).bfloat16().cuda()
+    bias = torch.randn(N, generator=gen).bfloat16().cuda()
+    res = torch.randn(M, N, generator=gen).bfloat16().cuda()
+    ref = xs.float() @ w.float().t()
+    # GELU in the epilogue (single output)
+    got, = native().gemm64(xs, w, bias=bias, epi=2, tile=tile)
+    _close(got, F.gelu(ref + bias.float(), approximate="tanh"), K)
+    # GELU dual store: h (pre-activation, rounded once) and gelu(h) of the ROUNDED h -- what the
+    # unfused gemm + gelu_fwd pair gives, so backward (dgelu of the stored h) is consistent
+    h, act = native().gemm64(xs, w, bias=bias, epi=2, out2=torch.empty(M, N, dtype=torch.bfloat16, device="cuda"),
+                             tile=tile)
+    want_h = ref + bias.float()
+    _close(h, want_h, K)
+    torch.testing.assert_close(act.float(), F.gelu(h.float(), approximate="tanh"), rtol=1.6e-2, atol=1e-2)
+    # alpha + residual: round(round(alpha x W^T) + res)
+    got, = native().gemm64(xs, w, alpha=0.5, epi=32, res=res, tile=tile)
+    _close(got, (0.5 * ref).bfloat16().float() + res.float(), K)
+    # x gelu'(res): the input gradient through a GELU (dgrad NN layout: dy [M, K] @ W [K, N])
+    wn = (torch.randn(K, N, generator=gen) * 0.1).bfloat16().cuda()
+    dy = torch.randn(M, K, generator=gen).bfloat16().cuda()
+    got, = native().gemm64(dy, wn, False, True, epi=16, res=res, tile=tile)
+    xr = res.float().requires_grad_(True)
+    gg, = torch.autograd.grad(F.gelu(xr, approximate="tanh").sum(), xr)
+    _close(got, (dy.float() @ wn.float()) * gg, K)
+    # fp32 output into a strided destination
+    out = torch.zeros(M, N + 32, device="cuda")
+    native().gemm64(xs, w, out=out[:, :N], out_f32=True, tile=tile)
+    torch.cuda.synchronize()
+    _close(out[:, :N], ref, K)
+    assert out[:, N:].abs().max().item() == 0.0
+
+
+def test_gemm64_rejects_bad_shapes():
+    from distributed_training_amd.ops import native
+
+    a = torch.zeros(256, 96, dtype=torch.bfloat16, device="cuda")  # K not a multiple of 64
+    b = torch.zeros(256, 96, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(RuntimeError, match="not covered"):
+        native().gemm64(a, b)
+    assert native().gemm64_tile(8192, 768, 768) != 0 and native().gemm64_tile(100, 768, 768) == 0
+
+
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_gemm64_persistent_multi_tile_exact(a_t, b_t, tile):
+    """More tiles than resident workgroups (576 > 256 / 512 slots): each workgroup walks several
+    tiles with the DMA pipeline running across tile boundaries and epilogues in between --
+    exact on small integers, every tile checked (also the K = 64 single-step case)."""
+    from distributed_training_amd.ops import native
+
+    bm, bn = TILES[tile]
+    gen = torch.Generator().manual_seed(100 + tile * 10 + 2 * a_t + b_t)
+    for M, N, K in ((32 * bm, 18 * bn, 192), (32 * bm, 18 * bn, 64)):
+        a = torch.randint(-3, 4, (K, M) if a_t else (M, K), generator=gen).float()
+        b = torch.randint(-3, 4, (K, N) if b_t else (N, K), generator=gen).float()
+        want = (a.t() if a_t else a).cuda() @ (b if b_t else b.t()).cuda()
+        got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out_f32=True, tile=tile)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), (a_t, b_t, tile, M, N, K, (got - want).abs().max().item())

@@ -438,6 +438,39 @@ def test_gelu_linear_fused_backward(mode, monkeypatch):
         assert lm._GEMM_CHOICE.get(("dgelu", 512, 256, 384), 0) != 0
 
 
+@pytest.mark.parametrize("mode", ["dta", "torch"])
+def test_mlp_gelu_in_up_projection_epilogue(mode, monkeypatch):
+    """GPT-2 MLP with the GELU in c_fc's epilogue (dual store of h and gelu(h), DTA_GEMM=dta: the
+    64-deep GEMM; torch: hipBLASLt + the GELU kernel) and its backward folded into c_proj's
+    input-gradient GEMM, vs fp32 PyTorch: output and every parameter / input gradient."""
+    import torch.nn.functional as F
+
+    monkeypatch.setenv("DTA_GEMM", mode)
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    torch.manual_seed(13)
+    x = torch.randn(4, 128, 256, device=DEV).bfloat16().requires_grad_()
+    w1 = (torch.randn(1024, 256, device=DEV) * 0.05).bfloat16().requires_grad_()
+    b1 = (torch.randn(1024, device=DEV) * 0.1).bfloat16().requires_grad_()
+    w2 = (torch.randn(256, 1024, device=DEV) * 0.05).bfloat16().requires_grad_()
+    b2 = (torch.randn(256, device=DEV) * 0.1).bfloat16().requires_grad_()
+    before = dict(lm.GEMM_STATS)
+    h, a = lm.linear_gelu(x, w1, b1)
+    assert not a.requires_grad
+    y = lm.gelu_linear(h, w2, b2, a=a)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    ref = [t.detach().float().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    yf = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2]), approximate="tanh"), ref[3], ref[4])
+    (yf * gy.float()).sum().backward()
+    assert _rel(y, yf) < 1e-2
+    assert _rel(a, F.gelu(h.float(), approximate="tanh")) < 1e-2
+    for t, r in zip((x, w1, b1, w2, b2), ref):
+        assert _rel(t.grad, r.grad) < 2e-2
+    if mode == "dta":
+        assert lm._GEMM_CHOICE.get(("fwd_gelub", 512, 1024, 256), 0) >= lm.K64
+        assert lm.GEMM_STATS["dta"] > before["dta"]
+
+
 @pytest.mark.parametrize("threshold", ["0", "1", "200"])
 def test_ddp_deferred_grouped_weight_gradients(threshold, monkeypatch):
     """Weight + bias gradients deferred and computed by grouped launches (DTA_WGRAD_GROUP tiles
