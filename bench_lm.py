@@ -114,7 +114,7 @@ def main():
         from distributed_training_amd.ops.optim import FusedAdamW
         from distributed_training_amd.parallel.comm import make_comm
 
-        comm = make_comm(dev)
+        comm = make_comm(dev, bulk=True)  # DDP / FSDP traffic: RCCL or the IPC push plane per message size
         model = model.to(dev)
         if args.strategy == "ddp":
             from distributed_training_amd.parallel.ddp import DistributedDataParallel
@@ -272,6 +272,9 @@ def main():
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
         out["optimizer_in_backward"] = bool(overlap_opt)
         out["step_graph"] = graphed is not None
+        routes = getattr(getattr(wrapped, "comm", None), "routes", None)
+        if routes is not None:
+            out["comm_routes"] = routes()
         out["gemm_calls"] = {"dta": _lm.GEMM_STATS["dta"], "hipblaslt": _lm.GEMM_STATS["torch"]}
         out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": ("hipblaslt" if not v else
                                                              f"k64/t{v - _lm.K64}" if v >= _lm.K64 else f"r2/t{v}")

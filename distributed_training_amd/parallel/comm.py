@@ -420,14 +420,20 @@ class RcclComm(_StreamComm):
         self._comm.destroy()
 
 
-def make_comm(device: torch.device, prefer: str = "auto", group=None) -> Communicator:
+def make_comm(device: torch.device, prefer: str = "auto", group=None, bulk: bool = False) -> Communicator:
     """Pick the communicator for ``device``.
 
     GPU: native RCCL (``prefer`` auto|rccl, the default); the IPC direct-push
     collectives (:class:`~.ipc.IpcComm`) with ``prefer="ipc"`` / ``DTA_COMM=ipc``,
     and always when several ranks share one GPU (``DTA_SHARED_GPU=1``: RCCL
-    refuses that).  CPU, or ``DTA_COMM=torch``: torch.distributed (gloo)."""
+    refuses that).  ``bulk``: a communicator for large gradient / parameter traffic
+    (the DDP / FSDP engines): on a multi-GPU node RCCL and the IPC push plane are
+    BOTH built and each message is routed to the one that measured faster for its
+    op, dtype and size (:class:`~.routed.RoutedComm`; ``DTA_IPC_COLL=0`` disables it;
+    any failure falls back to RCCL on every rank).  CPU, or ``DTA_COMM=torch``:
+    torch.distributed (gloo)."""
     from .ipc import IpcComm, shared_gpu
+    from .p2p import intra_node
 
     rank = dist.get_rank() if dist.is_initialized() else 0
     ws = dist.get_world_size() if dist.is_initialized() else 1
@@ -436,5 +442,17 @@ def make_comm(device: torch.device, prefer: str = "auto", group=None) -> Communi
         if ws > 1 and (shared_gpu() or prefer == "ipc" or env == "ipc"):
             return IpcComm(rank, ws, device)
         if prefer in ("auto", "rccl", "ipc"):
-            return RcclComm(rank, ws, device)
+            rccl = RcclComm(rank, ws, device)
+            if bulk and 1 < ws <= 8 and intra_node() and os.environ.get("DTA_IPC_COLL", "auto") != "0":
+                try:
+                    ipc = IpcComm(rank, ws, device, tag="routed")
+                except Exception as e:  # noqa: BLE001 - raised on every rank alike (collective checks)
+                    import logging
+
+                    logging.getLogger(__name__).warning("IPC data plane unavailable (%s): RCCL only", e)
+                    return rccl
+                from .routed import RoutedComm
+
+                return RoutedComm(rccl, ipc)
+            return rccl
     return TorchComm(group=group, device=device)

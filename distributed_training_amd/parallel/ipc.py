@@ -6,8 +6,9 @@ whose data plane is the direct-push kernels of ``ipc_coll.hip`` and whose
 control plane (rendezvous, handle exchange, the rare op the kernels do not
 cover) is ``torch.distributed``.  Two uses:
 
-* **xGMI data plane on a real node** (``DTA_COMM=ipc``, or as the mid-size
-  bucket path of :class:`~.comm.RcclComm` with ``DTA_IPC_COLL=1``): one push
+* **xGMI data plane on a real node** (``DTA_COMM=ipc`` for everything, or -- the
+  default for the DDP / FSDP engines -- per message beside RCCL, wherever it
+  measured faster at construction: :class:`~.routed.RoutedComm`): one push
   hop per peer on each of the 7 point-to-point links instead of a ring's
   2(W-1) dependent steps; results are bit-identical on every
   rank (each chunk is reduced once, in rank order).

@@ -25,7 +25,7 @@ def default_comm(device: torch.device) -> Communicator:
     """One communicator per process and device (RCCL on GPU, gloo on CPU)."""
     key = str(device)
     if key not in _COMMS:
-        _COMMS[key] = make_comm(device) if device.type == "cuda" else TorchComm(device=device)
+        _COMMS[key] = make_comm(device, bulk=True) if device.type == "cuda" else TorchComm(device=device)
     return _COMMS[key]
 
 

@@ -328,3 +328,54 @@ def test_fsdp_cpu_offload_matches_device_shards(ws, opt_name):
         _offload_worker(0, 1, opt_name)
     else:
         run_gloo(_offload_worker, ws, opt_name)
+
+
+def _routed_worker(rank, ws):
+    """RoutedComm on the GPU: two IPC data planes of different configuration stand in for RCCL
+    and the push plane (RCCL refuses two ranks on one GPU).  The calibration table is the same
+    on every rank; with each route forced, every op is exact; routing follows the size classes."""
+    import hashlib
+
+    import torch.distributed as dist
+
+    from distributed_training_amd.parallel.ipc import IpcComm
+    from distributed_training_amd.parallel.routed import MiB, RoutedComm
+
+    dev = _shared()
+    prim = IpcComm(rank, ws, dev, tag="prim", slot_mb=1)
+    fast = IpcComm(rank, ws, dev, tag="fast", slot_mb=8)
+    rc = RoutedComm(prim, fast, sizes=(MiB, 4 * MiB), iters=2)
+    sig = hashlib.sha256(repr(sorted(rc.routes().items())).encode()).digest()
+    sigs = [None] * ws
+    dist.all_gather_object(sigs, sig)
+    assert all(s == sig for s in sigs), "ranks disagree on the route table"
+    g = torch.Generator(device="cpu").manual_seed(7 + rank)
+    for route in ("primary", "fast"):
+        rc.table = {k: [route, route] for k in rc.table}
+        before = rc.counts[route]
+        for dt in (torch.float32, torch.bfloat16):
+            for n in (1000, 600000):  # both size classes
+                x = torch.randn(n, generator=g).to(dt).to(dev)
+                parts = _gather_cpu(x)
+                want = parts[0].clone()
+                for p in parts[1:]:
+                    want = want + p
+                rc.all_reduce(x, "sum")
+                torch.cuda.synchronize()
+                assert torch.equal(x.cpu(), want.to(dt)), (route, dt, n)
+                m = n // ws
+                out = torch.empty(ws * m, dtype=dt, device=dev)
+                rc.all_gather_into(out, torch.full((m,), float(rank + 1), dtype=dt, device=dev))
+                o = torch.empty(m, dtype=dt, device=dev)
+                rc.reduce_scatter_into(o, torch.ones(ws * m, dtype=dt, device=dev), "sum")
+                torch.cuda.synchronize()
+                assert torch.equal(out.cpu(), torch.arange(1, ws + 1).repeat_interleave(m).to(dt))
+                assert torch.equal(o.cpu(), torch.full((m,), float(ws)).to(dt))
+        assert rc.counts[route] == before + 12
+    rc.poll_errors()
+    rc.destroy()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_routed_comm_shared_gpu(ws):
+    run_gloo(_routed_worker, ws)

@@ -449,3 +449,42 @@ def _fsdp_llama_units(rank, ws, steps):
 @pytest.mark.parametrize("ws", [2, 4])
 def test_native_fsdp_llama_embedding_head_units(ws):
     run_gloo(_fsdp_llama_units, ws, 3)
+
+
+def _routed_cpu(rank, ws):
+    """RoutedComm mechanics over two gloo data planes: a calibrated table identical on every
+    rank, messages routed by (op, dtype, size class), results exact on both routes."""
+    import hashlib
+
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.routed import MiB, RoutedComm
+
+    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB // 16, MiB // 4), iters=2)
+    sig = hashlib.sha256(repr(sorted(rc.routes().items())).encode()).digest()
+    sigs = [None] * ws
+    dist.all_gather_object(sigs, sig)
+    assert all(s == sig for s in sigs), "ranks disagree on the route table"
+    for table_route in ("primary", "fast"):
+        rc.table = {k: [table_route] * 2 for k in rc.table}
+        before = dict(rc.counts)
+        for n in (1000, 50000):  # both size classes (4 KB, 200 KB of fp32)
+            x = torch.arange(n, dtype=torch.float32) + rank
+            rc.all_reduce(x, "sum")
+            assert torch.equal(x, 2 * torch.arange(n, dtype=torch.float32) + sum(range(ws)))
+            out = torch.empty(ws * n)
+            rc.all_gather_into(out, torch.full((n,), float(rank)))
+            assert torch.equal(out, torch.arange(ws).repeat_interleave(n).float())
+            o = torch.empty(n)
+            rc.reduce_scatter_into(o, torch.ones(ws * n), "sum")
+            assert torch.equal(o, torch.full((n,), float(ws)))
+        assert rc.counts[table_route] == before[table_route] + 6
+    # max is never routed to the fast plane
+    rc.table = {k: ["fast"] * 2 for k in rc.table}
+    before = dict(rc.counts)
+    y = torch.tensor([float(rank)])
+    rc.all_reduce(y, "max")
+    assert float(y) == ws - 1 and rc.counts == before
+
+
+def test_routed_comm_cpu():
+    run_gloo(_routed_cpu, 2)
