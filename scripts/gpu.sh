@@ -21,7 +21,8 @@ task=${1:-tests}
 shift || true
 case "$task" in
   tests)
-    timeout -k 10 1000 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 120 --timeout-method thread \
+    [ $# -eq 0 ] && set -- tests
+    timeout -k 10 1000 python -u -m pytest "$@" -m gpu -x -v --timeout 120 --timeout-method thread \
       > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu.log ;;
   smoke)

@@ -379,3 +379,67 @@ def _routed_worker(rank, ws):
 @pytest.mark.parametrize("ws", [2, 4])
 def test_routed_comm_shared_gpu(ws):
     run_gloo(_routed_worker, ws)
+
+
+def _graph_multirank_worker(rank, ws):
+    """The whole DDP step (GPT-2 with several buckets, deferred grouped weight gradients, the
+    bucket all-reduces on the IPC comm stream, fused AdamW) captured ONCE per rank as a hipGraph
+    and replayed: losses and fp32 master weights bit-identical to the eager steps on the same
+    batches on every rank, and identical across ranks (the replayed collectives really ran)."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.engine.step_graph import GraphedStep
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops import lm
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    g = torch.Generator(device="cpu").manual_seed(40 + rank)  # different batches per rank
+    data = [torch.randint(0, 1024, (2, 129), generator=g).to(dev) for _ in range(5)]
+    seq = [data[0]] * 3 + data[1:]  # GraphedStep's 3 warm-up steps train on the static batch
+    out = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        comm = IpcComm(rank, ws, dev, tag=f"graph{int(graphed)}")
+        ddp = DistributedDataParallel(model, comm=comm, device=dev, param_dtype=torch.bfloat16,
+                                      bucket_cap_mb=0.5, first_bucket_mb=0.25)
+        assert len(ddp.buckets) >= 4
+        opt = FusedAdamW(ddp.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+        before = lm.GEMM_STATS["deferred_wgrad"]
+
+        def step(xb):
+            opt.zero_grad(set_to_none=True)
+            loss = ddp(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        losses = []
+        if graphed:
+            gs = GraphedStep(step, [data[0].clone()], warmup=3, engine=ddp)
+            assert gs.ok, gs.error
+            for xb in seq[3:]:
+                losses.append(gs(xb).float().clone())
+        else:
+            for xb in seq:
+                losses.append(step(xb).float().clone())
+            losses = losses[3:]
+            assert lm.GEMM_STATS["deferred_wgrad"] > before  # the grouped deferred path is exercised
+        torch.cuda.synchronize()
+        comm.poll_errors()
+        out.append((torch.stack(losses).cpu(), ddp.flat.master.clone()))
+    assert torch.equal(out[0][0], out[1][0]), (rank, out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1]), rank
+    # replicas identical across ranks (gradients were averaged by the replayed collectives)
+    parts = _gather_cpu(out[1][1])
+    assert all(torch.equal(p, parts[0]) for p in parts[1:])
+    assert not torch.equal(out[1][1], out[0][1] * 0)  # (sanity: trained weights)
+    dist.barrier()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_step_graph_multirank_matches_eager(ws):
+    run_gloo(_graph_multirank_worker, ws)
