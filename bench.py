@@ -11,8 +11,14 @@ Linear(512,1), random init; synthetic data = the reference's MyTrainDataset
 (2048 samples of rand(20), rand(1)) with DistributedSampler order; batch 32
 per GPU; SGD lr 1e-3; MSE loss (the reference's cross-entropy on a 1-wide
 output is identically zero).  Every timed step does the full
-work: gather, forward, loss, backward, RCCL all-reduce of the gradients, SGD
-update.  bf16 = MFMA operand precision (fp32 accumulate, fp32 master weights).
+work: gather, forward, loss, backward, gradient exchange, SGD update.  The
+exchange: at N > 1 the persistent program's in-kernel all-reduce of the 1 / N
+pre-scaled gradients over xGMI peer memory (or RCCL, whichever form the
+start-up calibration measured faster: "step_form" in the JSON); at N = 1 there
+is no peer and the persistent program runs no exchange (an all-reduce over one
+rank is the identity; torch's DDP at world size 1 still launches one -- so does
+this program's per-step form, DTA_MLP_PERSISTENT=0, with ``--allreduce-world1 1``).
+bf16 = MFMA operand precision (fp32 accumulate, fp32 master weights).
 
 ``--impl fused`` (default): this framework's fused gfx950 step program.
 ``--impl generic``: this framework's generic engine (autograd + native DDP

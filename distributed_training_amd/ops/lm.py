@@ -452,7 +452,7 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # opens a forward generation per call (:func:`new_forward_generation`) and the
 # native Linear counts its uses in it; without a DDP engine (no generations) no
 # weight qualifies.  Measured on the GPT-2 small DDP step (one MI355X,
-# scripts/gpu_ab_lm.sh, same-box pairs): 11.9-12.45 -> 11.4-12.2 ms with the 128 x 128
+# same-box A/B pairs, round 2): 11.9-12.45 -> 11.4-12.2 ms with the 128 x 128
 # split-K kernel at split 2 on one side stream in 6 of 8 pairs, but 12.4 -> 15.6 / 18.2 ms
 # on one box (the hardware scheduler's interleaving of the two queues is not under
 # this code's control), so it is not the default; its own split 11.5, split 1 12.3 ms; the
@@ -1047,7 +1047,7 @@ class _LinearCrossEntropy(Function):
             dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             # (the scale on the [N, C] operand instead of this [V, C] product measured no better: same-box
-            # GPT-2 pairs 11.12-12.46 vs 11.05-11.39 ms, scripts/gpu_ab_heads.sh)
+            # GPT-2 pairs 11.12-12.46 vs 11.05-11.39 ms, round 2)
             dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam)).mul_(s)
         return dx, dw, None, None
 

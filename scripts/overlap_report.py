@@ -123,7 +123,46 @@ def main(d):
         print("\n# roctx ranges (host, window): count, total us, name")
         for name, (n, us) in sorted(rng.items(), key=lambda kv: -kv[1][1])[:30]:
             print(f"{n:5d} {us:10.1f}  {name}")
+        _per_collective(ms, ks, t0, pu)
     return 0
+
+
+def _per_collective(ms, ks, t0, pu):
+    """Collective kernels attributed to the host range that enqueued them (bucket all-reduce,
+    FSDP unit all-gather / reduce-scatter): every comm kernel starting after a collective range
+    began and before the next one began belongs to it.  Per range name: kernels, device time,
+    and the share of it overlapped by compute kernels."""
+    marks = []
+    for r in ms:
+        try:
+            name = _col(r, "Function", "Message", "Name")
+            s = int(_col(r, "Start_Timestamp"))
+        except (KeyError, ValueError):
+            continue
+        if (t0 is None or s >= t0) and any(k in name for k in ("allgather", "reduce_scatter", "allreduce")):
+            marks.append((s, name))
+    if not marks:
+        return
+    marks.sort()
+    comm = sorted((int(_col(r, "Start_Timestamp")), int(_col(r, "End_Timestamp")))
+                  for r in ks if any(k in _col(r, "Kernel_Name").lower() for k in COMM_KEYS)
+                  and (t0 is None or int(_col(r, "Start_Timestamp")) >= t0))
+    per = defaultdict(list)
+    j = 0
+    for i, (s, name) in enumerate(marks):
+        nxt = marks[i + 1][0] if i + 1 < len(marks) else float("inf")
+        while j < len(comm) and comm[j][0] < s:
+            j += 1
+        k = j
+        while k < len(comm) and comm[k][0] < nxt:
+            per[name].append(comm[k])
+            k += 1
+    print("\n# collectives by enqueueing range (window): kernels, device us, overlapped by compute %, range")
+    for name, iv in sorted(per.items()):
+        u = _union(iv)
+        tot = _measure(u)
+        ovl = _intersect(u, pu)
+        print(f"{len(iv):5d} {tot / 1e3:10.1f} {100 * ovl / tot if tot else 0.0:6.1f}  {name}")
 
 
 if __name__ == "__main__":
