@@ -36,12 +36,12 @@ class ConfigError(ValueError):
 class ConfigNode(dict):
     """dict with attribute access; nested dicts are ConfigNodes."""
 
-    def __init__(self, *args, **kwargs):
+    def __init__(self, *args, **kwargs) -> None:
         super().__init__()
         for k, v in dict(*args, **kwargs).items():
             self[k] = v
 
-    def __setitem__(self, key, value):
+    def __setitem__(self, key, value) -> None:
         super().__setitem__(key, _wrap(value))
 
     def __getattr__(self, item):
@@ -50,10 +50,10 @@ class ConfigNode(dict):
         except KeyError as e:
             raise AttributeError(f"config has no key {item!r} (keys: {list(self.keys())})") from e
 
-    def __setattr__(self, key, value):
+    def __setattr__(self, key, value) -> None:
         self[key] = value
 
-    def __delattr__(self, item):
+    def __delattr__(self, item) -> None:
         del self[item]
 
     def __deepcopy__(self, memo):
@@ -121,7 +121,7 @@ def parse_value(text: str) -> Any:
 class Override:
     __slots__ = ("key", "value", "op")
 
-    def __init__(self, key: str, value: Any, op: str):
+    def __init__(self, key: str, value: Any, op: str) -> None:
         self.key, self.value, self.op = key, value, op
 
     def __repr__(self):

@@ -32,7 +32,7 @@ class MyTrainDataset(Dataset):
     """
 
     def __init__(self, size: int, input_size: int = 20, output_size: int = 1, seed: Optional[int] = None,
-                 vectorized: Optional[bool] = None):
+                 vectorized: Optional[bool] = None) -> None:
         self.size = int(size)
         gen = None
         if seed is not None:
@@ -65,7 +65,7 @@ class SyntheticTokens(Dataset):
     """Random token sequences for the GPT-2 / Llama benchmark configs
     (random-init weights, synthetic data: there is no dataset download)."""
 
-    def __init__(self, size: int, seq_len: int, vocab_size: int, seed: int = 0):
+    def __init__(self, size: int, seq_len: int, vocab_size: int, seed: int = 0) -> None:
         g = torch.Generator()
         g.manual_seed(seed)
         self.seq_len = seq_len
@@ -87,7 +87,7 @@ class DeviceDataLoader:
     """
 
     def __init__(self, dataset, batch_size: int, sampler: Optional[DistributedSampler] = None,
-                 device: Optional[torch.device] = None, drop_last: bool = False):
+                 device: Optional[torch.device] = None, drop_last: bool = False) -> None:
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.sampler = sampler if sampler is not None else DistributedSampler(dataset)

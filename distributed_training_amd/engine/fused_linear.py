@@ -61,7 +61,7 @@ def linear_eligible(module: nn.Module, optimizer, loader, loss: str, device: tor
 
 class FusedLinearProgram:
     def __init__(self, module: nn.Linear, optimizer, loader, comm, loss: str = "cross_entropy",
-                 loss_len: int = 4096):
+                 loss_len: int = 4096) -> None:
         self.module = module
         self.opt = optimizer
         self.loader = loader

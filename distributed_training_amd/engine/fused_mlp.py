@@ -81,7 +81,7 @@ class FusedMLPProgram:
 
     def __init__(self, module, optimizer, loader, comm, loss: str = "mse", graph_steps: int = 32,
                  own_tiles: Optional[int] = None, allreduce_world1: bool = True, loss_len: int = 4096,
-                 persistent: Optional[bool] = None):
+                 persistent: Optional[bool] = None) -> None:
         self.module = module
         self.opt = optimizer
         self.loader = loader

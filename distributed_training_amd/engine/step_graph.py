@@ -57,7 +57,7 @@ def _agree_all_ok(engine: Any, ok: bool, device: torch.device) -> bool:
 
 class GraphedStep:
     def __init__(self, step_fn: Callable[..., torch.Tensor], static_inputs: Sequence[torch.Tensor],
-                 warmup: int = 3, engine: Optional[Any] = None):
+                 warmup: int = 3, engine: Optional[Any] = None) -> None:
         """``step_fn(*static_inputs)`` runs one full training step (zero_grad, forward,
         backward, optimizer step) and returns the loss tensor.  ``warmup`` eager steps
         run first on the capture stream (they are real training steps).  ``engine``:

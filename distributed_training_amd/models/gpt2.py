@@ -45,7 +45,7 @@ class GPT2Config:
 
 
 class LayerNorm(nn.Module):
-    def __init__(self, n: int, eps: float = 1e-5):
+    def __init__(self, n: int, eps: float = 1e-5) -> None:
         super().__init__()
         self.weight = nn.Parameter(torch.ones(n))
         self.bias = nn.Parameter(torch.zeros(n))
@@ -62,7 +62,7 @@ class LayerNorm(nn.Module):
 
 
 class CausalSelfAttention(nn.Module):
-    def __init__(self, cfg: GPT2Config):
+    def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
         self.n_head = cfg.n_head
         self.c_attn = lm.Linear(cfg.n_embd, 3 * cfg.n_embd)
@@ -76,7 +76,7 @@ class CausalSelfAttention(nn.Module):
 
 
 class MLP(nn.Module):
-    def __init__(self, cfg: GPT2Config):
+    def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
         self.c_fc = lm.Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
@@ -89,7 +89,7 @@ class MLP(nn.Module):
 
 
 class Block(nn.Module):
-    def __init__(self, cfg: GPT2Config):
+    def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
         self.ln_1 = LayerNorm(cfg.n_embd)
         self.attn = CausalSelfAttention(cfg)
@@ -109,7 +109,7 @@ class Block(nn.Module):
 class GPT2(nn.Module):
     block_class = Block
 
-    def __init__(self, cfg: GPT2Config):
+    def __init__(self, cfg: GPT2Config) -> None:
         super().__init__()
         self.cfg = cfg
         self.vocab_size = cfg.vocab_size
@@ -128,7 +128,7 @@ class GPT2(nn.Module):
                 nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * cfg.n_layer))
 
     @staticmethod
-    def _init(m):
+    def _init(m) -> None:
         if isinstance(m, nn.Linear):
             nn.init.normal_(m.weight, 0.0, 0.02)
             if m.bias is not None:
@@ -136,7 +136,7 @@ class GPT2(nn.Module):
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, 0.0, 0.02)
 
-    def enable_activation_checkpointing(self, on: bool = True):
+    def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 
     def num_params(self) -> int:

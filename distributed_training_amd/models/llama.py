@@ -41,7 +41,7 @@ class LlamaConfig:
 
 
 class RMSNorm(nn.Module):
-    def __init__(self, n: int, eps: float):
+    def __init__(self, n: int, eps: float) -> None:
         super().__init__()
         self.weight = nn.Parameter(torch.ones(n))
         self.eps = eps
@@ -57,7 +57,7 @@ class RMSNorm(nn.Module):
 
 
 class Attention(nn.Module):
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig) -> None:
         super().__init__()
         self.H, self.Hkv = cfg.n_head, cfg.n_kv_head
         self.D = cfg.n_embd // cfg.n_head
@@ -72,7 +72,7 @@ class Attention(nn.Module):
 
 
 class FeedForward(nn.Module):
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig) -> None:
         super().__init__()
         self.w13 = lm.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
         self.w2 = lm.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
@@ -82,7 +82,7 @@ class FeedForward(nn.Module):
 
 
 class Block(nn.Module):
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig) -> None:
         super().__init__()
         self.attention_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
         self.attention = Attention(cfg)
@@ -99,7 +99,7 @@ class Block(nn.Module):
 class Llama(nn.Module):
     block_class = Block
 
-    def __init__(self, cfg: LlamaConfig):
+    def __init__(self, cfg: LlamaConfig) -> None:
         super().__init__()
         self.cfg = cfg
         self.vocab_size = cfg.vocab_size
@@ -119,7 +119,7 @@ class Llama(nn.Module):
                 s = std / math.sqrt(2 * cfg.n_layer) if n.endswith(("wo.weight", "w2.weight")) else std
                 nn.init.normal_(p, 0.0, s)
 
-    def enable_activation_checkpointing(self, on: bool = True):
+    def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 
     def fsdp_extra_units(self):

@@ -26,7 +26,7 @@ ACTS = {
 
 class MLP(nn.Module):
     def __init__(self, input_size: int = 20, hidden_size: Union[int, Sequence[int]] = 512, output_size: int = 1,
-                 activation: str = "relu"):
+                 activation: str = "relu") -> None:
         super().__init__()
         hidden: List[int] = [hidden_size] if isinstance(hidden_size, int) else list(hidden_size)
         dims = [input_size] + hidden + [output_size]

@@ -18,7 +18,7 @@ _native: Optional[Any] = None
 _native_err: Optional[BaseException] = None
 
 
-def _try_import():
+def _try_import() -> None:
     global _native, _native_err
     if _native is not None or _native_err is not None:
         return

@@ -26,7 +26,7 @@ from torch.autograd import Function
 from . import native
 
 
-def _need_bf16(*ts):
+def _need_bf16(*ts) -> None:
     for t in ts:
         if t.dtype != torch.bfloat16:
             raise TypeError(f"GPU transformer ops need bf16 tensors (got {t.dtype}); "

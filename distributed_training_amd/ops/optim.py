@@ -111,7 +111,7 @@ def _covers(params, fg) -> bool:
 
 class FusedSGD(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
-                 weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False):
+                 weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False) -> None:
         if nesterov and (momentum <= 0 or dampening != 0):
             raise ValueError("Nesterov momentum requires a momentum and zero dampening")
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
@@ -219,7 +219,7 @@ class FusedSGD(torch.optim.Optimizer):
                 if v is not None:
                     self.state[p]["momentum_buffer"] = v.to(p.device, torch.float32).reshape(p.shape).clone()
 
-    def _single_gpu(self, fg, p, lr, mom, damp, wd, nest, maxi):
+    def _single_gpu(self, fg, p, lr, mom, damp, wd, nest, maxi) -> None:
         i = fg.index_of(p)
         state = self.state[p]
         first = "momentum_buffer" not in state or state["momentum_buffer"] is None
@@ -232,7 +232,7 @@ class FusedSGD(torch.optim.Optimizer):
         native().flat_sgd(m, m, g, None if buf is None else buf.view(-1), pb, lr, mom, damp, wd, 1.0, nest, maxi,
                           first, -1)
 
-    def zero_grad(self, set_to_none: bool = True):
+    def zero_grad(self, set_to_none: bool = True) -> None:
         flats_done = set()
         for group in self.param_groups:
             flats, singles = _split_params(group["params"])
@@ -252,7 +252,7 @@ class FusedSGD(torch.optim.Optimizer):
                         p.grad.zero_()
 
 
-def _adam_ref(p, g, m, v, vmax, step, lr, b1, b2, eps, wd, adamw, maximize, amsgrad):
+def _adam_ref(p, g, m, v, vmax, step, lr, b1, b2, eps, wd, adamw, maximize, amsgrad) -> None:
     g = -g if maximize else g
     if wd:
         if adamw:
@@ -275,7 +275,7 @@ class FusedAdamW(torch.optim.Optimizer):
     """AdamW (``adamw=True``, default) or Adam with L2 (``adamw=False``)."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 amsgrad: bool = False, maximize: bool = False, adamw: bool = True):
+                 amsgrad: bool = False, maximize: bool = False, adamw: bool = True) -> None:
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
                         maximize=maximize, adamw=adamw)
         super().__init__(params, defaults)

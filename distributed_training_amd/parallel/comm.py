@@ -51,7 +51,7 @@ def _stdout_to_stderr():
 class CommWork:
     """Handle of an asynchronous collective."""
 
-    def __init__(self, torch_work=None, event=None, post=None):
+    def __init__(self, torch_work=None, event=None, post=None) -> None:
         self._work = torch_work
         self._event = event
         self._post = post
@@ -103,7 +103,7 @@ class TorchComm(Communicator):
 
     name = "torch"
 
-    def __init__(self, group=None, device: Optional[torch.device] = None):
+    def __init__(self, group=None, device: Optional[torch.device] = None) -> None:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -155,13 +155,13 @@ class TorchComm(Communicator):
         work = dist.broadcast(t, src=src, group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def all_to_all_single(self, out, inp):
+    def all_to_all_single(self, out, inp) -> None:
         if self.world_size == 1:
             out.copy_(inp)
             return
         dist.all_to_all_single(out, inp, group=self.group)
 
-    def barrier(self):
+    def barrier(self) -> None:
         if self.world_size > 1:
             dist.barrier(group=self.group)
 
@@ -189,7 +189,7 @@ class CommWatchdog:
     device synchronisation: tracking is a deque append per collective."""
 
     def __init__(self, name: str, timeout_s: float, on_timeout: Callable[[], None], poll_s: float = 0.0,
-                 exit_grace_s: float = 60.0):
+                 exit_grace_s: float = 60.0) -> None:
         self.name = name
         self.timeout_s = float(timeout_s)
         self.poll_s = float(poll_s) if poll_s > 0 else max(0.05, min(2.0, self.timeout_s / 20))
@@ -309,7 +309,7 @@ class RcclComm(_StreamComm):
     name = "rccl"
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
-                 stream_priority: int = -1, timeout_s: Optional[float] = None):
+                 stream_priority: int = -1, timeout_s: Optional[float] = None) -> None:
         from ..ops import ensure_rccl
 
         C = ensure_rccl()
@@ -340,7 +340,7 @@ class RcclComm(_StreamComm):
         if world_size > 1 and store is not None:
             from .p2p import maybe_create
 
-            def _min(t):
+            def _min(t) -> None:
                 self._comm.all_reduce(t, "min", int(torch.cuda.current_stream(device).cuda_stream))
                 torch.cuda.current_stream(device).synchronize()
 
@@ -373,7 +373,7 @@ class RcclComm(_StreamComm):
         return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t],
                              f"broadcast {t.numel()} x {t.dtype}")
 
-    def all_to_all_single(self, out, inp):
+    def all_to_all_single(self, out, inp) -> None:
         self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp], "all_to_all")
 
     def abort(self) -> None:
@@ -408,13 +408,13 @@ class RcclComm(_StreamComm):
         if self._p2p is not None:
             self._p2p.poll()
 
-    def barrier(self):
+    def barrier(self) -> None:
         x = torch.zeros(1, device=self.device)
         self.all_reduce(x)
         torch.cuda.current_stream(self.device).synchronize()
         self.raise_if_error()
 
-    def destroy(self):
+    def destroy(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()
         self._comm.destroy()

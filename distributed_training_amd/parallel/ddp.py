@@ -60,7 +60,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Communicator] = None,
                  device: Optional[torch.device] = None, bucket_cap_mb="auto",
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
-                 param_dtype: torch.dtype = torch.float32, init_sync: bool = True):
+                 param_dtype: torch.dtype = torch.float32, init_sync: bool = True) -> None:
         super().__init__()
         self.module = module
         self.comm = comm or TorchComm()
@@ -245,7 +245,7 @@ class DistributedDataParallel(nn.Module):
         self._ov_first = True
         ref = weakref.ref(self)
 
-        def on_flush():
+        def on_flush() -> None:
             me = ref()
             if me is None:  # engine gone: drop this listener
                 if on_flush in lm.FLUSH_LISTENERS:

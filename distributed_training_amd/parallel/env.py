@@ -37,7 +37,7 @@ class DistributedEnvironment:
     """Manages distributed training setup and environment variables."""
 
     def __init__(self, device: str = "auto", backend: Optional[str] = None, timeout_s: Optional[float] = None,
-                 comm: str = "auto"):
+                 comm: str = "auto") -> None:
         self.device = _determine_device(device)
         self.is_gpu = self.device == "cuda"
         self.global_rank = int(os.environ.get("RANK", 0))

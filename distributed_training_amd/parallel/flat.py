@@ -43,7 +43,7 @@ class FlatParamGroup:
     def __init__(self, params: Sequence[torch.nn.Parameter], device: torch.device,
                  param_dtype: torch.dtype = torch.float32, grad_dtype: Optional[torch.dtype] = None,
                  names: Optional[Sequence[str]] = None, pad_after: Optional[Dict[int, int]] = None,
-                 pin_memory: bool = False):
+                 pin_memory: bool = False) -> None:
         self.params: List[torch.nn.Parameter] = list(params)
         self.names = list(names) if names is not None else [f"p{i}" for i in range(len(self.params))]
         self.device = device

@@ -118,7 +118,7 @@ class _SplitInto(torch.autograd.Function):
 
 class _Unit:
     def __init__(self, owner: "FullyShardedDataParallel", module: nn.Module,
-                 entries: List[Tuple[nn.Module, str, str, nn.Parameter]], is_root: bool, index: int):
+                 entries: List[Tuple[nn.Module, str, str, nn.Parameter]], is_root: bool, index: int) -> None:
         self.owner = owner
         self.module = module
         self.is_root = is_root
@@ -297,7 +297,7 @@ class FullyShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Communicator] = None,
                  device: Optional[torch.device] = None, wrap_policy: WrapPolicy = None,
                  param_dtype: torch.dtype = torch.float32, reshard_after_forward: bool = True,
-                 prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False):
+                 prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False) -> None:
         super().__init__()
         self.cpu_offload = bool(cpu_offload)
         if self.cpu_offload and param_dtype != torch.float32:

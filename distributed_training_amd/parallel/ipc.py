@@ -66,7 +66,7 @@ class IpcComm(_StreamComm):
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
                  slot_mb: Optional[float] = None, timeout_s: Optional[float] = None, self_test: bool = True,
-                 stream_priority: int = -1):
+                 stream_priority: int = -1) -> None:
         from ..ops import native
 
         if not 1 <= world_size <= 8:
@@ -180,7 +180,7 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._all_reduce_native(t, op, s), async_op, [t])
         tmp = t.contiguous().clone()  # fresh allocation: 16-byte aligned
 
-        def run(s):
+        def run(s) -> None:
             self._all_reduce_native(tmp, op, s)
             with torch.cuda.stream(self.stream):
                 t.copy_(tmp.view_as(t))
@@ -214,7 +214,7 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._reduce_scatter_native(out, inp, op, s), async_op, [out, inp])
         mp = -(-m // 8) * 8  # pad each chunk to 16-byte alignment
 
-        def run(s):
+        def run(s) -> None:
             with torch.cuda.stream(self.stream):
                 ip = torch.zeros(W, mp, dtype=inp.dtype, device=inp.device)
                 ip[:, :m].copy_(inp.reshape(W, m))
@@ -238,7 +238,7 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._all_gather_native(out, inp, s), async_op, [out, inp])
         mp = -(-(m * es) // 16) * 16 // es if (16 % es == 0) else m
 
-        def run(s):
+        def run(s) -> None:
             with torch.cuda.stream(self.stream):
                 ip = torch.zeros(mp, dtype=inp.dtype, device=inp.device)
                 ip[:m].copy_(inp.reshape(-1))
@@ -262,14 +262,14 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._broadcast_native(t, src, s), async_op, [t])
         tmp = t.contiguous().clone()
 
-        def run(s):
+        def run(s) -> None:
             self._broadcast_native(tmp, src, s)
             with torch.cuda.stream(self.stream):
                 t.copy_(tmp.view_as(t))
 
         return self._enqueue(run, async_op, [t, tmp])
 
-    def all_to_all_single(self, out, inp):
+    def all_to_all_single(self, out, inp) -> None:
         if self.world_size == 1:
             out.copy_(inp)
             return
@@ -280,7 +280,7 @@ class IpcComm(_StreamComm):
         else:
             dist.all_to_all_single(out, inp)
 
-    def barrier(self):
+    def barrier(self) -> None:
         torch.cuda.current_stream(self.device).synchronize()
         if self.world_size > 1:
             self.stream.synchronize()
@@ -294,7 +294,7 @@ class IpcComm(_StreamComm):
 
     check_errors = poll_errors
 
-    def destroy(self):
+    def destroy(self) -> None:
         if self._h is not None:
             self._h.destroy()
             self._h = None

@@ -30,7 +30,7 @@ class P2PAllReduce:
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store, tag: str = "default",
                  max_elems: int = DEFAULT_MAX_ELEMS, timeout_iters: int = DEFAULT_TIMEOUT_ITERS,
-                 protocol: str = "ll"):
+                 protocol: str = "ll") -> None:
         from ..ops import native
 
         self.rank, self.world_size, self.device = rank, world_size, device

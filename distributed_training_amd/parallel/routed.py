@@ -46,7 +46,7 @@ class RoutedComm(Communicator):
 
     def __init__(self, primary: Communicator, fast: Communicator, sizes: Tuple[int, ...] = SIZES,
                  margin: float = 0.9, calibrate: bool = True, iters: int = 5,
-                 table: Optional[Dict[Tuple[str, torch.dtype], List[str]]] = None):
+                 table: Optional[Dict[Tuple[str, torch.dtype], List[str]]] = None) -> None:
         """``primary``: the default data plane (RCCL); ``fast``: the IPC push collectives.
         ``table`` (tests): a fixed route table instead of the calibration."""
         self.primary, self.fast = primary, fast
@@ -99,7 +99,7 @@ class RoutedComm(Communicator):
             out = torch.empty(n // W, dtype=dt, device=dev)
             fn = lambda: comm.reduce_scatter_into(out, inp, "sum")  # noqa: E731
 
-        def sync():
+        def sync() -> None:
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
 

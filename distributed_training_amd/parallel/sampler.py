@@ -22,7 +22,7 @@ class DistributedSampler(Sampler):
     """Drop-in for ``torch.utils.data.distributed.DistributedSampler``."""
 
     def __init__(self, dataset, num_replicas: Optional[int] = None, rank: Optional[int] = None,
-                 shuffle: bool = True, seed: int = 0, drop_last: bool = False):
+                 shuffle: bool = True, seed: int = 0, drop_last: bool = False) -> None:
         if num_replicas is None or rank is None:
             import torch.distributed as dist
 

@@ -72,7 +72,7 @@ class DistributedStrategy(ABC):
 
 class DDPStrategy(DistributedStrategy):
     def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb="auto", first_bucket_mb=None,
-                 mixed_precision: Optional[str] = None, comm: Optional[Communicator] = None):
+                 mixed_precision: Optional[str] = None, comm: Optional[Communicator] = None) -> None:
         self.local_rank = local_rank
         self.is_gpu = is_gpu
         self.bucket_cap_mb = bucket_cap_mb
@@ -101,7 +101,7 @@ class DDPStrategy(DistributedStrategy):
 class FSDPStrategy(DistributedStrategy):
     def __init__(self, is_gpu: bool, wrap_policy=None, mixed_precision: Optional[str] = None,
                  reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None,
-                 cpu_offload: bool = False):
+                 cpu_offload: bool = False) -> None:
         self.is_gpu = is_gpu
         # the reference offloads only when there is no GPU (fsdp_strategy.py:23-25), where this
         # engine's shards live on the host anyway; on a GPU run it is an explicit opt-in

@@ -59,7 +59,7 @@ def set_enabled(on: bool) -> None:
 class _Range:
     __slots__ = ("name",)
 
-    def __init__(self, name: str):
+    def __init__(self, name: str) -> None:
         self.name = name
 
     def __enter__(self):
@@ -98,16 +98,16 @@ def mark(name: str) -> None:
 class StepTimer:
     """Wall-clock step timer with device synchronisation at the boundaries."""
 
-    def __init__(self, device: Optional[torch.device] = None):
+    def __init__(self, device: Optional[torch.device] = None) -> None:
         self.device = device
         self.times: List[float] = []
         self._t0 = None
 
-    def _sync(self):
+    def _sync(self) -> None:
         if self.device is not None and self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
-    def start(self):
+    def start(self) -> None:
         self._sync()
         self._t0 = time.perf_counter()
 

@@ -75,7 +75,7 @@ def rank_logger(rank: int, log_dir: str = "logs") -> logging.Logger:
 class ManualDDP:
     """What DistributedDataParallel does, spelled out (no hooks, no overlap)."""
 
-    def __init__(self, model: nn.Module, comm, world_size: int, bucketed: bool = False):
+    def __init__(self, model: nn.Module, comm, world_size: int, bucketed: bool = False) -> None:
         self.model = model
         self.comm = comm
         self.world_size = world_size
