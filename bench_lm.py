@@ -184,7 +184,10 @@ def main():
         prof.pop()
 
     graphed = None
-    if args.impl == "native" and args.strategy == "ddp" and not args.no_graph:
+    # DDP: any world size (its bucket collectives are captured too); FSDP: one rank, where every unit
+    # aliases its shard (nothing is freed or re-allocated between units, so the step is capturable)
+    graph_ok = args.strategy == "ddp" or (ws == 1 and getattr(wrapped, "graph_capturable", lambda: False)())
+    if args.impl == "native" and graph_ok and not args.no_graph:
         # the whole step (zero_grad, forward, backward with the bucket hooks, AdamW) as ONE hipGraph;
         # its construction runs 3 eager warm-up steps and the capture (untimed, before the warm-up below)
         from distributed_training_amd.engine.step_graph import GraphedStep

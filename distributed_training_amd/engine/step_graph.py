@@ -19,8 +19,9 @@ What makes the native step capturable:
   synchronize) is made during the eager warm-up steps, before capture.
 The bucket collectives of the DDP engine are captured too (RCCL and the IPC push
 kernels are graph-capturable; tests/test_ipc_gpu.py replays a captured multi-rank
-step against the eager one); the FSDP engine is not (it frees and re-allocates unit
-storage between units), so it keeps the eager step.
+step against the eager one).  The FSDP engine at one rank too (every unit aliases its
+shard: ``FullyShardedDataParallel.graph_capturable``); at several ranks it frees and
+re-allocates unit storage between units, so it keeps the eager step.
 
 Host logic that the replay skips is redone around it:
 * the communicator's error poll of the engine's end-of-backward finalize (a peer

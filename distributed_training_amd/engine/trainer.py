@@ -199,8 +199,9 @@ class Trainer:
         c = self.config
         # only the fused optimizers keep their step count on the device (torch's AdamW keeps it on the
         # host and cannot be captured)
-        return (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip
-                and isinstance(self._strategy, DDPStrategy) and hasattr(self.model, "flat")
+        capturable = (isinstance(self._strategy, DDPStrategy) and hasattr(self.model, "flat")) or \
+            getattr(self.model, "graph_capturable", lambda: False)()
+        return (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip and capturable
                 and isinstance(self.optimizer, (FusedSGD, FusedAdamW))
                 and not c.desync_check_every and getattr(self, "_graphed", None) is not False)
 

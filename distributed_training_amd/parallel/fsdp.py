@@ -547,6 +547,12 @@ class FullyShardedDataParallel(nn.Module):
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):
                 u.free()
 
+    def graph_capturable(self) -> bool:
+        """The whole step can be captured as one hipGraph (engine/step_graph.py): at one rank without
+        CPU offload every unit aliases its shard, so no storage is freed or re-allocated between
+        units and no collective runs -- the replay repeats the same kernels on the same buffers."""
+        return self.world_size == 1 and not self.cpu_offload and all(u.alias for u in self.units)
+
     def _mark_grads_fresh(self) -> None:
         self._grad_fresh = True
         self._written = set()

@@ -728,6 +728,51 @@ def test_graphed_ddp_step_matches_eager():
     assert torch.equal(out[0][1], out[1][1])
 
 
+def test_fsdp_one_rank_step_graph_matches_eager():
+    """FSDP at one rank (every unit aliases its shard) captured as one hipGraph: the same losses
+    and fp32 master weights, bit for bit, as the eager steps on the same batches."""
+    from distributed_training_amd.engine.step_graph import GraphedStep
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    data = [torch.randint(0, 1024, (2, 257), generator=g).to(dev) for _ in range(4)]
+    seq = [data[0]] * 3 + data[1:]
+    out = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        w = FullyShardedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, wrap_policy=lm_wrap_policy(model),
+                                     param_dtype=torch.bfloat16)
+        assert w.graph_capturable()
+        opt = FusedAdamW(w.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+
+        def step(xb):
+            opt.zero_grad(set_to_none=True)
+            loss = w(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        losses = []
+        if graphed:
+            gs = GraphedStep(step, [data[0].clone()], warmup=3, engine=w)
+            assert gs.ok, gs.error
+            for xb in seq[3:]:
+                losses.append(gs(xb).float().clone())
+        else:
+            for xb in seq:
+                losses.append(step(xb).float().clone())
+            losses = losses[3:]
+        torch.cuda.synchronize()
+        out.append((torch.stack(losses).cpu(), w.shards.master.clone()))
+    assert torch.equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_fsdp_weight_used_twice_first_claim():
     """FSDP unit whose FIRST gradient piece of the backward belongs to a weight used twice: the
     buffer creation of that first claim must not erase the claim (the second use would get the
