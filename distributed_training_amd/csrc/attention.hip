@@ -44,6 +44,8 @@ namespace dta {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1.0e30f;
+// online-softmax rescale threshold (log2 domain): P up to 2^8 = 256 between rescales (bf16 / fp32 safe)
+constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -251,9 +253,12 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   #pragma unroll
         for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
       mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
-      const float mnew = fmaxf(m, mblk * c);
-      // rescale O and l only when some row's max moved (exact; no threshold)
-      if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+      // rescale O and l only when some row's max grew by more than kRescaleThr (log2 units):
+      // otherwise m stays and this block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md
+      // T13; the decision precedes every exponentiation of the block, so nothing at the old max
+      // is left unscaled).  The first block always rescales (m starts at -1e30).
+      if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
+        const float mnew = fmaxf(m, mblk * c);
         const float alpha = fexp2(m - mnew);
         l *= alpha;
   #pragma unroll
@@ -330,9 +335,12 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   #pragma unroll
         for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
       mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
-      const float mnew = fmaxf(m, mblk * c);
-      // rescale O and l only when some row's max moved (exact; no threshold)
-      if (__builtin_amdgcn_ballot_w64(mnew != m)) {
+      // rescale O and l only when some row's max grew by more than kRescaleThr (log2 units):
+      // otherwise m stays and this block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md
+      // T13; the decision precedes every exponentiation of the block, so nothing at the old max
+      // is left unscaled).  The first block always rescales (m starts at -1e30).
+      if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
+        const float mnew = fmaxf(m, mblk * c);
         const float alpha = fexp2(m - mnew);
         l *= alpha;
   #pragma unroll
@@ -423,7 +431,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   constexpr int NDT = D / 32;
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * D];
   __shared__ __attribute__((aligned(16))) bf16 dOs[2][BM * D];
-  __shared__ __attribute__((aligned(16))) float rc[2][2][BM];  // [buf][-lse/scale | -delta][q]
+  __shared__ __attribute__((aligned(16))) float rc[2][2][BM];  // [buf][-lse/scale | -delta][q] (16-B rows: float4 reads)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -489,12 +497,16 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       const int q0 = q0s + qt * 32;
       if (CAUSAL && NQT > 1 && q0 + 31 < kw0) continue;
       // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
+      // row constants of this lane's 16 accumulator rows: rows qt*32 + 8g + 4hh + 0..3 are 4
+      // consecutive floats -- 4 ds_read_b128 per array instead of 16 scalar reads
       f32x16 s, dp;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = qt * 32 + mfma32_row(i, lane);
-        s[i] = rc[buf][0][qi];
-        dp[i] = rc[buf][1][qi];
+      for (int g = 0; g < 4; ++g) {
+        const int q4 = qt * 32 + 8 * g + 4 * hh;
+        const float4 sv = *reinterpret_cast<const float4*>(&rc[buf][0][q4]);
+        const float4 dv = *reinterpret_cast<const float4*>(&rc[buf][1][q4]);
+        s[4 * g] = sv.x; s[4 * g + 1] = sv.y; s[4 * g + 2] = sv.z; s[4 * g + 3] = sv.w;
+        dp[4 * g] = dv.x; dp[4 * g + 1] = dv.y; dp[4 * g + 2] = dv.z; dp[4 * g + 3] = dv.w;
       }
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
