@@ -37,6 +37,7 @@ import os
 import sys
 import time
 from pathlib import Path
+from typing import Any
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -44,7 +45,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "samples/sec (whole node) + DDP scaling efficiency, toy MLP at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse() -> Any:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2048)
@@ -64,7 +65,7 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist(args):
+def setup_dist(args: Any) -> Any:
     import torch
     import torch.distributed as dist
 
@@ -86,7 +87,7 @@ def setup_dist(args):
     return rank, ws, dev
 
 
-def build(args, dev, ws):
+def build(args: Any, dev: Any, ws: Any) -> Any:
     import torch
 
     from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
@@ -101,7 +102,7 @@ def build(args, dev, ws):
     return ds, model, loader
 
 
-def run_fused(args, dev, ws):
+def run_fused(args: Any, dev: Any, ws: Any) -> Any:
     import torch
 
     from distributed_training_amd.engine.fused_mlp import FusedMLPProgram, fused_eligible
@@ -119,10 +120,10 @@ def run_fused(args, dev, ws):
     prog = FusedMLPProgram(model, opt, loader, comm, loss="mse", graph_steps=args.graph_steps,
                            own_tiles=args.own_tiles or None, allreduce_world1=bool(args.allreduce_world1))
 
-    def step_fn(n):
+    def step_fn(n: Any) -> None:
         prog.run_steps(n)
 
-    def finish():
+    def finish() -> Any:
         prog.store_to_module()
         return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
 
@@ -134,7 +135,7 @@ def run_fused(args, dev, ws):
     return step_fn, finish, comm
 
 
-def run_fused_linear(args, dev, ws):
+def run_fused_linear(args: Any, dev: Any, ws: Any) -> Any:
     """The reference's default workload (src/distributed_trainer.py:160-165, 199-200):
     nn.Linear(20, 1), F.cross_entropy on float targets, fp32, SGD, DDP -- on the fused
     Linear step program (csrc/linear_step.hip)."""
@@ -160,10 +161,10 @@ def run_fused_linear(args, dev, ws):
         raise SystemExit(f"fused Linear path not applicable: {why}")
     prog = FusedLinearProgram(model, opt, loader, comm, loss="cross_entropy")
 
-    def step_fn(n):
+    def step_fn(n: Any) -> None:
         prog.run_steps(n)
 
-    def finish():
+    def finish() -> Any:
         prog.store_to_module()
         return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
 
@@ -171,7 +172,7 @@ def run_fused_linear(args, dev, ws):
     return step_fn, finish, comm
 
 
-def run_generic(args, dev, ws):
+def run_generic(args: Any, dev: Any, ws: Any) -> Any:
     import torch
     import torch.nn.functional as F
 
@@ -185,7 +186,7 @@ def run_generic(args, dev, ws):
     opt = FusedSGD(ddp.parameters(), lr=args.lr)
     state = {"it": None, "epoch": 0, "loss": None}
 
-    def next_batch():
+    def next_batch() -> Any:
         while True:
             if state["it"] is None:
                 loader.sampler.set_epoch(state["epoch"])
@@ -196,7 +197,7 @@ def run_generic(args, dev, ws):
                 state["it"] = None
                 state["epoch"] += 1
 
-    def step_fn(n):
+    def step_fn(n: Any) -> None:
         for _ in range(n):
             x, y = next_batch()
             opt.zero_grad()
@@ -207,13 +208,13 @@ def run_generic(args, dev, ws):
             opt.step()
             state["loss"] = loss
 
-    def finish():
+    def finish() -> Any:
         return float(state["loss"].item()) if state["loss"] is not None else float("nan")
 
     return step_fn, finish, comm
 
 
-def run_torch(args, dev, ws):
+def run_torch(args: Any, dev: Any, ws: Any) -> Any:
     """Stock PyTorch-ROCm with the reference's loop (src/distributed_trainer.py:160-183)."""
     import torch
     import torch.nn.functional as F
@@ -234,7 +235,7 @@ def run_torch(args, dev, ws):
     loader = DataLoader(ds, batch_size=args.batch, pin_memory=True, shuffle=False, sampler=sampler)
     state = {"it": None, "epoch": 0, "loss": None}
 
-    def next_batch():
+    def next_batch() -> Any:
         while True:
             if state["it"] is None:
                 sampler.set_epoch(state["epoch"])
@@ -245,7 +246,7 @@ def run_torch(args, dev, ws):
                 state["it"] = None
                 state["epoch"] += 1
 
-    def step_fn(n):
+    def step_fn(n: Any) -> None:
         for _ in range(n):
             x, y = next_batch()
             x = x.to(dev)
@@ -261,13 +262,13 @@ def run_torch(args, dev, ws):
             opt.step()
             state["loss"] = loss
 
-    def finish():
+    def finish() -> Any:
         return float(state["loss"].item()) if state["loss"] is not None else float("nan")
 
     return step_fn, finish, None
 
 
-def main():
+def main() -> None:
     args = parse()
     import torch
     import torch.distributed as dist
@@ -280,13 +281,13 @@ def main():
         runner = run_fused_linear
     step_fn, finish, comm = runner(args, dev, ws)
 
-    def dbarrier():
+    def dbarrier() -> None:
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[dev.index])
         else:
             dist.barrier()
 
-    def barrier():
+    def barrier() -> None:
         torch.cuda.synchronize(dev)
         if ws > 1:  # (one rank: the synchronize is the whole bracket; a second one is host time in the timed region)
             dbarrier()
@@ -299,7 +300,7 @@ def main():
     # torch.distributed.barrier's host-side launch and bookkeeping in the timed region.
     fast = getattr(comm, "barrier", None) if ws > 1 and comm is not None else None
 
-    def end_barrier():
+    def end_barrier() -> None:
         if fast is None:
             barrier()
             return

@@ -20,6 +20,10 @@ import os
 import sys
 import time
 from pathlib import Path
+from typing import TYPE_CHECKING, Any, Optional
+
+if TYPE_CHECKING:
+    import torch
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -27,7 +31,7 @@ sys.path.insert(0, str(ROOT))
 PEAK_BF16 = 2.5e15  # dense bf16 MFMA peak per MI355X
 
 
-def parse():
+def parse() -> Any:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--model", default="gpt2", choices=["gpt2", "llama3_8b", "llama_1b", "llama_tiny"])
@@ -52,7 +56,7 @@ def parse():
     return ap.parse_args()
 
 
-def model_cfg(name, layers):
+def model_cfg(name: str, layers: Any) -> Any:
     from distributed_training_amd.models.gpt2 import GPT2Config
     from distributed_training_amd.models.llama import LlamaConfig
 
@@ -70,7 +74,7 @@ def model_cfg(name, layers):
     return c
 
 
-def main():
+def main() -> None:
     args = parse()
     if args.tunableop:
         os.environ.setdefault("PYTORCH_TUNABLEOP_ENABLED", "1")
@@ -130,7 +134,7 @@ def main():
         opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
         overlap_opt = args.strategy == "ddp" and args.overlap_opt and wrapped.overlap_optimizer(opt)
 
-        def loss_fn(logits, y):
+        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> Any:
             return lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
     else:
         import torch.nn.functional as F
@@ -153,7 +157,7 @@ def main():
                             mixed_precision=MixedPrecision(param_dtype=torch.bfloat16, reduce_dtype=torch.bfloat16))
         opt = torch.optim.AdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
 
-        def loss_fn(logits, y):
+        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> Any:
             return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), y.reshape(-1))
 
     nb = data.shape[0] // args.batch
@@ -161,7 +165,7 @@ def main():
 
     from distributed_training_amd.utils import profiling as prof
 
-    def step():
+    def step() -> None:
         prof.push("step")
         i = state["i"] % nb
         state["i"] += 1
@@ -192,7 +196,7 @@ def main():
         # its construction runs 3 eager warm-up steps and the capture (untimed, before the warm-up below)
         from distributed_training_amd.engine.step_graph import GraphedStep
 
-        def gstep(xb):
+        def gstep(xb: Any) -> Any:
             opt.zero_grad(set_to_none=True)
             loss = wrapped(xb[:, :-1], xb[:, 1:])
             loss.backward()
@@ -205,18 +209,18 @@ def main():
             graphed = None
 
     if graphed is not None:
-        def step():  # noqa: F811 - the graph replay replaces the eager step
+        def step() -> None:  # noqa: F811 - the graph replay replaces the eager step
             i = state["i"] % nb
             state["i"] += 1
             state["loss"] = graphed(data[i * args.batch:(i + 1) * args.batch])
 
-    def dbarrier():
+    def dbarrier() -> None:
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[local])
         else:
             dist.barrier()
 
-    def barrier():
+    def barrier() -> None:
         torch.cuda.synchronize(dev)
         if ws > 1:
             dbarrier()
@@ -291,34 +295,35 @@ def main():
         dist.destroy_process_group()
 
 
-def _patch_torch_ops():
+def _patch_torch_ops() -> None:
     """Route the models' op calls to stock PyTorch (for the baseline)."""
     import torch
     import torch.nn.functional as F
 
     from distributed_training_amd.ops import lm
 
-    def attention(q, k, v, causal=True, scale=None):
+    def attention(q: torch.Tensor, k: torch.Tensor, v: Any, causal: bool = True, scale: Optional[float] = None) -> Any:
         H, Hkv = q.shape[2], k.shape[2]
         qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
         return F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale,
                                               enable_gqa=H != Hkv).transpose(1, 2)
 
-    def attention_packed(qkv, n_head, n_kv_head, causal=True, scale=None, rope=None):
+    def attention_packed(qkv: torch.Tensor, n_head: Any, n_kv_head: Any, causal: bool = True,
+                         scale: Optional[float] = None, rope: Any = None) -> Any:
         q, k, v = lm._split_qkv(qkv, n_head, n_kv_head)
         if rope is not None:
             q, k = lm.rope_reference(q, *rope), lm.rope_reference(k, *rope)
         return attention(q, k, v, causal, scale)
 
-    def add_ln(x, res, w, b, eps=1e-5):
+    def add_ln(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
         xn = x + res
         return xn, F.layer_norm(xn, (xn.shape[-1],), w, b, eps)
 
-    def add_rms(x, res, w, eps=1e-5):
+    def add_rms(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
         xn = x + res
         return xn, F.rms_norm(xn, (xn.shape[-1],), w, eps)
 
-    def linear_ce(x, w, target, ignore_index=-100):
+    def linear_ce(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
         logits = F.linear(x, w)
         return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1),
                                ignore_index=ignore_index)

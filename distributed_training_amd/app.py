@@ -8,7 +8,7 @@ reference flow and log lines (``"Training failed: ..."`` then re-raise;
 from __future__ import annotations
 
 import logging
-from typing import Tuple
+from typing import Any, Tuple
 
 import torch
 from torch.utils.data import Dataset
@@ -22,7 +22,7 @@ from .utils.logging_utils import setup_logging
 logger = logging.getLogger("distributed_training_amd.trainer")
 
 
-def _get(node, key, default=None):
+def _get(node: Any, key: str, default: Any = None) -> Any:
     if node is None:
         return default
     if hasattr(node, "get"):
@@ -30,7 +30,7 @@ def _get(node, key, default=None):
     return getattr(node, key, default)
 
 
-def build_model(cfg_model) -> torch.nn.Module:
+def build_model(cfg_model: Any) -> torch.nn.Module:
     name = str(_get(cfg_model, "name", "") or "")
     if name in ("gpt2", "gpt2_small"):
         from .models.gpt2 import GPT2, GPT2Config
@@ -45,7 +45,7 @@ def build_model(cfg_model) -> torch.nn.Module:
     return build_mlp(cfg_model)
 
 
-def build_optimizer(cfg_train, params):
+def build_optimizer(cfg_train: Any, params: Any) -> Any:
     from .ops.optim import build_optimizer as _b
 
     name = str(_get(cfg_train, "optimizer", "sgd"))
@@ -57,7 +57,7 @@ def build_optimizer(cfg_train, params):
     return _b(name, params, lr=lr, betas=betas, weight_decay=wd)
 
 
-def load_train_objs(cfg) -> Tuple[Dataset, torch.nn.Module, torch.optim.Optimizer]:
+def load_train_objs(cfg: Any) -> Tuple[Dataset, torch.nn.Module, torch.optim.Optimizer]:
     seed = _get(cfg.train, "seed", None)
     if seed is not None:
         torch.manual_seed(int(seed))
@@ -76,7 +76,7 @@ def prepare_dataloader(dataset: Dataset, batch_size: int) -> DeviceDataLoader:
     return DeviceDataLoader(dataset, batch_size=batch_size, sampler=DistributedSampler(dataset))
 
 
-def _wrap_policy(name, model):
+def _wrap_policy(name: str, model: Any) -> Any:
     if not name:
         return None
     if name == "block":  # blocks + the model's extra units (Llama: embedding, output head)
@@ -90,14 +90,14 @@ def _wrap_policy(name, model):
     return None
 
 
-def _mb(v):
+def _mb(v: Any) -> Any:
     """Bucket size knob: a number of MiB, or "auto" / None (derived for xGMI)."""
     if v is None or str(v).lower() in ("auto", "none", "null"):
         return None if v is None or str(v).lower() in ("none", "null") else "auto"
     return float(v)
 
 
-def training_config_from(cfg, model=None) -> TrainingConfig:
+def training_config_from(cfg: Any, model: Any = None) -> TrainingConfig:
     t = cfg.train
     return TrainingConfig(
         max_epochs=t.total_epochs,
@@ -125,7 +125,7 @@ def training_config_from(cfg, model=None) -> TrainingConfig:
     )
 
 
-def run(cfg) -> Trainer:
+def run(cfg: Any) -> Trainer:
     """Main training entry point (reference ``main`` body)."""
     env = None
     try:

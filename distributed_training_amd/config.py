@@ -36,27 +36,27 @@ class ConfigError(ValueError):
 class ConfigNode(dict):
     """dict with attribute access; nested dicts are ConfigNodes."""
 
-    def __init__(self, *args, **kwargs) -> None:
+    def __init__(self, *args: Any, **kwargs: Any) -> None:
         super().__init__()
         for k, v in dict(*args, **kwargs).items():
             self[k] = v
 
-    def __setitem__(self, key, value) -> None:
+    def __setitem__(self, key: Any, value: Any) -> None:
         super().__setitem__(key, _wrap(value))
 
-    def __getattr__(self, item):
+    def __getattr__(self, item: str) -> Any:
         try:
             return self[item]
         except KeyError as e:
             raise AttributeError(f"config has no key {item!r} (keys: {list(self.keys())})") from e
 
-    def __setattr__(self, key, value) -> None:
+    def __setattr__(self, key: str, value: Any) -> None:
         self[key] = value
 
-    def __delattr__(self, item) -> None:
+    def __delattr__(self, item: str) -> None:
         del self[item]
 
-    def __deepcopy__(self, memo):
+    def __deepcopy__(self, memo: Any) -> Any:
         return ConfigNode({k: copy.deepcopy(v, memo) for k, v in self.items()})
 
     def to_dict(self) -> dict:
@@ -77,7 +77,7 @@ class ConfigNode(dict):
         return yaml.safe_dump(self.to_dict(), sort_keys=False)
 
 
-def _wrap(v):
+def _wrap(v: Any) -> Any:
     if isinstance(v, ConfigNode):
         return v
     if isinstance(v, dict):
@@ -124,7 +124,7 @@ class Override:
     def __init__(self, key: str, value: Any, op: str) -> None:
         self.key, self.value, self.op = key, value, op
 
-    def __repr__(self):
+    def __repr__(self) -> str:
         return f"Override({self.op}{self.key}={self.value!r})"
 
 
@@ -354,13 +354,13 @@ def prepare_run_dir(cfg: ConfigNode) -> Path:
     return out
 
 
-def main_decorator(config_path: str, config_name: str, version_base=None) -> Callable:
+def main_decorator(config_path: str, config_name: str, version_base: Optional[str] = None) -> Callable:
     """Drop-in for ``@hydra.main``: composes the config from ``sys.argv`` and
     calls the task function with it."""
 
-    def deco(fn: Callable[[ConfigNode], Any]):
+    def deco(fn: Callable[[ConfigNode], Any]) -> Any:
         @functools.wraps(fn)
-        def wrapper(cfg_passthrough: Optional[ConfigNode] = None, argv: Optional[Sequence[str]] = None):
+        def wrapper(cfg_passthrough: Optional[ConfigNode] = None, argv: Optional[Sequence[str]] = None) -> Any:
             if cfg_passthrough is not None:
                 return fn(cfg_passthrough)
             src = Path(sys.modules[fn.__module__].__file__).resolve().parent

@@ -15,7 +15,7 @@ copies, no host round trip.
 from __future__ import annotations
 
 import math
-from typing import Iterator, Optional, Tuple
+from typing import Any, Iterator, Optional, Tuple
 
 import torch
 from torch.utils.data import Dataset
@@ -51,7 +51,7 @@ class MyTrainDataset(Dataset):
                 self.Y[i] = torch.rand(output_size, generator=gen)
 
     @property
-    def data(self):
+    def data(self) -> Any:
         return list(zip(self.X, self.Y))
 
     def __len__(self) -> int:
@@ -74,7 +74,7 @@ class SyntheticTokens(Dataset):
     def __len__(self) -> int:
         return self.tokens.shape[0]
 
-    def __getitem__(self, i: int):
+    def __getitem__(self, i: int) -> Any:
         t = self.tokens[i]
         return t[:-1], t[1:]
 
@@ -86,7 +86,7 @@ class DeviceDataLoader:
     sampler=sampler, drop_last=drop_last)`` would, already on ``device``.
     """
 
-    def __init__(self, dataset, batch_size: int, sampler: Optional[DistributedSampler] = None,
+    def __init__(self, dataset: Any, batch_size: int, sampler: Optional[DistributedSampler] = None,
                  device: Optional[torch.device] = None, drop_last: bool = False) -> None:
         self.dataset = dataset
         self.batch_size = int(batch_size)
@@ -96,7 +96,7 @@ class DeviceDataLoader:
         self.pin_memory = False
         self._tensors = None
 
-    def to(self, device) -> "DeviceDataLoader":
+    def to(self, device: Any) -> "DeviceDataLoader":
         self.device = torch.device(device)
         self._tensors = None
         return self

@@ -31,7 +31,7 @@ logger = logging.getLogger("distributed_training_amd.trainer")
 class ModelCheckpoint:
     """Handles model checkpointing operations."""
 
-    def __init__(self, path: Path, env, strategy, save_optimizer: bool = False) -> None:
+    def __init__(self, path: Path, env: Any, strategy: Any, save_optimizer: bool = False) -> None:
         self.path = Path(path)
         self.env = env
         self.strategy = strategy

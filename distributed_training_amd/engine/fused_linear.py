@@ -20,7 +20,7 @@ order exactly (indices uploaded per epoch into a device ring).
 from __future__ import annotations
 
 import logging
-from typing import List, Optional
+from typing import Any, List, Optional
 
 import torch
 import torch.nn as nn
@@ -32,7 +32,7 @@ logger = logging.getLogger(__name__)
 LOSS_KINDS = {"mse": 0, "cross_entropy": 1}
 
 
-def linear_eligible(module: nn.Module, optimizer, loader, loss: str, device: torch.device) -> Optional[str]:
+def linear_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, device: torch.device) -> Optional[str]:
     """None when the fused Linear program applies, else the reason it does not."""
     from ..data.datasets import DeviceDataLoader
 
@@ -60,7 +60,7 @@ def linear_eligible(module: nn.Module, optimizer, loader, loss: str, device: tor
 
 
 class FusedLinearProgram:
-    def __init__(self, module: nn.Linear, optimizer, loader, comm, loss: str = "cross_entropy",
+    def __init__(self, module: nn.Linear, optimizer: Any, loader: Any, comm: Any, loss: str = "cross_entropy",
                  loss_len: int = 4096) -> None:
         self.module = module
         self.opt = optimizer
@@ -97,13 +97,13 @@ class FusedLinearProgram:
         self.load_from_module()
 
     # ------------------------------------------------------------ state sync
-    def hyper(self):
+    def hyper(self) -> Any:
         g = self.opt.param_groups[0]
         return {"lr": g["lr"], "momentum": g.get("momentum", 0.0), "dampening": g.get("dampening", 0.0),
                 "weight_decay": g.get("weight_decay", 0.0), "nesterov": bool(g.get("nesterov", False)),
                 "maximize": bool(g.get("maximize", False))}
 
-    def _views(self):
+    def _views(self) -> Any:
         C, I = self.C, self.I
         return {"weight": self.P[:C * I].view(C, I), "bias": self.P[C * I:]}
 

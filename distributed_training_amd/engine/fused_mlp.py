@@ -24,7 +24,7 @@ import logging
 import os
 import sys
 import time
-from typing import Dict, List, Optional
+from typing import Any, Dict, List, Optional
 
 import torch
 import torch.nn as nn
@@ -36,7 +36,7 @@ logger = logging.getLogger(__name__)
 _TRACE = bool(os.environ.get("DTA_BENCH_TRACE"))
 
 
-def fused_eligible(module: nn.Module, optimizer, loader, loss: str, device: torch.device) -> Optional[str]:
+def fused_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, device: torch.device) -> Optional[str]:
     """Return None when the fused program applies, else the reason it does not."""
     from ..data.datasets import DeviceDataLoader
     from ..models.mlp import MLP
@@ -79,7 +79,7 @@ class FusedMLPProgram:
     (``DTA_MLP_XMODE=auto``, the default; or force oneshot / rsag / step).
     """
 
-    def __init__(self, module, optimizer, loader, comm, loss: str = "mse", graph_steps: int = 32,
+    def __init__(self, module: Any, optimizer: Any, loader: Any, comm: Any, loss: str = "mse", graph_steps: int = 32,
                  own_tiles: Optional[int] = None, allreduce_world1: bool = True, loss_len: int = 4096,
                  persistent: Optional[bool] = None) -> None:
         self.module = module

@@ -92,7 +92,7 @@ def lm_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
 class Trainer:
     """Manages the training process in a distributed environment."""
 
-    def __init__(self, model: torch.nn.Module, train_data, optimizer: torch.optim.Optimizer,
+    def __init__(self, model: torch.nn.Module, train_data: Any, optimizer: torch.optim.Optimizer,
                  config: TrainingConfig, env: DistributedEnvironment) -> None:
         self.env = env
         self.config = config
@@ -146,7 +146,7 @@ class Trainer:
         model, self.epochs_run = self.checkpoint.load(model, device, self.optimizer)
         return model
 
-    def _rebind_optimizer(self, model: torch.nn.Module, original_params) -> None:
+    def _rebind_optimizer(self, model: torch.nn.Module, original_params: Any) -> None:
         """FSDP replaces the parameters by shards: rebuild the optimizer over
         them (same class and hyper-parameters).  Torch optimizers over GPU
         parameters become the fused HIP optimizers."""

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
+from typing import Any, Optional
 
 import torch
 import torch.nn as nn
@@ -37,7 +38,7 @@ class GPT2Config:
         return (self.vocab_size + 63) // 64 * 64
 
     @staticmethod
-    def from_cfg(c) -> "GPT2Config":
+    def from_cfg(c: Any) -> "GPT2Config":
         g = c.get if hasattr(c, "get") else (lambda k, d=None: getattr(c, k, d))
         return GPT2Config(int(g("n_layer", 12)), int(g("n_head", 12)), int(g("n_embd", 768)),
                           int(g("vocab_size", 50257)), int(g("block_size", 1024)), float(g("dropout", 0.0) or 0.0),
@@ -51,10 +52,10 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(n))
         self.eps = eps
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         return lm.layer_norm(x, self.weight, self.bias, self.eps)
 
-    def add_forward(self, x, res):
+    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Any:
         """``(x + res, LN(x + res))`` in one kernel; ``res=None`` -> ``(x, LN(x))``."""
         if res is None:
             return x, self(x)
@@ -68,7 +69,7 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = lm.Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = lm.Linear(cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         B, S, C = x.shape
         # q/k/v are read in place from the projection output; dq/dk/dv land in one packed buffer
         y = lm.attention_packed(self.c_attn(x), self.n_head, self.n_head, causal=True)
@@ -81,7 +82,7 @@ class MLP(nn.Module):
         self.c_fc = lm.Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         # c_proj(gelu(c_fc(x))): the GELU in c_fc's GEMM epilogue (pre-activation and activation stored
         # in one pass), its backward folded into c_proj's input-gradient GEMM
         h, a = lm.linear_gelu(x, self.c_fc.weight, self.c_fc.bias)
@@ -96,7 +97,7 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd)
         self.mlp = MLP(cfg)
 
-    def forward(self, x, h=None):
+    def forward(self, x: torch.Tensor, h: Optional[torch.Tensor] = None) -> Any:
         """``h``: the previous block's MLP output, not yet added to the
         residual stream -- the add is fused into this block's ln_1 (and this
         block's MLP output is handed on the same way), so no residual add runs
@@ -128,7 +129,7 @@ class GPT2(nn.Module):
                 nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * cfg.n_layer))
 
     @staticmethod
-    def _init(m) -> None:
+    def _init(m: Any) -> None:
         if isinstance(m, nn.Linear):
             nn.init.normal_(m.weight, 0.0, 0.02)
             if m.bias is not None:
@@ -142,7 +143,7 @@ class GPT2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx, targets=None):
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
         """Logits ``[B, S, V]``; with ``targets``, the mean token cross-entropy
         (LM head and loss fused: the logits are never materialised twice)."""
         B, S = idx.shape

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
+from typing import Any, Optional
 
 import torch
 import torch.nn as nn
@@ -32,7 +33,7 @@ class LlamaConfig:
     tie_weights: bool = False
 
     @staticmethod
-    def from_cfg(c) -> "LlamaConfig":
+    def from_cfg(c: Any) -> "LlamaConfig":
         g = c.get if hasattr(c, "get") else (lambda k, d=None: getattr(c, k, d))
         return LlamaConfig(int(g("n_layer", 32)), int(g("n_head", 32)), int(g("n_kv_head", 8)),
                            int(g("n_embd", 4096)), int(g("ffn_hidden", 14336)), int(g("vocab_size", 128256)),
@@ -46,10 +47,10 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(n))
         self.eps = eps
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         return lm.rms_norm(x, self.weight, self.eps)
 
-    def add_forward(self, x, res):
+    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Any:
         """``(x + res, RMSNorm(x + res))`` in one kernel; ``res=None`` -> ``(x, RMSNorm(x))``."""
         if res is None:
             return x, self(x)
@@ -64,7 +65,7 @@ class Attention(nn.Module):
         self.wqkv = lm.Linear(cfg.n_embd, (self.H + 2 * self.Hkv) * self.D, bias=False)
         self.wo = lm.Linear(self.H * self.D, cfg.n_embd, bias=False)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
         B, S, _ = x.shape
         # RoPE + GQA attention on the packed projection output (one packed dQKV in backward)
         y = lm.attention_packed(self.wqkv(x), self.H, self.Hkv, causal=True, rope=(cos, sin))
@@ -77,7 +78,7 @@ class FeedForward(nn.Module):
         self.w13 = lm.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
         self.w2 = lm.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         return self.w2(lm.swiglu(self.w13(x)))
 
 
@@ -89,7 +90,7 @@ class Block(nn.Module):
         self.ffn_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
         self.feed_forward = FeedForward(cfg)
 
-    def forward(self, x, cos, sin, h=None):
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, h: Optional[torch.Tensor] = None) -> Any:
         """Residual adds fused into the norms (see GPT-2 ``Block``); returns ``(x, h)``."""
         x, y = self.attention_norm.add_forward(x, h)
         x, y = self.ffn_norm.add_forward(x, self.attention(y, cos, sin))
@@ -122,7 +123,7 @@ class Llama(nn.Module):
     def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 
-    def fsdp_extra_units(self):
+    def fsdp_extra_units(self) -> Any:
         """Modules that are FSDP units of their own besides the blocks (parallel/fsdp.py
         ``lm_wrap_policy``): the embedding and the output head, 525 M parameters each at 8B --
         in the root unit they would be gathered synchronously before the forward and held
@@ -132,7 +133,7 @@ class Llama(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx, targets=None):
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
         """Logits; with ``targets``, the mean token cross-entropy (head + loss fused)."""
         x = self.tok_embeddings(idx)
         cos, sin = self.rope_cos, self.rope_sin

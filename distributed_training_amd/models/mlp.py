@@ -9,7 +9,7 @@ training step has a dedicated fused gfx950 kernel (``ops/mlp_fused.py``).
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Union
+from typing import Any, List, Optional, Sequence, Union
 
 import torch
 import torch.nn as nn
@@ -52,7 +52,7 @@ class MLP(nn.Module):
         return self.num_layers == 2
 
 
-def build_mlp(cfg_model) -> nn.Module:
+def build_mlp(cfg_model: Any) -> nn.Module:
     """``cfg.model`` -> module.  No ``hidden_size`` => the reference's Linear."""
     get = cfg_model.get if hasattr(cfg_model, "get") else (lambda k, d=None: getattr(cfg_model, k, d))
     hidden = get("hidden_size", None)

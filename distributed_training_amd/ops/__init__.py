@@ -33,7 +33,7 @@ def has_native() -> bool:
     return _native is not None
 
 
-def native():
+def native() -> Any:
     """Return the ``_C`` module or raise a descriptive error."""
     _try_import()
     if _native is None:
@@ -48,7 +48,7 @@ def native():
 _rccl_ready = False
 
 
-def ensure_rccl():
+def ensure_rccl() -> Any:
     """Resolve the RCCL API from the librccl.so PyTorch ships (one RCCL runtime
     per process)."""
     global _rccl_ready
@@ -75,7 +75,7 @@ def ensure_rccl():
     raise RuntimeError("could not load librccl: " + "; ".join(errs or ["no candidate found"]))
 
 
-def stream_handle(stream=None) -> int:
+def stream_handle(stream: Any = None) -> int:
     """HIP stream handle for a torch stream (-1 = current torch stream)."""
     if stream is None:
         return -1

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Callable, Dict, Optional, Tuple
+from typing import Any, Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -26,7 +26,7 @@ from torch.autograd import Function
 from . import native
 
 
-def _need_bf16(*ts) -> None:
+def _need_bf16(*ts: Any) -> None:
     for t in ts:
         if t.dtype != torch.bfloat16:
             raise TypeError(f"GPU transformer ops need bf16 tensors (got {t.dtype}); "
@@ -34,7 +34,8 @@ def _need_bf16(*ts) -> None:
 
 
 # ------------------------------------------------------------------ attention
-def attention_reference(q, k, v, causal: bool = True, scale: Optional[float] = None) -> torch.Tensor:
+def attention_reference(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
+                        scale: Optional[float] = None) -> torch.Tensor:
     """[B, S, H, D] / [B, S, Hkv, D] -> [B, S, H, D], fp32 math."""
     B, S, H, D = q.shape
     Hkv = k.shape[2]
@@ -53,21 +54,22 @@ def attention_reference(q, k, v, causal: bool = True, scale: Optional[float] = N
 
 class _FlashAttn(Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
+    def forward(ctx: Any, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool, scale: float) -> Any:
         o, lse = native().attn_fwd(q, k, v, bool(causal), float(scale), -1)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale = causal, scale
         return o
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx: Any, do: torch.Tensor) -> Any:
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
         dq, dk, dv = native().attn_bwd(do, q, k, v, o, lse, bool(ctx.causal), float(ctx.scale), -1)
         return dq, dk, dv, None, None
 
 
-def attention(q, k, v, causal: bool = True, scale: Optional[float] = None) -> torch.Tensor:
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
+              scale: Optional[float] = None) -> torch.Tensor:
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda:
         _need_bf16(q, k, v)
@@ -75,7 +77,7 @@ def attention(q, k, v, causal: bool = True, scale: Optional[float] = None) -> to
     return attention_reference(q, k, v, causal, scale)
 
 
-def _split_qkv(qkv: torch.Tensor, H: int, Hkv: int):
+def _split_qkv(qkv: torch.Tensor, H: int, Hkv: int) -> Any:
     B, S, W = qkv.shape
     D = W // (H + 2 * Hkv)
     t = qkv.view(B, S, H + 2 * Hkv, D)
@@ -90,7 +92,8 @@ class _PackedAttn(Function):
     slice gradients into the projection output's gradient."""
 
     @staticmethod
-    def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin):
+    def forward(ctx: Any, qkv: torch.Tensor, H: int, Hkv: int, causal: bool, scale: float, cos: torch.Tensor,
+                sin: torch.Tensor) -> Any:
         B, S, W = qkv.shape
         D = W // (H + 2 * Hkv)
         if cos is not None:
@@ -103,7 +106,7 @@ class _PackedAttn(Function):
         return o
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx: Any, do: torch.Tensor) -> Any:
         qkv, o, lse, cos, sin = ctx.saved_tensors
         H, Hkv, causal, scale, has_rope = ctx.cfg
         B, S, W = qkv.shape
@@ -117,7 +120,7 @@ class _PackedAttn(Function):
         return dqkv, None, None, None, None, None, None
 
 
-def attention_packed(qkv, n_head: int, n_kv_head: int, causal: bool = True, scale: Optional[float] = None,
+def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: bool = True, scale: Optional[float] = None,
                      rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """``qkv`` [B, S, (H + 2 Hkv) D] -> attention output [B, S, H, D] (RoPE on q, k if given)."""
     B, S, W = qkv.shape
@@ -138,7 +141,7 @@ def attention_packed(qkv, n_head: int, n_kv_head: int, causal: bool = True, scal
 # ------------------------------------------------------------------ norms
 class _Norm(Function):
     @staticmethod
-    def forward(ctx, x, w, b, rms, eps):
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool, eps: float) -> Any:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, mean, rstd, _ = native().norm_fwd(x2, w.contiguous(), None if rms else b.contiguous(), rms, eps, -1)
@@ -148,7 +151,7 @@ class _Norm(Function):
         return y.view(shape)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         x2, w, mean, rstd = ctx.saved_tensors
         pw, pb = ctx.params
         dx, dw, db = native().norm_bwd(dy.reshape(x2.shape).contiguous(), x2, w.contiguous(), mean, rstd, ctx.rms,
@@ -162,7 +165,8 @@ class _AddNorm(Function):
     residual-stream gradient of x_new inside the norm-backward kernel."""
 
     @staticmethod
-    def forward(ctx, x, res, w, b, rms, eps):
+    def forward(ctx: Any, x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool,
+                eps: float) -> Any:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, mean, rstd, xsum = native().norm_fwd(x2, w.contiguous(), None if rms else b.contiguous(), rms, eps, -1,
@@ -173,7 +177,7 @@ class _AddNorm(Function):
         return xsum.view(shape), y.view(shape)
 
     @staticmethod
-    def backward(ctx, g_x, g_y):
+    def backward(ctx: Any, g_x: torch.Tensor, g_y: torch.Tensor) -> Any:
         xsum, w, mean, rstd = ctx.saved_tensors
         if g_y is None:
             return g_x, g_x, None, None, None, None
@@ -186,7 +190,7 @@ class _AddNorm(Function):
         return dx, dx, dw, (None if ctx.rms else db), None, None
 
 
-def add_layer_norm(x, res, w, b, eps: float = 1e-5):
+def add_layer_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
     """Returns ``(x + res, layer_norm(x + res))``."""
     if x.is_cuda:
         _need_bf16(x, res, w, b)
@@ -195,7 +199,7 @@ def add_layer_norm(x, res, w, b, eps: float = 1e-5):
     return xn, F.layer_norm(xn, (xn.shape[-1],), w, b, eps)
 
 
-def add_rms_norm(x, res, w, eps: float = 1e-5):
+def add_rms_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
     """Returns ``(x + res, rms_norm(x + res))``."""
     if x.is_cuda:
         _need_bf16(x, res, w)
@@ -204,14 +208,14 @@ def add_rms_norm(x, res, w, eps: float = 1e-5):
     return xn, rms_norm(xn, w, eps)
 
 
-def layer_norm(x, w, b, eps: float = 1e-5):
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
     if x.is_cuda:
         _need_bf16(x, w, b)
         return _Norm.apply(x, w, b, False, eps)
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
-def rms_norm(x, w, eps: float = 1e-5):
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
     if x.is_cuda:
         _need_bf16(x, w)
         return _Norm.apply(x, w, None, True, eps)
@@ -336,14 +340,16 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
     return c
 
 
-def _run_gemm(impl: int, a, b, a_t: bool, b_t: bool, out=None, alpha: float = 1.0, bias=None):
+def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
+              alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> Any:
     C = native()
     if impl >= K64:
         return C.gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
     return C.gemm(a, b, a_t, b_t, out, False, alpha, bias, 0, None, impl)
 
 
-def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias=None, out=None) -> bool:
+def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> bool:
     return (a.stride(-1) == 1 and b.stride(-1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous())
             and (out is None or (out.is_contiguous() and out.data_ptr() % 16 == 0)))
@@ -356,7 +362,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
 
-    def run_torch():
+    def run_torch() -> Any:
         A = a.t() if a_t else a
         B = b if b_t else b.t()
         if bias is not None and alpha == 1.0:
@@ -388,11 +394,11 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     N = w.shape[0]
     C = native()
 
-    def run_torch():
+    def run_torch() -> Any:
         h = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
         return h, C.gelu_fwd(h, -1)
 
-    def run_k64(t):
+    def run_k64(t: int) -> Any:
         h = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
         return tuple(C.gemm64(x2, w, False, False, h, torch.empty_like(h), False, 1.0, b, 2, None, t))
 
@@ -603,7 +609,7 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
 
 
 def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
-                 b: Optional[torch.Tensor] = None):
+                 b: Optional[torch.Tensor] = None) -> Any:
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
     Small outputs with a long token reduction (GPT-2: 768 x 768 .. 3072 x 768
     over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip), which fills
@@ -669,7 +675,7 @@ class _Linear(Function):
     kernel or :func:`gemm` (see _weight_grad)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> Any:
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)  # the Parameters themselves (their .grad decides a direct write)
@@ -679,7 +685,7 @@ class _Linear(Function):
         return gemm(x2, w, bias=b, kind="fwd").view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         x, w = ctx.saved_tensors
         pw, pb = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -707,12 +713,12 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and h2.is_contiguous()
           and h2.data_ptr() % 16 == 0 and N % 8 == 0)
 
-    def run(impl):
+    def run(impl: Any) -> Any:
         if impl >= K64:
             return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
         return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, impl)
 
-    def run_torch():
+    def run_torch() -> Any:
         return C.gelu_bwd(torch.mm(dy2, w), h2, -1)
 
     impl = 0
@@ -734,7 +740,7 @@ class _GeluLinear(Function):
     :func:`_dgelu_dgrad` (the GELU backward folded into the input-gradient GEMM)."""
 
     @staticmethod
-    def forward(ctx, h, w, b, a=None):
+    def forward(ctx: Any, h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, a: Optional[torch.Tensor] = None) -> Any:
         hc = h.contiguous()
         if a is None:
             a = native().gelu_fwd(hc, -1)
@@ -747,7 +753,7 @@ class _GeluLinear(Function):
         return gemm(a2, w, bias=b, kind="fwd").view(*h.shape[:-1], w.shape[0])
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         h, a, w = ctx.saved_tensors
         pw, pb = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -773,7 +779,7 @@ class _LinearGelu(Function):
     and backward is exactly :class:`_Linear`'s."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> Any:
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)
@@ -787,11 +793,11 @@ class _LinearGelu(Function):
         return h, a
 
     @staticmethod
-    def backward(ctx, dh, da):
+    def backward(ctx: Any, dh: torch.Tensor, da: torch.Tensor) -> Any:
         return _Linear.backward(ctx, dh)
 
 
-def linear_gelu(x, w, b=None):
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> Any:
     """``(h, gelu(h))`` for ``h = linear(x, w, b)``; feed both to :func:`gelu_linear` (``a=``)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
@@ -800,7 +806,8 @@ def linear_gelu(x, w, b=None):
     return h, gelu(h).detach()
 
 
-def gelu_linear(h, w, b=None, a=None):
+def gelu_linear(h: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+                a: Optional[torch.Tensor] = None) -> Any:
     """``linear(gelu(h), w, b)`` with the GELU backward fused into the input-gradient GEMM on GPU;
     ``a``: gelu(h) already computed (by :func:`linear_gelu`'s epilogue)."""
     if h.is_cuda and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
@@ -809,7 +816,7 @@ def gelu_linear(h, w, b=None, a=None):
     return linear(gelu(h), w, b)
 
 
-def linear(x, w, b=None):
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> Any:
     if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
         return _Linear.apply(x, w, b)
@@ -819,7 +826,7 @@ def linear(x, w, b=None):
 class Linear(torch.nn.Linear):
     """``nn.Linear`` (same parameters / state-dict keys) routed through :func:`linear`."""
 
-    def forward(self, x):
+    def forward(self, x: torch.Tensor) -> Any:
         return linear(x, self.weight, self.bias)
 
 
@@ -831,7 +838,7 @@ class LMHead(torch.nn.Linear):
     last blocks, its gradient reduce-scattered as soon as the head's backward -- the first of
     the backward -- is done."""
 
-    def forward(self, y, targets=None):
+    def forward(self, y: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
         if targets is not None:
             return linear_cross_entropy(y, self.weight, targets)
         return linear(y, self.weight, self.bias)
@@ -843,25 +850,25 @@ class Embedding(torch.nn.Embedding):
 
     fsdp_backward_needs_params = False
 
-    def forward(self, idx):
+    def forward(self, idx: torch.Tensor) -> Any:
         return embedding(idx, self.weight)
 
 
 # ------------------------------------------------------------------ activations
 class _Gelu(Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx: Any, x: torch.Tensor) -> Any:
         xc = x.contiguous()
         ctx.save_for_backward(xc)
         return native().gelu_fwd(xc, -1)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         (x,) = ctx.saved_tensors
         return native().gelu_bwd(dy.contiguous(), x, -1)
 
 
-def gelu(x):
+def gelu(x: torch.Tensor) -> Any:
     if x.is_cuda:
         _need_bf16(x)
         return _Gelu.apply(x)
@@ -870,18 +877,18 @@ def gelu(x):
 
 class _SwiGLU(Function):
     @staticmethod
-    def forward(ctx, ab):
+    def forward(ctx: Any, ab: torch.Tensor) -> Any:
         abc = ab.contiguous()
         ctx.save_for_backward(abc)
         return native().swiglu_fwd(abc, -1)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         (ab,) = ctx.saved_tensors
         return native().swiglu_bwd(dy.contiguous(), ab, -1)
 
 
-def swiglu(ab):
+def swiglu(ab: torch.Tensor) -> Any:
     """``silu(a) * b`` for ``ab = [a | b]`` along the last dim."""
     if ab.is_cuda:
         _need_bf16(ab)
@@ -891,14 +898,15 @@ def swiglu(ab):
 
 
 # ------------------------------------------------------------------ rotary
-def rope_tables(seq_len: int, head_dim: int, theta: float = 10000.0, device=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def rope_tables(seq_len: int, head_dim: int, theta: float = 10000.0,
+                device: Any = None) -> Tuple[torch.Tensor, torch.Tensor]:
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
     t = torch.arange(seq_len, dtype=torch.float64)
     f = torch.outer(t, inv)
     return f.cos().float().to(device), f.sin().float().to(device)
 
 
-def rope_reference(x, cos, sin):
+def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
     S, D = x.shape[1], x.shape[-1]
     c = cos[:S].view(1, S, 1, D // 2).to(torch.float32)
     s = sin[:S].view(1, S, 1, D // 2).to(torch.float32)
@@ -908,21 +916,21 @@ def rope_reference(x, cos, sin):
 
 class _Rope(Function):
     @staticmethod
-    def forward(ctx, x, cos, sin):
+    def forward(ctx: Any, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
         y = x.contiguous().clone()
         native().rope_(y, cos, sin, False, -1)
         ctx.save_for_backward(cos, sin)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         cos, sin = ctx.saved_tensors
         dx = dy.contiguous().clone()
         native().rope_(dx, cos, sin, True, -1)
         return dx, None, None
 
 
-def apply_rope(x, cos, sin):
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
     """Rotate-half RoPE on [B, S, heads, D]."""
     if x.is_cuda:
         _need_bf16(x)
@@ -966,13 +974,13 @@ class _Embedding(Function):
     bucket copy of the sum."""
 
     @staticmethod
-    def forward(ctx, idx, w):
+    def forward(ctx: Any, idx: torch.Tensor, w: torch.Tensor) -> Any:
         ctx.save_for_backward(idx)
         ctx.wparam = w
         return F.embedding(idx, w)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx: Any, dy: torch.Tensor) -> Any:
         (idx,) = ctx.saved_tensors
         w = ctx.wparam
         if not ctx.needs_input_grad[1]:
@@ -1005,7 +1013,7 @@ def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------ loss
 class _CrossEntropy(Function):
     @staticmethod
-    def forward(ctx, logits, target, ignore_index):
+    def forward(ctx: Any, logits: torch.Tensor, target: torch.Tensor, ignore_index: int) -> Any:
         # no host sync: the valid-token count stays on the device
         count = (target != ignore_index).sum().clamp_min(1).float()
         dlogits = torch.empty_like(logits)
@@ -1014,7 +1022,7 @@ class _CrossEntropy(Function):
         return loss_rows.sum() / count
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx: Any, g: torch.Tensor) -> Any:
         dlogits, count = ctx.saved_tensors
         return dlogits * (g / count).to(dlogits.dtype), None, None
 
@@ -1028,7 +1036,7 @@ class _LinearCrossEntropy(Function):
     pass over it."""
 
     @staticmethod
-    def forward(ctx, x, w, target, ignore_index):
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int) -> Any:
         x2 = x.reshape(-1, x.shape[-1])
         logits = gemm(x2, w, kind="head_fwd")
         count = (target != ignore_index).sum().clamp_min(1).float()
@@ -1039,7 +1047,7 @@ class _LinearCrossEntropy(Function):
         return loss_rows.sum() / count
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx: Any, g: torch.Tensor) -> Any:
         x2, w, dlogits, count = ctx.saved_tensors
         s = (g / count).to(dlogits.dtype)  # stays on the device (no host sync in backward)
         dx = dw = None
@@ -1052,7 +1060,7 @@ class _LinearCrossEntropy(Function):
         return dx, dw, None, None
 
 
-def linear_cross_entropy(x, w, target, ignore_index: int = -100):
+def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
     """Mean token cross-entropy of ``x @ w.T`` against ``target`` (the LM head + loss)."""
     if x.is_cuda:
         _need_bf16(x, w)
@@ -1061,7 +1069,7 @@ def linear_cross_entropy(x, w, target, ignore_index: int = -100):
     return F.cross_entropy(logits.float(), target.reshape(-1), ignore_index=ignore_index)
 
 
-def cross_entropy(logits, target, ignore_index: int = -100):
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
     """Mean token cross-entropy over ``logits [N, V]`` (fused fwd+bwd kernel on GPU)."""
     if logits.is_cuda:
         _need_bf16(logits)

@@ -11,7 +11,7 @@ Names match ``nn.Linear`` state-dict order of the MLP model
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, Optional, Tuple
+from typing import Any, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -41,7 +41,7 @@ class MlpLayout:
     total: int
 
     @property
-    def offsets(self):
+    def offsets(self) -> Any:
         return [self.o_w1, self.o_b1, self.o_w2, self.o_b2]
 
     def views(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
@@ -110,9 +110,11 @@ def pad_features(X: torch.Tensor) -> torch.Tensor:
     return Xp
 
 
-def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout: MlpLayout,
+def persistent_steps(Xp: torch.Tensor, T: torch.Tensor, idx_ring: torch.Tensor, cursor: torch.Tensor,
+                     loss_ring: torch.Tensor, loss_cursor: torch.Tensor, mom_started: torch.Tensor, P: torch.Tensor,
+                     M: torch.Tensor, layout: MlpLayout,
                      batch: int, nsteps: int, act: str, loss: str, grad_scale: float, sgd: Dict[str, float],
-                     stream=None, dbg=None, dbg_step: int = 0, xinfo=None) -> None:
+                     stream: Any = None, dbg: Any = None, dbg_step: int = 0, xinfo: Any = None) -> None:
     """``nsteps`` complete training steps (gather, forward, loss, backward, SGD) in ONE launch.
     ``xinfo`` (from :func:`exchange_info`): DDP gradient exchange across ranks inside the loop."""
     native().mlp_persistent(
@@ -124,8 +126,10 @@ def persistent_steps(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_starte
         list(xinfo) if xinfo else [])
 
 
-def persistent_prepare(Xp, T, idx_ring, cursor, loss_ring, loss_cursor, mom_started, P, M, layout: MlpLayout,
-                       batch: int, act: str, loss: str, grad_scale: float, sgd: Dict[str, float], xinfo=None):
+def persistent_prepare(Xp: torch.Tensor, T: torch.Tensor, idx_ring: torch.Tensor, cursor: torch.Tensor,
+                       loss_ring: torch.Tensor, loss_cursor: torch.Tensor, mom_started: torch.Tensor, P: torch.Tensor,
+                       M: torch.Tensor, layout: MlpLayout, batch: int, act: str, loss: str, grad_scale: float,
+                       sgd: Dict[str, float], xinfo: Any = None) -> Any:
     """:func:`persistent_steps` with its arguments checked and packed once: returns a
     native object whose ``launch(nsteps, stream=-1)`` enqueues the loop (host cost of
     one kernel launch)."""
@@ -145,8 +149,8 @@ def helper_elems(hidden: int, out_dim: int) -> int:
     return (hidden // 32) * 1024 + 64 * (-(-out_dim // 64))
 
 
-def exchange_info(p2p, xepoch: torch.Tensor, slot_elems: int, mode: str = "oneshot",
-                  timeout_iters: int = 1 << 24, helper=None):
+def exchange_info(p2p: Any, xepoch: torch.Tensor, slot_elems: int, mode: str = "oneshot",
+                  timeout_iters: int = 1 << 24, helper: Any = None) -> Any:
     """Flatten a :class:`~..parallel.p2p.P2PAllReduce` (dedicated to this loop) into the
     kernel's exchange descriptor.  ``slot_elems``: slot stride (>= the parameter count,
     >= the helper exchange array); ``mode``: "oneshot" (every gradient to every rank),
@@ -162,7 +166,7 @@ def exchange_info(p2p, xepoch: torch.Tensor, slot_elems: int, mode: str = "onesh
     return info
 
 
-def helper_buffers(p2p, hidden: int, out_dim: int):
+def helper_buffers(p2p: Any, hidden: int, out_dim: int) -> Any:
     """The helper form's hand-off buffers, carved from the p2p buffer's uncached data
     and flag regions (unused by the LL protocol): plain stores there reach memory
     before an s_waitcnt returns, so a relaxed flag suffices -- no L2 write-back or
@@ -178,7 +182,7 @@ def helper_buffers(p2p, hidden: int, out_dim: int):
 STAGE_ROWS, STAGE_COLS = 128, 32
 
 
-def make_stage(device):
+def make_stage(device: Any) -> Any:
     """Double-buffered staging slots for the pipelined batch gather."""
     return (torch.zeros(2, STAGE_ROWS, STAGE_COLS, dtype=torch.bfloat16, device=device),
             torch.zeros(2, STAGE_ROWS, 8, dtype=torch.float32, device=device),
@@ -186,10 +190,12 @@ def make_stage(device):
 
 
 def fused_step(
-    X, T, idx_ring, cursor, stage, loss_ring, p_in, p_out, g_prev, g_out, mom_in, mom_out,
+    X: torch.Tensor, T: torch.Tensor, idx_ring: torch.Tensor, cursor: torch.Tensor, stage: torch.Tensor,
+    loss_ring: torch.Tensor, p_in: torch.Tensor, p_out: torch.Tensor, g_prev: torch.Tensor, g_out: torch.Tensor,
+    mom_in: torch.Tensor, mom_out: torch.Tensor,
     layout: MlpLayout, batch: int, own_tiles: int, act: str, loss: str, apply_update: bool,
-    grad_scale: float, sgd: Dict[str, float], prev_grad_scale: float, first_step: bool, stream=None,
-    dbg_stamps=None, parity: int = 0, gather_self: bool = True,
+    grad_scale: float, sgd: Dict[str, float], prev_grad_scale: float, first_step: bool, stream: Any = None,
+    dbg_stamps: Any = None, parity: int = 0, gather_self: bool = True,
 ) -> None:
     """One fused step.  ``gather_self`` reads this step's batch straight from the
     index ring at ``cursor`` (and leaves the cursor for the caller to advance);

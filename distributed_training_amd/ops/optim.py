@@ -12,7 +12,7 @@ Semantics follow torch.optim exactly (tested against it), so the reference's
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from typing import Any, Dict, List, Optional
 
 import torch
 
@@ -30,7 +30,7 @@ def _grad32(fg_grad: torch.Tensor) -> torch.Tensor:
     return fg_grad if fg_grad.dtype == torch.float32 else fg_grad.float()
 
 
-def _split_params(group_params):
+def _split_params(group_params: Any) -> Any:
     flats: Dict[int, list] = {}
     flat_objs = {}
     singles = []
@@ -45,8 +45,8 @@ def _split_params(group_params):
     return [(flat_objs[k], v) for k, v in flats.items()], singles
 
 
-def _sgd_ref(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], lr, momentum, dampening, wd,
-             nesterov, maximize, first) -> None:
+def _sgd_ref(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], lr: float, momentum: float,
+             dampening: float, wd: float, nesterov: bool, maximize: bool, first: bool) -> None:
     d = -g if maximize else g
     if wd:
         d = d.add(p, alpha=wd)
@@ -82,7 +82,7 @@ def _saved_state_by_param(opt: torch.optim.Optimizer, state_dict: dict) -> Dict[
     return out
 
 
-def _restore_flat(fg, by_param: Dict[torch.nn.Parameter, dict], key: str) -> Optional[torch.Tensor]:
+def _restore_flat(fg: Any, by_param: Dict[torch.nn.Parameter, dict], key: str) -> Optional[torch.Tensor]:
     """A fresh flat fp32 buffer (the layout of ``fg.master``) filled with each
     parameter's saved ``key`` tensor; None when no parameter has one."""
     if not any(key in by_param.get(p, {}) for p in fg.params):
@@ -95,7 +95,7 @@ def _restore_flat(fg, by_param: Dict[torch.nn.Parameter, dict], key: str) -> Opt
     return flat
 
 
-def _stepped_in_backward(fg) -> bool:
+def _stepped_in_backward(fg: Any) -> bool:
     """True (once) when the DDP engine already ran this step bucket by bucket inside the
     backward (parallel/ddp.py ``overlap_optimizer``): ``step()`` then has nothing to do."""
     if getattr(fg, "stepped_in_backward", False):
@@ -104,13 +104,13 @@ def _stepped_in_backward(fg) -> bool:
     return False
 
 
-def _covers(params, fg) -> bool:
+def _covers(params: Any, fg: Any) -> bool:
     ids = {id(p) for p in params}
     return len(ids) == len(fg.params) and all(id(p) in ids for p in fg.params)
 
 
 class FusedSGD(torch.optim.Optimizer):
-    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+    def __init__(self, params: Any, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False) -> None:
         if nesterov and (momentum <= 0 or dampening != 0):
             raise ValueError("Nesterov momentum requires a momentum and zero dampening")
@@ -119,12 +119,12 @@ class FusedSGD(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._flat_state: Dict[int, dict] = {}
 
-    def hyper(self, group=None) -> dict:
+    def hyper(self, group: Any = None) -> dict:
         g = group or self.param_groups[0]
         return {k: g[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov", "maximize")}
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure: Any = None) -> Any:
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -171,11 +171,11 @@ class FusedSGD(torch.optim.Optimizer):
         return loss
 
     # -------------------------------------------------- step split over DDP buckets
-    def range_capable(self, fg) -> bool:
+    def range_capable(self, fg: Any) -> bool:
         return len(self.param_groups) == 1 and _covers(self.param_groups[0]["params"], fg)
 
     @torch.no_grad()
-    def step_range(self, fg, lo: int, hi: int, first: bool) -> None:
+    def step_range(self, fg: Any, lo: int, hi: int, first: bool) -> None:
         """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
         current stream): the same per-element math as :meth:`step` over the whole buffer,
         so a step split into ranges is bit-identical.  ``first``: the step's first range."""
@@ -191,7 +191,7 @@ class FusedSGD(torch.optim.Optimizer):
                           g["lr"], g["momentum"], g["dampening"], g["weight_decay"], 1.0, g["nesterov"],
                           g["maximize"], st["first"], -1)
 
-    def end_ranges(self, fg) -> None:
+    def end_ranges(self, fg: Any) -> None:
         """Every range of this step launched."""
         self._flat_state.setdefault(id(fg), {"first": True})["first"] = False
 
@@ -219,7 +219,8 @@ class FusedSGD(torch.optim.Optimizer):
                 if v is not None:
                     self.state[p]["momentum_buffer"] = v.to(p.device, torch.float32).reshape(p.shape).clone()
 
-    def _single_gpu(self, fg, p, lr, mom, damp, wd, nest, maxi) -> None:
+    def _single_gpu(self, fg: Any, p: Any, lr: float, mom: float, damp: float, wd: float, nest: bool,
+                    maxi: bool) -> None:
         i = fg.index_of(p)
         state = self.state[p]
         first = "momentum_buffer" not in state or state["momentum_buffer"] is None
@@ -252,7 +253,9 @@ class FusedSGD(torch.optim.Optimizer):
                         p.grad.zero_()
 
 
-def _adam_ref(p, g, m, v, vmax, step, lr, b1, b2, eps, wd, adamw, maximize, amsgrad) -> None:
+def _adam_ref(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, vmax: torch.Tensor, step: int,
+              lr: float, b1: float, b2: float, eps: float, wd: float, adamw: bool, maximize: bool,
+              amsgrad: bool) -> None:
     g = -g if maximize else g
     if wd:
         if adamw:
@@ -274,15 +277,15 @@ def _adam_ref(p, g, m, v, vmax, step, lr, b1, b2, eps, wd, adamw, maximize, amsg
 class FusedAdamW(torch.optim.Optimizer):
     """AdamW (``adamw=True``, default) or Adam with L2 (``adamw=False``)."""
 
-    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 amsgrad: bool = False, maximize: bool = False, adamw: bool = True) -> None:
+    def __init__(self, params: Any, lr: float = 1e-3, betas: Any = (0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, maximize: bool = False, adamw: bool = True) -> None:
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
                         maximize=maximize, adamw=adamw)
         super().__init__(params, defaults)
         self._flat_state: Dict[int, dict] = {}
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure: Any = None) -> Any:
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -327,7 +330,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     zero_grad = FusedSGD.zero_grad
 
-    def _flat(self, fg, ams: bool) -> dict:
+    def _flat(self, fg: Any, ams: bool) -> dict:
         st = self._flat_state.get(id(fg))
         if st is None:
             st = {"m": torch.zeros_like(fg.master), "v": torch.zeros_like(fg.master),
@@ -346,7 +349,7 @@ class FusedAdamW(torch.optim.Optimizer):
     range_capable = FusedSGD.range_capable
 
     @torch.no_grad()
-    def step_range(self, fg, lo: int, hi: int, first: bool) -> None:
+    def step_range(self, fg: Any, lo: int, hi: int, first: bool) -> None:
         """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
         current stream); ``first`` bumps the device step counter (the step's first range).
         Element-wise math identical to :meth:`step`: a split step is bit-identical."""
@@ -358,7 +361,7 @@ class FusedAdamW(torch.optim.Optimizer):
                            fg.compute[lo:hi] if fg.mixed else None, st["step"], g["lr"], b1, b2, g["eps"],
                            g["weight_decay"], 1.0, g["adamw"], g["maximize"], ams, first, -1)
 
-    def end_ranges(self, fg) -> None:
+    def end_ranges(self, fg: Any) -> None:
         pass
 
     @torch.no_grad()
@@ -401,7 +404,7 @@ class FusedAdamW(torch.optim.Optimizer):
                         float(torch.as_tensor(sv["step"]).reshape(-1)[0]))
 
 
-def build_optimizer(name: str, params, **kw) -> torch.optim.Optimizer:
+def build_optimizer(name: str, params: Any, **kw: Any) -> torch.optim.Optimizer:
     name = name.lower()
     if name == "sgd":
         return FusedSGD(params, **kw)

@@ -25,7 +25,7 @@ import os
 import sys
 import threading
 import time
-from typing import Callable, Deque, List, Optional, Tuple
+from typing import Any, Callable, Deque, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -35,7 +35,7 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
 
 
 @contextlib.contextmanager
-def _stdout_to_stderr():
+def _stdout_to_stderr() -> Any:
     """Redirect the C-level stdout (fd 1) to stderr for the duration."""
     sys.stdout.flush()
     saved = os.dup(1)
@@ -51,7 +51,7 @@ def _stdout_to_stderr():
 class CommWork:
     """Handle of an asynchronous collective."""
 
-    def __init__(self, torch_work=None, event=None, post=None) -> None:
+    def __init__(self, torch_work: Any = None, event: Any = None, post: Any = None) -> None:
         self._work = torch_work
         self._event = event
         self._post = post
@@ -103,19 +103,19 @@ class TorchComm(Communicator):
 
     name = "torch"
 
-    def __init__(self, group=None, device: Optional[torch.device] = None) -> None:
+    def __init__(self, group: Any = None, device: Optional[torch.device] = None) -> None:
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
         self.device = device or torch.device("cpu")
         self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
 
-    def _w(self, work, async_op):
+    def _w(self, work: Any, async_op: bool) -> Any:
         if async_op:
             return CommWork(torch_work=work)
         return None
 
-    def all_reduce(self, t, op="sum", async_op=False):
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Any:
         if self.world_size == 1:
             return CommWork() if async_op else None
         if op == "avg":
@@ -124,7 +124,7 @@ class TorchComm(Communicator):
         work = dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def all_gather_into(self, out, inp, async_op=False):
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Any:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -132,7 +132,7 @@ class TorchComm(Communicator):
         work = dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Any:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -149,13 +149,13 @@ class TorchComm(Communicator):
             post()
         return None
 
-    def broadcast(self, t, src=0, async_op=False):
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
         if self.world_size == 1:
             return CommWork() if async_op else None
         work = dist.broadcast(t, src=src, group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def all_to_all_single(self, out, inp) -> None:
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.world_size == 1:
             out.copy_(inp)
             return
@@ -202,7 +202,7 @@ class CommWatchdog:
         self._reported = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
-    def track(self, event, desc: str) -> None:
+    def track(self, event: Any, desc: str) -> None:
         """``event``: anything with ``query() -> bool`` (a ``torch.cuda.Event`` recorded after the collective)."""
         if self.timeout_s <= 0:
             return
@@ -268,7 +268,7 @@ class _StreamComm(Communicator):
     stream: torch.cuda.Stream
     watchdog: Optional[CommWatchdog] = None
 
-    def _enqueue(self, fn, async_op: bool, tensors: List[torch.Tensor], desc: str = "collective"
+    def _enqueue(self, fn: Any, async_op: bool, tensors: List[torch.Tensor], desc: str = "collective"
                  ) -> Optional[CommWork]:
         self.raise_if_error()
         cur = torch.cuda.current_stream(self.device)
@@ -308,7 +308,7 @@ class RcclComm(_StreamComm):
 
     name = "rccl"
 
-    def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
+    def __init__(self, rank: int, world_size: int, device: torch.device, store: Any = None, tag: str = "default",
                  stream_priority: int = -1, timeout_s: Optional[float] = None) -> None:
         from ..ops import ensure_rccl
 
@@ -340,7 +340,7 @@ class RcclComm(_StreamComm):
         if world_size > 1 and store is not None:
             from .p2p import maybe_create
 
-            def _min(t) -> None:
+            def _min(t: Any) -> None:
                 self._comm.all_reduce(t, "min", int(torch.cuda.current_stream(device).cuda_stream))
                 torch.cuda.current_stream(device).synchronize()
 
@@ -349,7 +349,7 @@ class RcclComm(_StreamComm):
     def supports_avg(self) -> bool:
         return True
 
-    def all_reduce(self, t, op="sum", async_op=False):
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Any:
         if self._p2p_ok(t, op):
             sc = 1.0 / self.world_size if op == "avg" else 1.0
             h, it = self._p2p._h, self._p2p.timeout_iters
@@ -357,7 +357,7 @@ class RcclComm(_StreamComm):
         return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t],
                              f"all_reduce {t.numel()} x {t.dtype}")
 
-    def all_gather_into(self, out, inp, async_op=False):
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Any:
         if self.world_size == 1:  # single rank: a device copy on the current stream
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -365,15 +365,15 @@ class RcclComm(_StreamComm):
         return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp],
                              f"all_gather {inp.numel()} x {inp.dtype}")
 
-    def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Any:
         return self._enqueue(lambda s: self._comm.reduce_scatter(out, inp, op, s), async_op, [out, inp],
                              f"reduce_scatter {out.numel()} x {out.dtype}")
 
-    def broadcast(self, t, src=0, async_op=False):
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
         return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t],
                              f"broadcast {t.numel()} x {t.dtype}")
 
-    def all_to_all_single(self, out, inp) -> None:
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp], "all_to_all")
 
     def abort(self) -> None:
@@ -384,7 +384,7 @@ class RcclComm(_StreamComm):
     def _p2p_ok(self, t: torch.Tensor, op: str) -> bool:
         return self._p2p is not None and op in ("sum", "avg") and self._p2p.supports(t)
 
-    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream: Any = None) -> None:
         """Enqueue on ``stream`` (default: current) with no stream hop: used
         inside hipGraph-captured step programs."""
         s = stream or torch.cuda.current_stream(self.device)
@@ -420,7 +420,7 @@ class RcclComm(_StreamComm):
         self._comm.destroy()
 
 
-def make_comm(device: torch.device, prefer: str = "auto", group=None, bulk: bool = False) -> Communicator:
+def make_comm(device: torch.device, prefer: str = "auto", group: Any = None, bulk: bool = False) -> Communicator:
     """Pick the communicator for ``device``.
 
     GPU: native RCCL (``prefer`` auto|rccl, the default); the IPC direct-push

@@ -41,7 +41,7 @@ from __future__ import annotations
 import contextlib
 import hashlib
 import logging
-from typing import List, Optional
+from typing import Any, List, Optional
 
 import torch
 import torch.nn as nn
@@ -58,7 +58,7 @@ MiB = 1 << 20
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Communicator] = None,
-                 device: Optional[torch.device] = None, bucket_cap_mb="auto",
+                 device: Optional[torch.device] = None, bucket_cap_mb: Any = "auto",
                  first_bucket_mb: Optional[float] = None, broadcast_buffers: bool = True,
                  param_dtype: torch.dtype = torch.float32, init_sync: bool = True) -> None:
         super().__init__()
@@ -142,7 +142,7 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._pending = [[] for _ in self.buckets]
 
-    def _make_hook(self, i: int):
+    def _make_hook(self, i: int) -> Any:
         def hook(p: torch.Tensor) -> None:
             if not self.require_sync:
                 return
@@ -212,7 +212,7 @@ class DistributedDataParallel(nn.Module):
             self._works.append(self.comm.all_reduce(sl, op="sum", async_op=True))
 
     # ------------------------------------------------------------ optimizer in backward
-    def overlap_optimizer(self, optimizer) -> bool:
+    def overlap_optimizer(self, optimizer: Any) -> bool:
         """Run ``optimizer``'s update bucket by bucket INSIDE the backward, on a side HIP
         stream, as soon as a bucket's gradients are final (all-reduced across ranks; at one
         rank: written, including deferred weight gradients) -- the update of the late layers
@@ -256,7 +256,7 @@ class DistributedDataParallel(nn.Module):
         lm.FLUSH_LISTENERS.append(on_flush)
         return True
 
-    def _ov_range(self, b: int):
+    def _ov_range(self, b: int) -> Any:
         bk = self.buckets[b]
         end = self.flat.master.numel() if b == len(self.buckets) - 1 else bk.end
         return bk.start, end
@@ -322,7 +322,7 @@ class DistributedDataParallel(nn.Module):
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()  # a timed-out peer exchange raises here, not silently later
 
-    def forward(self, *args, **kwargs):
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
         if self.broadcast_buffers and self.world_size > 1 and self.require_sync:
             self._broadcast_buffers()
         if self.flat.grad.is_cuda:
@@ -332,7 +332,7 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
-    def no_sync(self):
+    def no_sync(self) -> Any:
         old = self.require_sync
         self.require_sync = False
         try:
@@ -350,7 +350,7 @@ class DistributedDataParallel(nn.Module):
         return clip_flat_grad_norm_(self.flat, max_norm)
 
     # ------------------------------------------------------------ state
-    def state_dict(self, *args, **kwargs):
+    def state_dict(self, *args: Any, **kwargs: Any) -> Any:
         sd = super().state_dict(*args, **kwargs)
         if self.flat.mixed:  # checkpoints carry the fp32 master, not the bf16 compute copy
             # matched by storage, so tied aliases (GPT-2 lm_head.weight = wte.weight) get it too
@@ -361,7 +361,7 @@ class DistributedDataParallel(nn.Module):
                     sd[key] = self.flat.master_view(i).detach()
         return sd
 
-    def load_state_dict(self, state_dict, strict: bool = True):
+    def load_state_dict(self, state_dict: Any, strict: bool = True) -> Any:
         res = super().load_state_dict(state_dict, strict=strict)
         if self.flat.mixed:
             with torch.no_grad():

@@ -20,7 +20,7 @@ Trainer wraps the model) -- keeps working.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -195,7 +195,7 @@ class FlatParamGroup:
 
 
 @torch.no_grad()
-def clip_flat_grad_norm_(fg: FlatParamGroup, max_norm: float, comm=None, sharded: bool = False) -> torch.Tensor:
+def clip_flat_grad_norm_(fg: FlatParamGroup, max_norm: float, comm: Any = None, sharded: bool = False) -> torch.Tensor:
     """Global-norm gradient clipping over ONE flat gradient buffer (what
     ``torch.nn.utils.clip_grad_norm_`` computes over the module's parameters).
 
@@ -272,7 +272,7 @@ def xgmi_bucket_caps(world_size: int, grad_bytes: int, min_buckets: int = 6) -> 
 
 
 def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]], device: torch.device,
-                     param_dtype=torch.float32, grad_dtype=None, reverse: bool = True,
+                     param_dtype: Any = torch.float32, grad_dtype: Any = None, reverse: bool = True,
                      pad_after: Optional[Dict[int, int]] = None) -> FlatParamGroup:
     items = list(params_with_names)
     if reverse:
@@ -283,7 +283,7 @@ def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]]
                           pad_after=pad_after)
 
 
-def param_flat_tags(params) -> Dict[int, Tuple[FlatParamGroup, int]]:
+def param_flat_tags(params: Any) -> Dict[int, Tuple[FlatParamGroup, int]]:
     out = {}
     for p in params:
         tag = getattr(p, "_dta_flat", None)

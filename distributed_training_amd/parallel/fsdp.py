@@ -41,7 +41,7 @@ from __future__ import annotations
 
 import functools
 import logging
-from typing import Callable, Dict, List, Optional, Sequence, Set, Tuple, Type, Union
+from typing import Any, Callable, Dict, List, Optional, Sequence, Set, Tuple, Type, Union
 
 import torch
 import torch.nn as nn
@@ -94,13 +94,13 @@ class _SplitInto(torch.autograd.Function):
     the unit's gradient, plus a copy into the flat gradient after it)."""
 
     @staticmethod
-    def forward(ctx, full, unit):
+    def forward(ctx: Any, full: torch.Tensor, unit: Any) -> Any:
         ctx.unit = unit
         ctx.set_materialize_grads(False)
         return tuple(full.split(unit._split_sizes))
 
     @staticmethod
-    def backward(ctx, *grads):
+    def backward(ctx: Any, *grads: Any) -> Any:
         u = ctx.unit
         dest = u.grad_buffer()
         pos = 0
@@ -425,8 +425,8 @@ class FullyShardedDataParallel(nn.Module):
             return self._fwd_order[k]
         return None
 
-    def _make_pre_forward(self, u: _Unit):
-        def pre(mod, args):
+    def _make_pre_forward(self, u: _Unit) -> Any:
+        def pre(mod: Any, args: Any) -> Any:
             if u.in_backward:  # checkpoint recomputation: already gathered
                 u.unshard(async_op=False)
                 u.set_views()
@@ -443,8 +443,8 @@ class FullyShardedDataParallel(nn.Module):
 
         return pre
 
-    def _make_post_forward(self, u: _Unit):
-        def post(mod, args, output):
+    def _make_post_forward(self, u: _Unit) -> Any:
+        def post(mod: Any, args: Any, output: Any) -> Any:
             if u.in_backward:
                 # activation-checkpoint recomputation inside this unit's backward:
                 # the recomputed graph still needs the gathered parameters
@@ -460,12 +460,12 @@ class FullyShardedDataParallel(nn.Module):
 
         return post
 
-    def _register_pre_backward(self, u: _Unit, output) -> None:
+    def _register_pre_backward(self, u: _Unit, output: Any) -> None:
         if not torch.is_grad_enabled():
             return
         u._bwd_ready = False
 
-        def hook(grad):
+        def hook(grad: torch.Tensor) -> Any:
             if not u._bwd_ready:
                 u._bwd_ready = True
                 u.in_backward = True
@@ -481,7 +481,7 @@ class FullyShardedDataParallel(nn.Module):
             if t.requires_grad:
                 t.register_hook(hook)
 
-    def forward(self, *args, **kwargs):
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
         if self.prefetch and not self._record_order and self._fwd_order:
             self._fwd_order[0].unshard(async_op=True)  # the first unit (the embedding) in flight with the root's
         if self.root_unit is not None:
@@ -599,11 +599,11 @@ class FullyShardedDataParallel(nn.Module):
             return ordered
         return {}
 
-    def state_dict(self, *args, **kwargs):  # FULL_STATE_DICT semantics (reference save path)
+    def state_dict(self, *args: Any, **kwargs: Any) -> Any:  # FULL_STATE_DICT semantics (reference save path)
         return self.full_state_dict(rank0_only=True, offload_to_cpu=True)
 
     @torch.no_grad()
-    def load_state_dict(self, state_dict, strict: bool = True):
+    def load_state_dict(self, state_dict: Any, strict: bool = True) -> Any:
         fg = self.shards
         missing = []
         for u in self.units:
@@ -634,7 +634,7 @@ class FullyShardedDataParallel(nn.Module):
     _OPT_FORMAT = "dta_fsdp_full_optim_v1"
 
     @torch.no_grad()
-    def full_optim_state_dict(self, optimizer, rank0_only: bool = True) -> Dict:
+    def full_optim_state_dict(self, optimizer: Any, rank0_only: bool = True) -> Dict:
         """Collective: the optimizer state of the WHOLE model, keyed by original
         parameter names (world-size independent, like ``FULL_STATE_DICT``).  Each
         shard-sized state tensor (momentum, Adam moments) is all-gathered per unit
@@ -662,7 +662,7 @@ class FullyShardedDataParallel(nn.Module):
         return {"format": self._OPT_FORMAT, "state": out_state, "param_groups": groups}
 
     @torch.no_grad()
-    def load_full_optim_state_dict(self, optimizer, osd: Dict) -> None:
+    def load_full_optim_state_dict(self, optimizer: Any, osd: Dict) -> None:
         """Inverse of :meth:`full_optim_state_dict` on any world size: every rank
         rebuilds each unit's flat state from the per-parameter tensors and keeps its
         shard, then hands the optimizer a local state dict of its shard params."""
@@ -699,7 +699,7 @@ class FullyShardedDataParallel(nn.Module):
                  "shard": u.shard_size, "root": int(u.is_root)} for u in self.units]
 
 
-def _iter_tensors(x):
+def _iter_tensors(x: Any) -> Any:
     if isinstance(x, torch.Tensor):
         yield x
     elif isinstance(x, (list, tuple)):

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import logging
 import os
-from typing import Optional
+from typing import Any, Optional
 
 import torch
 import torch.distributed as dist
@@ -64,7 +64,7 @@ class IpcComm(_StreamComm):
 
     _seq: dict = {}
 
-    def __init__(self, rank: int, world_size: int, device: torch.device, store=None, tag: str = "default",
+    def __init__(self, rank: int, world_size: int, device: torch.device, store: Any = None, tag: str = "default",
                  slot_mb: Optional[float] = None, timeout_s: Optional[float] = None, self_test: bool = True,
                  stream_priority: int = -1) -> None:
         from ..ops import native
@@ -170,7 +170,7 @@ class IpcComm(_StreamComm):
         return t.is_cuda and t.dtype in (torch.float32, torch.bfloat16) and op in _RED
 
     # ------------------------------------------------------------ Communicator API
-    def all_reduce(self, t, op="sum", async_op=False):
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Any:
         if self.world_size == 1:
             return CommWork() if async_op else None
         if not self._arith(t, op):
@@ -180,14 +180,14 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._all_reduce_native(t, op, s), async_op, [t])
         tmp = t.contiguous().clone()  # fresh allocation: 16-byte aligned
 
-        def run(s) -> None:
+        def run(s: Any) -> None:
             self._all_reduce_native(tmp, op, s)
             with torch.cuda.stream(self.stream):
                 t.copy_(tmp.view_as(t))
 
         return self._enqueue(run, async_op, [t, tmp])
 
-    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum", stream: Any = None) -> None:
         """On ``stream`` (default: current) without the comm-stream hop (graph capture)."""
         s = stream or torch.cuda.current_stream(self.device)
         if self.world_size == 1:
@@ -196,7 +196,7 @@ class IpcComm(_StreamComm):
             raise ValueError("all_reduce_inline: aligned fp32 / bf16 tensor and sum / avg / max / min")
         self._all_reduce_native(t, op, int(s.cuda_stream))
 
-    def reduce_scatter_into(self, out, inp, op="sum", async_op=False):
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Any:
         W = self.world_size
         if inp.numel() != W * out.numel():
             raise ValueError("reduce_scatter_into: input must hold world_size x output elements")
@@ -214,7 +214,7 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._reduce_scatter_native(out, inp, op, s), async_op, [out, inp])
         mp = -(-m // 8) * 8  # pad each chunk to 16-byte alignment
 
-        def run(s) -> None:
+        def run(s: Any) -> None:
             with torch.cuda.stream(self.stream):
                 ip = torch.zeros(W, mp, dtype=inp.dtype, device=inp.device)
                 ip[:, :m].copy_(inp.reshape(W, m))
@@ -225,7 +225,7 @@ class IpcComm(_StreamComm):
 
         return self._enqueue(run, async_op, [out, inp])
 
-    def all_gather_into(self, out, inp, async_op=False):
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Any:
         W = self.world_size
         if out.numel() != W * inp.numel():
             raise ValueError("all_gather_into: output must hold world_size x input elements")
@@ -238,7 +238,7 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._all_gather_native(out, inp, s), async_op, [out, inp])
         mp = -(-(m * es) // 16) * 16 // es if (16 % es == 0) else m
 
-        def run(s) -> None:
+        def run(s: Any) -> None:
             with torch.cuda.stream(self.stream):
                 ip = torch.zeros(mp, dtype=inp.dtype, device=inp.device)
                 ip[:m].copy_(inp.reshape(-1))
@@ -249,7 +249,7 @@ class IpcComm(_StreamComm):
 
         return self._enqueue(run, async_op, [out, inp])
 
-    def broadcast(self, t, src=0, async_op=False):
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
         if self.world_size == 1:
             return CommWork() if async_op else None
         if (t.numel() * t.element_size()) % 2:  # odd byte count: control plane
@@ -262,14 +262,14 @@ class IpcComm(_StreamComm):
             return self._enqueue(lambda s: self._broadcast_native(t, src, s), async_op, [t])
         tmp = t.contiguous().clone()
 
-        def run(s) -> None:
+        def run(s: Any) -> None:
             self._broadcast_native(tmp, src, s)
             with torch.cuda.stream(self.stream):
                 t.copy_(tmp.view_as(t))
 
         return self._enqueue(run, async_op, [t, tmp])
 
-    def all_to_all_single(self, out, inp) -> None:
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         if self.world_size == 1:
             out.copy_(inp)
             return

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import logging
 import os
-from typing import Optional
+from typing import Any, Optional
 
 import torch
 
@@ -28,7 +28,7 @@ class P2PAllReduce:
 
     _seq: dict = {}
 
-    def __init__(self, rank: int, world_size: int, device: torch.device, store, tag: str = "default",
+    def __init__(self, rank: int, world_size: int, device: torch.device, store: Any, tag: str = "default",
                  max_elems: int = DEFAULT_MAX_ELEMS, timeout_iters: int = DEFAULT_TIMEOUT_ITERS,
                  protocol: str = "ll") -> None:
         from ..ops import native
@@ -93,7 +93,7 @@ def intra_node() -> bool:
     return lws == ws
 
 
-def maybe_create(rank: int, world_size: int, device: torch.device, store, verify_comm,
+def maybe_create(rank: int, world_size: int, device: torch.device, store: Any, verify_comm: Any,
                  tag: str = "default") -> Optional[P2PAllReduce]:
     """Create + self-test the p2p path on every rank (collective).  Returns
     None (all ranks agree) when disabled, not intra-node, or the test fails."""

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import logging
 import time
-from typing import Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 
@@ -138,7 +138,7 @@ class RoutedComm(Communicator):
         logger.info("routed comm table (rank %d): %s", self.rank, self.routes_from(table))
         return table
 
-    def routes_from(self, table) -> str:
+    def routes_from(self, table: Any) -> str:
         saved, self.table = getattr(self, "table", None), table
         try:
             return ", ".join(f"{k}: {v}" for k, v in self.routes().items())
@@ -150,24 +150,25 @@ class RoutedComm(Communicator):
     def supports_avg(self) -> bool:
         return self.primary.supports_avg() and self.fast.supports_avg()
 
-    def all_reduce(self, t, op="sum", async_op=False) -> Optional[CommWork]:
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
         c = self._route("all_reduce", t.dtype, t.numel() * t.element_size()) if op in ("sum", "avg") \
             else self.primary
         return c.all_reduce(t, op=op, async_op=async_op)
 
-    def all_gather_into(self, out, inp, async_op=False) -> Optional[CommWork]:
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Optional[CommWork]:
         c = self._route("all_gather", inp.dtype, out.numel() * out.element_size())
         return c.all_gather_into(out, inp, async_op=async_op)
 
-    def reduce_scatter_into(self, out, inp, op="sum", async_op=False) -> Optional[CommWork]:
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum",
+                            async_op: bool = False) -> Optional[CommWork]:
         c = self._route("reduce_scatter", inp.dtype, inp.numel() * inp.element_size()) if op in ("sum", "avg") \
             else self.primary
         return c.reduce_scatter_into(out, inp, op=op, async_op=async_op)
 
-    def broadcast(self, t, src=0, async_op=False) -> Optional[CommWork]:
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Optional[CommWork]:
         return self.primary.broadcast(t, src=src, async_op=async_op)
 
-    def all_to_all_single(self, out, inp) -> None:
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         self.primary.all_to_all_single(out, inp)
 
     def barrier(self) -> None:
@@ -179,7 +180,7 @@ class RoutedComm(Communicator):
             if poll is not None:
                 poll()
 
-    def watch_stream(self, stream, desc: str) -> None:
+    def watch_stream(self, stream: Any, desc: str) -> None:
         watch = getattr(self.primary, "watch_stream", None)
         if watch is not None:
             watch(stream, desc)
@@ -190,7 +191,8 @@ class RoutedComm(Communicator):
             if d is not None:
                 d()
 
-    def __getattr__(self, name):  # everything else (all_reduce_inline, _p2p, check_errors, ...): the primary's
+    # everything else (all_reduce_inline, _p2p, check_errors, ...): the primary's
+    def __getattr__(self, name: str) -> Any:
         if name in ("primary", "fast"):
             raise AttributeError(name)
         return getattr(self.primary, name)

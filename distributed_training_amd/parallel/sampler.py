@@ -12,7 +12,7 @@ device-resident loader can upload them in one copy.
 from __future__ import annotations
 
 import math
-from typing import Iterator, Optional
+from typing import Any, Iterator, Optional
 
 import torch
 from torch.utils.data import Sampler
@@ -21,7 +21,7 @@ from torch.utils.data import Sampler
 class DistributedSampler(Sampler):
     """Drop-in for ``torch.utils.data.distributed.DistributedSampler``."""
 
-    def __init__(self, dataset, num_replicas: Optional[int] = None, rank: Optional[int] = None,
+    def __init__(self, dataset: Any, num_replicas: Optional[int] = None, rank: Optional[int] = None,
                  shuffle: bool = True, seed: int = 0, drop_last: bool = False) -> None:
         if num_replicas is None or rank is None:
             import torch.distributed as dist

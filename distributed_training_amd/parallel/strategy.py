@@ -61,17 +61,17 @@ class DistributedStrategy(ABC):
         """State dict to checkpoint; called on ALL ranks."""
         return model.state_dict()
 
-    def optim_state(self, model: Module, optimizer) -> Dict[str, Any]:
+    def optim_state(self, model: Module, optimizer: Any) -> Dict[str, Any]:
         """Optimizer state to checkpoint; called on ALL ranks (replicated engines:
         every rank holds the complete state)."""
         return optimizer.state_dict()
 
-    def load_optim_state(self, model: Module, optimizer, osd: Dict[str, Any]) -> None:
+    def load_optim_state(self, model: Module, optimizer: Any, osd: Dict[str, Any]) -> None:
         optimizer.load_state_dict(osd)
 
 
 class DDPStrategy(DistributedStrategy):
-    def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb="auto", first_bucket_mb=None,
+    def __init__(self, local_rank: int, is_gpu: bool, bucket_cap_mb: Any = "auto", first_bucket_mb: Any = None,
                  mixed_precision: Optional[str] = None, comm: Optional[Communicator] = None) -> None:
         self.local_rank = local_rank
         self.is_gpu = is_gpu
@@ -99,7 +99,7 @@ class DDPStrategy(DistributedStrategy):
 
 
 class FSDPStrategy(DistributedStrategy):
-    def __init__(self, is_gpu: bool, wrap_policy=None, mixed_precision: Optional[str] = None,
+    def __init__(self, is_gpu: bool, wrap_policy: Any = None, mixed_precision: Optional[str] = None,
                  reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None,
                  cpu_offload: bool = False) -> None:
         self.is_gpu = is_gpu
@@ -127,12 +127,12 @@ class FSDPStrategy(DistributedStrategy):
         # FULL_STATE_DICT, offload_to_cpu=True, rank0_only=True (fsdp_strategy.py:31-35) -- on all ranks
         return model.full_state_dict(rank0_only=True, offload_to_cpu=True)
 
-    def optim_state(self, model: Module, optimizer) -> Dict[str, Any]:
+    def optim_state(self, model: Module, optimizer: Any) -> Dict[str, Any]:
         # each rank holds only its shards' state: gathered per unit into a full,
         # world-size independent state keyed by parameter name (collective)
         return model.full_optim_state_dict(optimizer, rank0_only=True)
 
-    def load_optim_state(self, model: Module, optimizer, osd: Dict[str, Any]) -> None:
+    def load_optim_state(self, model: Module, optimizer: Any, osd: Dict[str, Any]) -> None:
         model.load_full_optim_state_dict(optimizer, osd)
 
     def save_checkpoint(self, model: Module, state_dict: dict, path: str) -> None:

@@ -9,7 +9,7 @@ and MIN and raises if any rank differs.
 from __future__ import annotations
 
 import logging
-from typing import List
+from typing import Any, List
 
 import torch
 
@@ -33,7 +33,7 @@ def param_checksums(model: torch.nn.Module) -> torch.Tensor:
 
 
 @torch.no_grad()
-def check_replicas_in_sync(model: torch.nn.Module, env, rtol: float = 0.0) -> None:
+def check_replicas_in_sync(model: torch.nn.Module, env: Any, rtol: float = 0.0) -> None:
     import torch.distributed as dist
 
     if not dist.is_initialized() or dist.get_world_size() == 1:

@@ -11,6 +11,7 @@ from __future__ import annotations
 import logging
 import sys
 from pathlib import Path
+from typing import Any
 
 logger = logging.getLogger("distributed_training_amd.trainer")
 
@@ -18,7 +19,7 @@ FORMAT = "%(asctime)s | %(levelname)s | %(message)s"
 DATEFMT = "%Y-%m-%d %H:%M:%S"
 
 
-def setup_logging(cfg) -> None:
+def setup_logging(cfg: Any) -> None:
     """Configure logging to write to both file and console."""
     logging.basicConfig(level=logging.INFO)
     logger.info(f"Logging setup complete. Log file: {cfg.logging.file}")

@@ -11,14 +11,14 @@ import contextlib
 import ctypes
 import os
 import time
-from typing import Dict, List, Optional
+from typing import Any, Dict, List, Optional
 
 import torch
 
 _roctx = None
 
 
-def _load_roctx():
+def _load_roctx() -> Any:
     global _roctx
     if _roctx is not None:
         return _roctx if _roctx else None
@@ -62,11 +62,11 @@ class _Range:
     def __init__(self, name: str) -> None:
         self.name = name
 
-    def __enter__(self):
+    def __enter__(self) -> Any:
         _roctx.roctxRangePushA(self.name.encode())
         return self
 
-    def __exit__(self, *exc):
+    def __exit__(self, *exc: Any) -> None:
         _roctx.roctxRangePop()
         return False
 
@@ -74,7 +74,7 @@ class _Range:
 _NULL = contextlib.nullcontext()
 
 
-def range_(name: str):
+def range_(name: str) -> Any:
     """Context manager: a named roctx range around host work (enqueue of kernels /
     collectives); a shared no-op context when tracing is off."""
     return _Range(name) if enabled() else _NULL

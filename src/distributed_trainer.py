@@ -10,6 +10,7 @@ Same public names and signatures: ``TrainingConfig``,
 import logging
 import os
 import sys
+from typing import Any
 
 if __package__ in (None, ""):  # executed as a script by torchrun
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -29,7 +30,7 @@ __all__ = ["TrainingConfig", "DistributedEnvironment", "ModelCheckpoint", "Train
 
 
 @main_decorator(config_path="../conf", config_name="config", version_base=None)
-def main(cfg) -> None:
+def main(cfg: Any) -> None:
     """Main training entry point."""
     run(cfg)
 

@@ -14,6 +14,7 @@ trains the default config (what the cloud-init launcher does).
 import argparse
 import os
 import sys
+from typing import Any
 
 if __package__ in (None, ""):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -23,7 +24,7 @@ from distributed_training_amd.config import compose, prepare_run_dir, split_argv
 CONF_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "conf")
 
 
-def parse(argv=None):
+def parse(argv: Any = None) -> Any:
     argv = list(sys.argv[1:] if argv is None else argv)
     overrides, rest = split_argv(argv)
     ap = argparse.ArgumentParser(description="simple distributed training job")
@@ -41,7 +42,7 @@ def parse(argv=None):
     return overrides
 
 
-def main(argv=None):
+def main(argv: Any = None) -> Any:
     from distributed_training_amd.app import run
 
     overrides = parse(argv)

@@ -21,7 +21,7 @@ import logging
 import os
 import sys
 from pathlib import Path
-from typing import List, Tuple
+from typing import Any, List, Tuple
 
 import torch
 import torch.distributed as dist
@@ -75,7 +75,7 @@ def rank_logger(rank: int, log_dir: str = "logs") -> logging.Logger:
 class ManualDDP:
     """What DistributedDataParallel does, spelled out (no hooks, no overlap)."""
 
-    def __init__(self, model: nn.Module, comm, world_size: int, bucketed: bool = False) -> None:
+    def __init__(self, model: nn.Module, comm: Any, world_size: int, bucketed: bool = False) -> None:
         self.model = model
         self.comm = comm
         self.world_size = world_size
@@ -175,7 +175,7 @@ def get_argument_parser() -> argparse.ArgumentParser:
     return p
 
 
-def main(argv=None) -> None:
+def main(argv: Any = None) -> None:
     args = get_argument_parser().parse_args(argv)
     if not torch.cuda.is_available() and args.backend == "nccl":
         args.backend = "gloo"
