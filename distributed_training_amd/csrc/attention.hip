@@ -432,6 +432,10 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   __shared__ __attribute__((aligned(16))) bf16 Qs[2][BM * D];
   __shared__ __attribute__((aligned(16))) bf16 dOs[2][BM * D];
   __shared__ __attribute__((aligned(16))) float rc[2][2][BM];  // [buf][-lse/scale | -delta][q] (16-B rows: float4 reads)
+  // the workgroup's 128 keys of K and V, staged once: S / dP read their B operands from here
+  // instead of keeping them in 64 (D = 128) registers, which pushed the working set past the
+  // 256 arch VGPRs and made the compiler shuttle accumulators through AGPRs every slice
+  __shared__ __attribute__((aligned(16))) bf16 KVs[2][128 * D];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -448,16 +452,12 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + (int64_t)hk * D;
   const float c = a.scale * kLog2e, inv_scale = 1.f / a.scale;
 
-  bf16x8 kf[NKS], vf[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    if (key < a.S) {
-      kf[ks] = *reinterpret_cast<const bf16x8*>(kbase + (int64_t)key * a.k_ss + ks * 16 + hh * 8);
-      vf[ks] = *reinterpret_cast<const bf16x8*>(vbase + (int64_t)key * a.v_ss + ks * 16 + hh * 8);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kf[ks][j] = vf[ks][j] = f2bf(0.f);
-    }
+  {
+    TileRegs<128, D, 256> kt, vt;  // (keys >= S zero-filled; visible after the loop's first barrier)
+    tile_load(kt, kbase, a.k_ss, kblk0, a.S, tid);
+    tile_load(vt, vbase, a.v_ss, kblk0, a.S, tid);
+    tile_store(kt, KVs[0], tid);
+    tile_store(vt, KVs[1], tid);
   }
   f32x16 dvacc[NDT], dkacc[NDT];
 #pragma unroll
@@ -495,7 +495,8 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
       const int q0 = q0s + qt * 32;
-      if (CAUSAL && NQT > 1 && q0 + 31 < kw0) continue;
+      // (no per-tile skip: a fully masked tile occurs only in the diagonal slices, and a
+      // branch here splits the slice into blocks the scheduler cannot interleave)
       // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
       // row constants of this lane's 16 accumulator rows: rows qt*32 + 8g + 4hh + 0..3 are 4
       // consecutive floats -- 4 ds_read_b128 per array instead of 16 scalar reads
@@ -510,14 +511,15 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       }
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        s = mfma32x32x16(row_frag<D>(Qb, qt * 32 + r32, ks, hh), kf[ks], s);
-        dp = mfma32x32x16(row_frag<D>(Db, qt * 32 + r32, ks, hh), vf[ks], dp);
+        s = mfma32x32x16(row_frag<D>(Qb, qt * 32 + r32, ks, hh), row_frag<D>(KVs[0], wave * 32 + r32, ks, hh), s);
+        dp = mfma32x32x16(row_frag<D>(Db, qt * 32 + r32, ks, hh), row_frag<D>(KVs[1], wave * 32 + r32, ks, hh), dp);
       }
-      const bool need_mask = CAUSAL && q0 < kw0 + 31;
+      // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate per element
+      const int dl = CAUSAL && q0 < kw0 + 31 ? key - q0 - 4 * hh : -64;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float pv = fexp2(s[i] * c);
-        if (need_mask && key > q0 + mfma32_row(i, lane)) pv = 0.f;
+        if (CAUSAL && dl > mfma32_row(i, 0)) pv = 0.f;
         s[i] = pv;             // P
         dp[i] = pv * dp[i];    // dS (unscaled)
       }
@@ -637,10 +639,12 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
         s = mfma32x32x16(ka, qf[ks], s);
         dp = mfma32x32x16(va, df[ks], dp);
       }
+      // key k0 + t*32 + row(i) + 4hh > qrow <=> row(i) > ql
+      const int ql = need_mask ? qrow - k0 - t * 32 - 4 * hh : 64;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float pv = fexp2(s[i] * c);
-        if (need_mask && k0 + t * 32 + mfma32_row(i, lane) > qrow) pv = 0.f;
+        if (CAUSAL && mfma32_row(i, 0) > ql) pv = 0.f;
         dp[i] *= pv;  // dS^T
       }
       // dQ^T += K^T . dS^T  (K^T by transposed reads; dS^T as it stands)
