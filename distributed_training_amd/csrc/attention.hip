@@ -39,6 +39,11 @@
 #include "attention.h"
 
 #include <cstdlib>
+#include <type_traits>
+
+#ifndef DTA_DKDV_PF
+#define DTA_DKDV_PF 3
+#endif
 
 namespace dta {
 
@@ -49,6 +54,16 @@ constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time (register-ring
+// indices stay constants: a runtime index would put the ring in scratch)
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of
 // row q (columns 4p..4p+3) of a 4 x 16 block; lane i receives column i of the
 // four rows (row q in element q).
@@ -58,26 +73,24 @@ __device__ __forceinline__ bf16x4 lds_tr4(const bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-// LDS images are unpadded [rows][D] bf16 tiles with the 16-byte chunks of each
-// row XOR-swizzled by a function of the row, chosen (scripts/lds_banks.py, the
-// lane-group / bank rules of MI355X_MICROARCH.md §LDS) so that all three
-// accesses are conflict-free on the same image: the row read of an MFMA
-// operand (ds_read_b128, lane = row, 16 B of the head dim), the transposed
-// read (ds_read_b64_tr_b16, 4 rows x 16 columns per 16-lane group) and the
-// register-staged 16-byte stores.  No padding keeps K+V double buffers at
-// 32 KB (D = 64) / 64 KB (D = 128) per workgroup, so two or more workgroups
-// share a CU.
-template <int D>
-__device__ __forceinline__ int swz(int row) {
-  static_assert(D == 64 || D == 128, "head dim");
-  if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 3) & 1) | (((row >> 4) & 1) << 1);
-  else return ((row & 3) << 2) | ((row >> 2) & 3);
-}
-
-// element offset of (row, col) in a swizzled image (col % 4 == 0 for 8-byte reads)
+// LDS images are unpadded [rows][D] bf16 tiles cut into 8-row x 32-column
+// subtiles of 512 B (cdna_hip_programming.md T10, image (a)); inside a subtile
+// row r holds its four 16-byte chunks in the order chunk ^ ((r >> 2) & 3).  All
+// three accesses are conflict-free on this one image (scripts/lds_banks.py
+// "subtiled", the lane-group / bank rules of MI355X_MICROARCH.md §LDS): the row
+// read of an MFMA operand (ds_read_b128, lane = row, 16 B of the head dim), the
+// transposed read (ds_read_b64_tr_b16, 4 rows x 16 columns per 16-lane group)
+// and the register-staged 16-byte stores (tile_store's lane order).  Unlike a
+// per-row XOR over all D / 8 chunks, the reads of one lane at other head-dim
+// chunks / rows differ by a CONSTANT (+512 B per 32 columns, +D*16 B per 8
+// rows): a fragment loop needs two base registers and immediate offsets, not
+// one address register per k-step.  No padding keeps K+V double buffers at
+// 32 KB (D = 64) / 64 KB (D = 128) per workgroup.
 template <int D>
 __device__ __forceinline__ int lo(int row, int col) {
-  return row * D + ((((col >> 3) ^ swz<D>(row)) << 3) | (col & 7));
+  static_assert(D == 64 || D == 128, "head dim");
+  const int ch = col >> 3;
+  return (row >> 3) * (D * 8) + (ch >> 2) * 256 + (row & 7) * 32 + (((ch & 3) ^ ((row >> 2) & 3)) << 3) + (col & 7);
 }
 
 // A-operand fragment of X^T for a 32x32x16 MFMA whose B operand is an
@@ -102,21 +115,33 @@ __device__ __forceinline__ bf16x8 row_frag(const bf16* X, int row, int ks, int h
 }
 
 // Cooperative register staging of an [R][D] bf16 tile (NT threads, 16-byte
-// loads), rows >= nrows zero-filled; then one store into a swizzled LDS image.
+// loads), rows >= nrows zero-filled; then one store into the subtiled LDS image.
+// Chunk e of the tile -> (row, column): a wave covers 8 rows x 128 B (whole
+// 128-B lines of global memory), and each 8-lane group of its store covers two
+// rows of one 512-B subtile = 128 contiguous LDS bytes (conflict-free
+// ds_write_b128: MI355X_MICROARCH.md §LDS).
+template <int D>
+__device__ __forceinline__ void stage_rc(int e, int& r, int& c8) {
+  constexpr int P = D / 64;  // 128-byte column pairs of chunk blocks per row
+  const int l = e & 63, w = e >> 6;
+  r = 8 * (w / P) + 2 * ((l >> 4) & 3) + ((l >> 2) & 1);
+  c8 = 8 * (4 * (2 * (w % P) + ((l >> 3) & 1)) + (l & 3));
+}
+
 template <int R, int D, int NT>
 struct TileRegs {
   static constexpr int N = R * D / 8 / NT;
-  static_assert(N >= 1 && R * D == N * 8 * NT, "tile / thread count");
+  static_assert(N >= 1 && R * D == N * 8 * NT && R % 8 == 0 && NT % 64 == 0, "tile / thread count");
   bf16x8 v[N];
 };
 
 template <int R, int D, int NT>
 __device__ __forceinline__ void tile_load(TileRegs<R, D, NT>& t, const bf16* base, int64_t rs, int row0, int nrows,
                                           int tid) {
-  constexpr int CPR = D / 8;
 #pragma unroll
   for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
-    const int e = tid + l * NT, r = e / CPR, c8 = (e % CPR) * 8;
+    int r, c8;
+    stage_rc<D>(tid + l * NT, r, c8);
     if (row0 + r < nrows) {
       t.v[l] = *reinterpret_cast<const bf16x8*>(base + (int64_t)(row0 + r) * rs + c8);
     } else {
@@ -128,10 +153,10 @@ __device__ __forceinline__ void tile_load(TileRegs<R, D, NT>& t, const bf16* bas
 
 template <int R, int D, int NT>
 __device__ __forceinline__ void tile_store(const TileRegs<R, D, NT>& t, bf16* lds, int tid) {
-  constexpr int CPR = D / 8;
 #pragma unroll
   for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
-    const int e = tid + l * NT, r = e / CPR, c8 = (e % CPR) * 8;
+    int r, c8;
+    stage_rc<D>(tid + l * NT, r, c8);
     *reinterpret_cast<bf16x8*>(lds + lo<D>(r, c8)) = t.v[l];
   }
 }
@@ -421,6 +446,7 @@ template <int D>
 struct DkdvCfg {
   static constexpr int kBM = 64;
   static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
+  static constexpr int kPrefetch = DTA_DKDV_PF;  // MFMA ops between a fragment's LDS read and its use
 };
 
 template <int D, bool CAUSAL>
@@ -492,53 +518,80 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     if (CAUSAL && q0s + BM - 1 < kw0) continue;  // all of this wave's keys are after the slice
     const bf16* Qb = Qs[buf];
     const bf16* Db = dOs[buf];
+    // The slice as one software-pipelined stream of MFMA ops, per 32-query tile: NA ops of
+    // S = Q.K^T - LSE/scale / dP = dO.V^T - delta (alternating), the softmax, then NC ops of
+    // dV^T += dO^T.P / dK^T += Q^T.dS.  Every op's LDS fragments are read PF ops ahead into a
+    // register ring and sched_barriers pin that order, so each MFMA waits on reads issued
+    // PF MFMAs earlier (counted lgkmcnt) instead of on reads issued right before it -- the
+    // compiler's own schedule put an lgkmcnt(0) before every MFMA of the D = 128 kernel.
+    constexpr int NA = 2 * NKS, NC = 4 * NDT, NOP = NA + NC, TOT = NQT * NOP;
+    constexpr int PF = DkdvCfg<D>::kPrefetch, RING = PF + 1;
+    bf16x8 ring[RING][2];
+    f32x16 s, dp;
+    bf16x8 pb[2], db[2];
+    auto issue = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, qt = o / NOP, k = o % NOP;
+      bf16x8(&f)[2] = ring[o % RING];
+      if (k == 0) {
+        // row constants of this lane's 16 accumulator rows as the initial accumulators: rows
+        // qt*32 + 8g + 4hh + 0..3 are 4 consecutive floats (s / dp are free: the previous tile's
+        // softmax consumed them)
 #pragma unroll
-    for (int qt = 0; qt < NQT; ++qt) {
-      const int q0 = q0s + qt * 32;
-      // (no per-tile skip: a fully masked tile occurs only in the diagonal slices, and a
-      // branch here splits the slice into blocks the scheduler cannot interleave)
-      // S = Q.K^T - LSE/scale and dP = dO.V^T - delta: rows = queries, cols = keys
-      // row constants of this lane's 16 accumulator rows: rows qt*32 + 8g + 4hh + 0..3 are 4
-      // consecutive floats -- 4 ds_read_b128 per array instead of 16 scalar reads
-      f32x16 s, dp;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int q4 = qt * 32 + 8 * g + 4 * hh;
-        const float4 sv = *reinterpret_cast<const float4*>(&rc[buf][0][q4]);
-        const float4 dv = *reinterpret_cast<const float4*>(&rc[buf][1][q4]);
-        s[4 * g] = sv.x; s[4 * g + 1] = sv.y; s[4 * g + 2] = sv.z; s[4 * g + 3] = sv.w;
-        dp[4 * g] = dv.x; dp[4 * g + 1] = dv.y; dp[4 * g + 2] = dv.z; dp[4 * g + 3] = dv.w;
-      }
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        s = mfma32x32x16(row_frag<D>(Qb, qt * 32 + r32, ks, hh), row_frag<D>(KVs[0], wave * 32 + r32, ks, hh), s);
-        dp = mfma32x32x16(row_frag<D>(Db, qt * 32 + r32, ks, hh), row_frag<D>(KVs[1], wave * 32 + r32, ks, hh), dp);
-      }
-      // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate per element
-      const int dl = CAUSAL && q0 < kw0 + 31 ? key - q0 - 4 * hh : -64;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = fexp2(s[i] * c);
-        if (CAUSAL && dl > mfma32_row(i, 0)) pv = 0.f;
-        s[i] = pv;             // P
-        dp[i] = pv * dp[i];    // dS (unscaled)
-      }
-      // dV^T += dO^T . P ;  dK^T += Q^T . dS
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pb, db;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pb[j] = f2bf(s[8 * st + j]);
-          db[j] = f2bf(dp[8 * st + j]);
-        }
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          dvacc[dt] = mfma32x32x16(tr_frag<D>(Db, qt * 32, dt * 32, st, lane), pb, dvacc[dt]);
-          dkacc[dt] = mfma32x32x16(tr_frag<D>(Qb, qt * 32, dt * 32, st, lane), db, dkacc[dt]);
+        for (int g = 0; g < 4; ++g) {
+          const int q4 = qt * 32 + 8 * g + 4 * hh;
+          const float4 sv = *reinterpret_cast<const float4*>(&rc[buf][0][q4]);
+          const float4 dv = *reinterpret_cast<const float4*>(&rc[buf][1][q4]);
+          s[4 * g] = sv.x; s[4 * g + 1] = sv.y; s[4 * g + 2] = sv.z; s[4 * g + 3] = sv.w;
+          dp[4 * g] = dv.x; dp[4 * g + 1] = dv.y; dp[4 * g + 2] = dv.z; dp[4 * g + 3] = dv.w;
         }
       }
-    }
+      if constexpr (k < NA) {
+        f[0] = row_frag<D>((k & 1) ? Db : Qb, qt * 32 + r32, k >> 1, hh);
+        f[1] = row_frag<D>(KVs[k & 1], wave * 32 + r32, k >> 1, hh);
+      } else {
+        constexpr int cc = k - NA, st = (cc >> 1) / NDT, dt = (cc >> 1) % NDT;
+        f[0] = tr_frag<D>((cc & 1) ? Qb : Db, qt * 32, dt * 32, st, lane);
+      }
+    };
+    auto compute = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, qt = o / NOP, k = o % NOP;
+      const bf16x8(&f)[2] = ring[o % RING];
+      if constexpr (k < NA) {
+        if (k & 1) dp = mfma32x32x16(f[0], f[1], dp);
+        else s = mfma32x32x16(f[0], f[1], s);
+        if constexpr (k == NA - 1) {
+          const int q0 = q0s + qt * 32;
+          // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate
+          const int dl = CAUSAL && q0 < kw0 + 31 ? key - q0 - 4 * hh : -64;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float pv = fexp2(s[i] * c);
+            if (CAUSAL && dl > mfma32_row(i, 0)) pv = 0.f;
+            s[i] = pv;             // P
+            dp[i] = pv * dp[i];    // dS (unscaled)
+          }
+#pragma unroll
+          for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              pb[st][j] = f2bf(s[8 * st + j]);
+              db[st][j] = f2bf(dp[8 * st + j]);
+            }
+        }
+      } else {
+        constexpr int cc = k - NA, st = (cc >> 1) / NDT, dt = (cc >> 1) % NDT;
+        if constexpr (cc & 1) dkacc[dt] = mfma32x32x16(f[0], db[st], dkacc[dt]);
+        else dvacc[dt] = mfma32x32x16(f[0], pb[st], dvacc[dt]);
+      }
+    };
+    static_for<PF>([&](auto oc) { issue(oc); });
+    static_for<TOT>([&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      if constexpr (o + PF < TOT) issue(std::integral_constant<int, o + PF>{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(oc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
   }
   // ---- epilogue: dK = (dK^T)^T * scale, dV = (dV^T)^T ----
   if (key < a.S) {

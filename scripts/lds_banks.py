@@ -7,6 +7,7 @@ reads (ds_read_b64_tr_b16, operand with k = token) and the register-staged
 
     python scripts/lds_banks.py            # search swizzles for D = 64 and 128
     python scripts/lds_banks.py w1img      # persistent-MLP W1 image (csrc/mlp_persistent.hip wb_off)
+    python scripts/lds_banks.py subtiled   # csrc/attention.hip lo<D> + stage_rc (8-row x 32-col subtiles)
 """
 import sys
 import itertools
@@ -139,5 +140,35 @@ def w1img():
         print(f"H={H:3d} WS={WS:3d}: store {st}  tr-read {rd}")
 
 
+def subtiled():
+    """csrc/attention.hip: lo<D> (8-row x 32-column subtiles, chunk ^ ((row >> 2) & 3)) and the
+    staging order stage_rc<D> (a wave = 8 rows x 128 B; an 8-lane group = 2 rows of a subtile)."""
+    for D in (64, 128):
+        def off(row, col, D=D):
+            ch, within = divmod(col * 2, 16)
+            return (D * 16) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3)) + within
+
+        def stage(e, D=D):
+            P = D // 64
+            lane, w = e & 63, e >> 6
+            r = 8 * (w // P) + 2 * ((lane >> 4) & 3) + ((lane >> 2) & 1)
+            return r, 8 * (4 * (2 * (w % P) + ((lane >> 3) & 1)) + (lane & 3))
+
+        worst = {"row": 0, "tr": 0, "st": 0}
+        rows = 128
+        for row0 in range(0, rows, 32):
+            for ks in range(D // 16):
+                worst["row"] = max(worst["row"], cycles(row_read(off, row0, ks), B128_GROUPS, 16, 64))
+            for col0 in range(0, D, 32):
+                for s in range(2):
+                    for sec in (0, 1):
+                        worst["tr"] = max(worst["tr"], cycles(tr_read(off, row0, col0, s, sec), HALVES, 8, 64))
+        for wv in range(rows * D // 8 // 64):
+            worst["st"] = max(worst["st"], cycles([off(*stage(64 * wv + lane)) for lane in range(64)], W128_GROUPS, 16, 32))
+        cover = sorted(stage(e) for e in range(rows * D // 8))
+        assert cover == sorted((r, 8 * c) for r in range(rows) for c in range(D // 8)), "staging order misses chunks"
+        print(f"D={D}: {worst} (conflict-free: row 4, tr 2, st 8)")
+
+
 if __name__ == "__main__":
-    w1img() if sys.argv[1:] == ["w1img"] else main()
+    {"w1img": w1img, "subtiled": subtiled}.get((sys.argv[1:] or [""])[0], main)()
