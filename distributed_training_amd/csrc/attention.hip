@@ -44,6 +44,9 @@
 #ifndef DTA_DKDV_PF
 #define DTA_DKDV_PF 3
 #endif
+#ifndef DTA_DQ_PF
+#define DTA_DQ_PF 3
+#endif
 
 namespace dta {
 
@@ -616,6 +619,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
 template <int D>
 struct DqCfg {
   static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
+  static constexpr int kPrefetch = DTA_DQ_PF;
 };
 
 template <int D, bool CAUSAL, int NW>
@@ -682,35 +686,60 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
     const bool need_mask = CAUSAL && k0 + BN - 1 > q0w;
     // S^T = K.Q^T - LSE/scale, dP^T = V.dO^T - delta: rows = keys, cols = queries.
     // Keys >= S are zero rows of K and V: they add nothing to dQ.
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x16 s = splat16(s_init), dp = splat16(dp_init);
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 ka = row_frag<D>(Kb, t * 32 + r32, ks, hh);
-        const bf16x8 va = row_frag<D>(Vb, t * 32 + r32, ks, hh);
-        s = mfma32x32x16(ka, qf[ks], s);
-        dp = mfma32x32x16(va, df[ks], dp);
+    // Software-pipelined as the dK/dV slice: per 32-key tile NA ops of S^T / dP^T
+    // (alternating), the softmax, NC ops of dQ^T += K^T . dS^T; each op's LDS fragment
+    // is read PF ops ahead into a register ring (sched_barriers pin the order).
+    constexpr int NA = 2 * NKS, NC = 2 * NDT, NOP = NA + NC, TOT = 2 * NOP;
+    constexpr int PF = DqCfg<D>::kPrefetch, RING = PF + 1;
+    bf16x8 ring[RING];
+    f32x16 s, dp;
+    bf16x8 db[2];
+    auto issue = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, t = o / NOP, k = o % NOP;
+      if constexpr (k < NA) {
+        ring[o % RING] = row_frag<D>((k & 1) ? Vb : Kb, t * 32 + r32, k >> 1, hh);
+      } else {
+        constexpr int cc = k - NA;
+        ring[o % RING] = tr_frag<D>(Kb, t * 32, (cc % NDT) * 32, cc / NDT, lane);
       }
-      // key k0 + t*32 + row(i) + 4hh > qrow <=> row(i) > ql
-      const int ql = need_mask ? qrow - k0 - t * 32 - 4 * hh : 64;
+    };
+    auto compute = [&](auto oc) {
+      constexpr int o = decltype(oc)::value, t = o / NOP, k = o % NOP;
+      const bf16x8& f = ring[o % RING];
+      if constexpr (k < NA) {
+        if constexpr (k == 0) {
+          s = splat16(s_init);
+          dp = splat16(dp_init);
+        }
+        if constexpr (k & 1) dp = mfma32x32x16(f, df[k >> 1], dp);
+        else s = mfma32x32x16(f, qf[k >> 1], s);
+        if constexpr (k == NA - 1) {
+          // key k0 + t*32 + row(i) + 4hh > qrow <=> row(i) > ql
+          const int ql = need_mask ? qrow - k0 - t * 32 - 4 * hh : 64;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float pv = fexp2(s[i] * c);
-        if (CAUSAL && mfma32_row(i, 0) > ql) pv = 0.f;
-        dp[i] *= pv;  // dS^T
+          for (int i = 0; i < 16; ++i) {
+            float pv = fexp2(s[i] * c);
+            if (CAUSAL && mfma32_row(i, 0) > ql) pv = 0.f;
+            dp[i] *= pv;  // dS^T
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) db[s2][jj] = f2bf(dp[8 * s2 + jj]);
+        }
+      } else {
+        constexpr int cc = k - NA;
+        dqacc[cc % NDT] = mfma32x32x16(f, db[cc / NDT], dqacc[cc % NDT]);
       }
-      // dQ^T += K^T . dS^T  (K^T by transposed reads; dS^T as it stands)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 db;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) db[jj] = f2bf(dp[8 * s2 + jj]);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-          dqacc[dt] = mfma32x32x16(tr_frag<D>(Kb, t * 32, dt * 32, s2, lane), db, dqacc[dt]);
-      }
-    }
+    };
+    static_for<PF>([&](auto oc) { issue(oc); });
+    static_for<TOT>([&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      if constexpr (o + PF < TOT) issue(std::integral_constant<int, o + PF>{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(oc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
   }
   if (qrow < a.S) {
     bf16* dqr = static_cast<bf16*>(a.dq) + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * D;
