@@ -44,6 +44,9 @@
 #ifndef DTA_DKDV_PF
 #define DTA_DKDV_PF 3
 #endif
+#ifndef DTA_FWD_PF
+#define DTA_FWD_PF 3
+#endif
 #ifndef DTA_DQ_PF
 #define DTA_DQ_PF 3
 #endif
@@ -174,6 +177,7 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 template <int D>
 struct FwdCfg {
   static constexpr int kWavesPerSimd = D == 64 ? 3 : 2;
+  static constexpr int kPrefetch = DTA_FWD_PF;  // D = 64 block compute
 };
 
 // Block id -> (query block, batch, head).  Under the causal mask the work of a
@@ -234,6 +238,94 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   // the barrier after the store waits for LDS only (__syncthreads' fence would also wait
   // for the loads in flight).  D = 128: one set, one block ahead (register budget: the
   // loop below as it was).
+  // One 64-key block against this wave's 32 queries (D = 64), software-pipelined like the
+  // backward kernels: NS ops of S^T = K.Q^T (t = 32-key tile, k-step ks), the online softmax,
+  // NP ops of O^T += V^T.P (t, 16-key half sh, 32-wide d tile dt); each op's LDS fragment is
+  // read PF ops ahead into a register ring and sched_barriers pin the order.  (D = 128 keeps
+  // the compiler's schedule below: at two waves per SIMD in 256 registers the ring spilled
+  // and that forward ran 10-29 % slower.)
+  auto attend = [&](const bf16* Kb, const bf16* Vb, int k0) {
+    constexpr int NS = 2 * NKS, NP = 4 * NDT, TOT = NS + NP;
+    constexpr int PF = FwdCfg<D>::kPrefetch, RING = PF + 1;
+    bf16x8 ring[RING];
+    f32x16 st[2];
+    bf16x8 pb[2][2];
+    auto issue = [&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      if constexpr (o < NS) {
+        ring[o % RING] = row_frag<D>(Kb, (o / NKS) * 32 + r32, o % NKS, hh);
+      } else {
+        constexpr int cc = o - NS, t = cc / (2 * NDT), sh = (cc / NDT) % 2, dt = cc % NDT;
+        ring[o % RING] = tr_frag<D>(Vb, t * 32, dt * 32, sh, lane);
+      }
+    };
+    auto compute = [&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      if constexpr (o < NS) {
+        constexpr int t = o / NKS, ks = o % NKS;
+        if constexpr (ks == 0) st[t] = splat16(0.f);
+        st[t] = mfma32x32x16(ring[o % RING], qf[ks], st[t]);
+        if constexpr (o == NS - 1) {
+          // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
+          const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
+          if (need_mask) {
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) {
+                const int key = k0 + t2 * 32 + mfma32_row(i, lane);
+                if (key >= a.S || (CAUSAL && key > qrow)) st[t2][i] = kNegBig;
+              }
+          }
+          float mblk = st[0][0];
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t2][i]);
+          mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
+          // rescale O and l only when some row's max grew by more than kRescaleThr (as below)
+          if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
+            const float mnew = fmaxf(m, mblk * c);
+            const float alpha = fexp2(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+            m = mnew;
+          }
+          float lsum = 0.f;
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float p = fexp2(__builtin_fmaf(st[t2][i], c, -m));
+              st[t2][i] = p;
+              lsum += p;
+            }
+          l += lsum + __shfl_xor(lsum, 32, kWave);
+#pragma unroll
+          for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) pb[t2][sh][jj] = f2bf(st[t2][8 * sh + jj]);
+        }
+      } else {
+        // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
+        constexpr int cc = o - NS, t = cc / (2 * NDT), sh = (cc / NDT) % 2, dt = cc % NDT;
+        oacc[dt] = mfma32x32x16(ring[o % RING], pb[t][sh], oacc[dt]);
+      }
+    };
+    static_for<PF>([&](auto oc) { issue(oc); });
+    static_for<TOT>([&](auto oc) {
+      constexpr int o = decltype(oc)::value;
+      if constexpr (o + PF < TOT) issue(std::integral_constant<int, o + PF>{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(oc);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
   if constexpr (D == 64) {
   constexpr int AHEAD = 2;
   TileRegs<BN, D, NT> krA, vrA, krB, vrB;
@@ -254,68 +346,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
     }
       const int k0 = j * BN;
       if (CAUSAL && k0 > q0w + 31) return;  // every key of the block is after this wave's queries
-      const bf16* Kb = Ks[buf];
-      const bf16* Vb = Vs[buf];
-      // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
-      f32x16 st[2];
-  #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        st[t] = splat16(0.f);
-  #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) st[t] = mfma32x32x16(row_frag<D>(Kb, t * 32 + r32, ks, hh), qf[ks], st[t]);
-      }
-      // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
-      const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
-      if (need_mask) {
-  #pragma unroll
-        for (int t = 0; t < 2; ++t)
-  #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = k0 + t * 32 + mfma32_row(i, lane);
-            if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
-          }
-      }
-      float mblk = st[0][0];
-  #pragma unroll
-      for (int t = 0; t < 2; ++t)
-  #pragma unroll
-        for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
-      mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
-      // rescale O and l only when some row's max grew by more than kRescaleThr (log2 units):
-      // otherwise m stays and this block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md
-      // T13; the decision precedes every exponentiation of the block, so nothing at the old max
-      // is left unscaled).  The first block always rescales (m starts at -1e30).
-      if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
-        const float mnew = fmaxf(m, mblk * c);
-        const float alpha = fexp2(m - mnew);
-        l *= alpha;
-  #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-  #pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-        m = mnew;
-      }
-      float lsum = 0.f;
-  #pragma unroll
-      for (int t = 0; t < 2; ++t)
-  #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
-          st[t][i] = p;
-          lsum += p;
-        }
-      l += lsum + __shfl_xor(lsum, 32, kWave);
-      // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
-  #pragma unroll
-      for (int t = 0; t < 2; ++t)
-  #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 pb;
-  #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) pb[jj] = f2bf(st[t][8 * s + jj]);
-  #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
-        }
+      attend(Ks[buf], Vs[buf], k0);
   };
   for (int j = 0; j < nblk; j += 2) {
     block(j, krA, vrA);
