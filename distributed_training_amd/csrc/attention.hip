@@ -7,9 +7,8 @@
 // the output projection (no transposes).  GQA: q head h uses kv head
 // h / (H / Hkv).  Causal or full.  D in {64, 128}.
 //
-// Every K/V/Q/dO tile is staged ONCE, row-major, in LDS (row stride D + 32
-// elements: consecutive rows 48 / 16 banks apart, so the 4-row x 2-group
-// pattern of a transposed read is conflict-free) and read both by rows
+// Every K/V/Q/dO tile is staged ONCE in LDS (the subtiled image of lo<D>
+// below, conflict-free for all three access kinds) and read both by rows
 // (ds_read_b128, MFMA operands whose k index is the head dim) and by columns
 // with the gfx950 hardware-transpose read ds_read_b64_tr_b16 (operands whose
 // k index is the key / query position).  Tiles are double-buffered in LDS and
@@ -24,13 +23,14 @@
 //   row-major V tile through transposed reads).
 // BACKWARD, two atomic-free kernels (deterministic, no fp32 dQ buffer):
 //   dK/dV (workgroup = 4 waves x 32 keys of one (batch, kv head)): keys on the
-//     lanes, K/V fragments in registers; per 32-query slice (all q heads of
-//     the group) S = Q.K^T and dP = dO.V^T start from the row constants
+//     lanes, the workgroup's K/V staged once in LDS; per 64-query slice (all q
+//     heads of the group) S = Q.K^T and dP = dO.V^T start from the row constants
 //     -LSE/scale and -delta as initial accumulators, P = exp2(c S),
 //     dS = P dP; dV^T += dO^T.P and dK^T += Q^T.dS take P / dS as the B
 //     operand as they stand (dO^T / Q^T by transposed reads).
-//   dQ (workgroup = 4 waves x 32 queries): the forward's orientation; S^T and
-//     dP^T recomputed per 64-key block, dQ^T += K^T . dS^T.
+//   dQ (workgroup = 4 waves x 32 queries; runs FIRST): the forward's orientation;
+//     delta = rowsum(dO * O) from its dO fragments and one read of O, stored for
+//     dK/dV; S^T and dP^T recomputed per 64-key block, dQ^T += K^T . dS^T.
 //   The 10 B H S^2 D FLOPs of a fused backward become 14 (S and dP are
 //     computed twice) but the dQ float atomics -- bound at ~1.3 TB/s chip-wide
 //     (MI355X_MICROARCH.md 'Global float atomics'), which dominated the fused
@@ -448,29 +448,6 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
 }
 
 // ------------------------------------------------------------------ backward
-// delta[b,h,q] = sum_d dO * O   (8 threads per (b, q, h) row)
-template <int D>
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(AttnArgs a) {
-  const int tid = threadIdx.x;
-  const int64_t row = (int64_t)blockIdx.x * 32 + (tid >> 3);
-  const int64_t total = (int64_t)a.B * a.S * a.H;
-  if (row >= total) return;
-  const int h = row % a.H;
-  const int64_t bq = row / a.H;
-  const int q = bq % a.S, b = bq / a.S;
-  const bf16* o = static_cast<const bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)q * a.o_ss + (int64_t)h * D;
-  const bf16* d = static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)q * a.do_ss + (int64_t)h * D;
-  float acc = 0.f;
-  for (int c = (tid & 7) * 8; c < D; c += 64) {
-    const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + c);
-    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(d + c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += bf2f(ov[j]) * bf2f(dv[j]);
-  }
-#pragma unroll
-  for (int off = 4; off > 0; off >>= 1) acc += __shfl_xor(acc, off, kWave);
-  if ((tid & 7) == 0) a.delta[((int64_t)b * a.H + h) * a.S + q] = acc;
-}
 
 // Query rows per slice of the dK/dV kernel: 64 (two 32-row MFMA tiles) halves
 // the barriers per MFMA and doubles the compute behind each slice's prefetch
@@ -689,9 +666,24 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
       for (int j = 0; j < 8; ++j) qf[ks][j] = df[ks][j] = f2bf(0.f);
     }
   }
+  // delta = rowsum(dO * O) of this lane's query row, from the dO fragments already in registers
+  // and the same fragments of O (each half-wave holds half the row: one lane^32 exchange); written
+  // for the dK/dV kernel, which runs after this one (no separate delta pass)
+  float dsum = 0.f;
+  if (qrow < a.S) {
+    const bf16* obase = static_cast<const bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * D;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(obase + ks * 16 + hh * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += bf2f(ov[j]) * bf2f(df[ks][j]);
+    }
+  }
+  dsum += __shfl_xor(dsum, 32, kWave);
   const int64_t ri = ((int64_t)b * a.H + h) * a.S + qrow;
+  if (qrow < a.S && hh == 0) a.delta[ri] = dsum;
   const float s_init = qrow < a.S ? -a.lse[ri] / a.scale : kNegBig;
-  const float dp_init = qrow < a.S ? -a.delta[ri] : 0.f;
+  const float dp_init = qrow < a.S ? -dsum : 0.f;
   f32x16 dqacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dqacc[dt] = splat16(0.f);
@@ -834,18 +826,17 @@ static void dq_launch(const AttnArgs& a, bool causal, hipStream_t st) {
 
 template <int D>
 static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
-  const int64_t rows = (int64_t)a.B * a.S * a.H;
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, st, a);
+  // dQ first: it computes delta = rowsum(dO * O) for its query rows (one pass over O that the
+  // old separate delta kernel made) and stores it for the dK/dV kernel
+  if constexpr (D == 64) {
+    if (dq_waves(a, D) == 8) dq_launch<D, 8>(a, causal, st);
+    else dq_launch<D, 4>(a, causal, st);
+  } else {
+    dq_launch<D, 4>(a, causal, st);
+  }
   dim3 gkv((unsigned)(((a.S + 127) / 128) * a.B * a.Hkv));
   if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
-  if constexpr (D == 64) {
-    if (dq_waves(a, D) == 8) {
-      dq_launch<D, 8>(a, causal, st);
-      return hipGetLastError();
-    }
-  }
-  dq_launch<D, 4>(a, causal, st);
   return hipGetLastError();
 }
 

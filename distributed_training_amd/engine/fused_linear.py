@@ -20,7 +20,7 @@ order exactly (indices uploaded per epoch into a device ring).
 from __future__ import annotations
 
 import logging
-from typing import Any, List, Optional
+from typing import Any, Dict, List, Optional
 
 import torch
 import torch.nn as nn
@@ -49,10 +49,6 @@ def linear_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, d
     g = optimizer.param_groups[0]
     if "momentum" not in g or "betas" in g:
         return "optimizer is not SGD"
-    if g.get("momentum", 0):
-        # the program keeps its momentum in its own buffer, which the optimizer's state (and so a
-        # checkpoint's OPTIM_STATE) would never see; the reference's SGD has none (distributed_trainer.py:200)
-        return "SGD with momentum runs on the generic engine path"
     C, I = module.weight.shape
     if not native().linear_step_supported(I, C, loader.batch_size, False):
         return "shape outside the fused kernel's limits"
@@ -107,6 +103,11 @@ class FusedLinearProgram:
         C, I = self.C, self.I
         return {"weight": self.P[:C * I].view(C, I), "bias": self.P[C * I:]}
 
+    def _mom_views(self) -> Dict[str, torch.Tensor]:
+        assert self.M is not None
+        C, I = self.C, self.I
+        return {"weight": self.M[:C * I].view(C, I), "bias": self.M[C * I:]}
+
     @torch.no_grad()
     def load_from_module(self) -> None:
         v = self._views()
@@ -114,6 +115,17 @@ class FusedLinearProgram:
             tag = getattr(p, "_dta_flat", None)  # fp32 master of the DDP engine, if it keeps one
             src = tag[0].master_view(tag[1]) if tag is not None else p.detach()
             v[name].copy_(src.float())
+        if self.M is not None:
+            # the momentum lives in the program's buffer while it runs and in the optimizer's
+            # state (so in a checkpoint's OPTIM_STATE) between runs: a resumed run continues it
+            mv = self._mom_views()
+            started = False
+            for name, p in self.module.named_parameters():
+                buf = self.opt.state.get(p, {}).get("momentum_buffer")
+                if buf is not None:
+                    mv[name].copy_(buf.reshape(mv[name].shape).float())
+                    started = True
+            self.flags[0] = int(started)
 
     @torch.no_grad()
     def flush(self) -> None:
@@ -132,6 +144,10 @@ class FusedLinearProgram:
             if tag is not None:
                 tag[0].master_view(tag[1]).copy_(v[name])
             p.copy_(v[name].to(p.dtype))
+        if self.M is not None and int(self.flags[0].item()):
+            mv = self._mom_views()
+            for name, p in self.module.named_parameters():
+                self.opt.state[p]["momentum_buffer"] = mv[name].reshape(p.shape).clone()
 
     # ------------------------------------------------------------ stepping
     def _kernel(self, nsteps: int, g_out: bool) -> None:

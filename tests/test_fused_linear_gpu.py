@@ -35,6 +35,7 @@ def _reference(model, X, T, batches, loss, sgd_kw):
         for p, *gs in zip(ref.parameters(), *grads):
             p.grad = sum(gs) / len(gs)
         opt.step()
+    ref.opt = opt
     return ref, losses
 
 
@@ -82,6 +83,25 @@ def test_linear_program_matches_reference_loop(loss, out_dim, sgd_kw):
     torch.testing.assert_close(got, torch.tensor(losses), rtol=2e-5, atol=2e-6)
     torch.testing.assert_close(model.weight.detach().cpu(), ref.weight.detach(), rtol=2e-5, atol=2e-6)
     torch.testing.assert_close(model.bias.detach().cpu(), ref.bias.detach(), rtol=2e-5, atol=2e-6)
+    if sgd_kw.get("momentum"):
+        # the program's momentum reaches the optimizer state (checkpoint OPTIM_STATE) ...
+        for p, q in zip(model.parameters(), ref.parameters()):
+            torch.testing.assert_close(opt.state[p]["momentum_buffer"].cpu(), ref.opt.state[q]["momentum_buffer"],
+                                       rtol=2e-5, atol=2e-6)
+        # ... and a new program (a resumed run) continues it: one more epoch matches the reference's
+        prog2 = FusedLinearProgram(model, opt, loader, comm, loss=loss)
+        prog2.run_epoch(3)
+        prog2.store_to_module()
+        torch.cuda.synchronize()
+        sampler.set_epoch(3)
+        idx = sampler.epoch_indices()
+        for i in range(0, len(idx), 32):
+            ref.zero_grad()
+            out = ref(ds.X[idx[i:i + 32]])
+            t = ds.Y[idx[i:i + 32]]
+            (F.cross_entropy(out, t) if loss == "cross_entropy" else F.mse_loss(out, t)).backward()
+            ref.opt.step()
+        torch.testing.assert_close(model.weight.detach().cpu(), ref.weight.detach(), rtol=5e-5, atol=5e-6)
 
 
 def test_reference_default_is_a_noop_step():
