@@ -573,11 +573,16 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
         if constexpr (k == NA - 1) {
           const int q0 = q0s + qt * 32;
           // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate
-          const int dl = CAUSAL && q0 < kw0 + 31 ? key - q0 - 4 * hh : -64;
+          // (a wave-uniform branch around the compare / select: only the diagonal slices pay them)
+          if (CAUSAL && q0 < kw0 + 31) {
+            const int dl = key - q0 - 4 * hh;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (dl > mfma32_row(i, 0)) s[i] = kNegBig;  // exp2 -> P = 0
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float pv = fexp2(s[i] * c);
-            if (CAUSAL && dl > mfma32_row(i, 0)) pv = 0.f;
+            const float pv = fexp2(s[i] * c);
             s[i] = pv;             // P
             dp[i] = pv * dp[i];    // dS (unscaled)
           }
@@ -738,11 +743,15 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
         else s = mfma32x32x16(f, qf[k >> 1], s);
         if constexpr (k == NA - 1) {
           // key k0 + t*32 + row(i) + 4hh > qrow <=> row(i) > ql
-          const int ql = need_mask ? qrow - k0 - t * 32 - 4 * hh : 64;
+          if (need_mask) {  // wave-uniform: the diagonal blocks only
+            const int ql = qrow - k0 - t * 32 - 4 * hh;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (mfma32_row(i, 0) > ql) s[i] = kNegBig;  // exp2 -> P = 0
+          }
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float pv = fexp2(s[i] * c);
-            if (CAUSAL && mfma32_row(i, 0) > ql) pv = 0.f;
+            const float pv = fexp2(s[i] * c);
             dp[i] *= pv;  // dS^T
           }
 #pragma unroll
