@@ -70,8 +70,11 @@ def _headers_digest() -> str:
 # attention.hip: MFMA accumulators in the VGPR form.  The default heuristic picks the AGPR
 # form for the D = 128 backward kernels (one wave per SIMD, 512 registers) and then shuttles
 # the dK/dV / dQ accumulators between the two files every loop iteration (868 / 416
-# v_accvgpr moves per kernel vs 338 / 154 in the VGPR form).
-_PER_FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# v_accvgpr moves per kernel vs 338 / 154 in the VGPR form).  No SLP vectorisation: it packs
+# the softmax's f32 multiplies into v_pk_mul_f32 on misaligned register pairs and re-aligns them
+# with v_mov / v_alignbit / v_perm (65-100 extra VALU ops per kernel in MFMA gaps; the guide's
+# "packed f32 VALU beside MFMAs is an anti-lever").
+_PER_FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _compile_cmds() -> List[tuple]:
