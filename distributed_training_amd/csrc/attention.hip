@@ -60,6 +60,17 @@ constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// x[lane] (max | +) x[lane ^ 32] by v_permlane32_swap: a VALU op.  __shfl_xor goes through
+// ds_bpermute, whose lgkmcnt(0) wait also waits for every fragment read the pipeline has in flight.
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // f(integral_constant<int, I>) for I = 0 .. N-1, unrolled at compile time (register-ring
 // indices stay constants: a runtime index would put the ring in scratch)
 template <int N, int I = 0, typename F>
@@ -269,20 +280,21 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
           // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
           const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
           if (need_mask) {
+            // key k0 + t*32 + row(i) + 4hh is masked past the sequence or (causal) past the
+            // query: both are "block-relative row > lim", one compare against an immediate
+            const int lim = min(a.S - 1, CAUSAL ? qrow : a.S) - k0 - 4 * hh;
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-              for (int i = 0; i < 16; ++i) {
-                const int key = k0 + t2 * 32 + mfma32_row(i, lane);
-                if (key >= a.S || (CAUSAL && key > qrow)) st[t2][i] = kNegBig;
-              }
+              for (int i = 0; i < 16; ++i)
+                if (t2 * 32 + mfma32_row(i, 0) > lim) st[t2][i] = kNegBig;
           }
           float mblk = st[0][0];
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
             for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t2][i]);
-          mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
+          mblk = xor32_max(mblk);
           // rescale O and l only when some row's max grew by more than kRescaleThr (as below)
           if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
             const float mnew = fmaxf(m, mblk * c);
@@ -303,7 +315,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
               st[t2][i] = p;
               lsum += p;
             }
-          l += lsum + __shfl_xor(lsum, 32, kWave);
+          l += xor32_sum(lsum);
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
@@ -380,20 +392,19 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
       // ---- mask, online softmax (per-lane query row; scale folded into one FMA) ----
       const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
       if (need_mask) {
+        const int lim = min(a.S - 1, CAUSAL ? qrow : a.S) - k0 - 4 * hh;  // as attend()
   #pragma unroll
         for (int t = 0; t < 2; ++t)
   #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = k0 + t * 32 + mfma32_row(i, lane);
-            if (key >= a.S || (CAUSAL && key > qrow)) st[t][i] = kNegBig;
-          }
+          for (int i = 0; i < 16; ++i)
+            if (t * 32 + mfma32_row(i, 0) > lim) st[t][i] = kNegBig;
       }
       float mblk = st[0][0];
   #pragma unroll
       for (int t = 0; t < 2; ++t)
   #pragma unroll
         for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
-      mblk = fmaxf(mblk, __shfl_xor(mblk, 32, kWave));
+      mblk = xor32_max(mblk);
       // rescale O and l only when some row's max grew by more than kRescaleThr (log2 units):
       // otherwise m stays and this block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md
       // T13; the decision precedes every exponentiation of the block, so nothing at the old max
@@ -417,7 +428,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
           st[t][i] = p;
           lsum += p;
         }
-      l += lsum + __shfl_xor(lsum, 32, kWave);
+      l += xor32_sum(lsum);
       // ---- O^T += V^T . P  (V^T fragments by transposed reads of the V tile) ----
   #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -458,6 +469,7 @@ struct DkdvCfg {
   static constexpr int kBM = 64;
   static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
   static constexpr int kPrefetch = DTA_DKDV_PF;  // MFMA ops between a fragment's LDS read and its use
+  static constexpr int kAhead = D == 64 ? 2 : 1;   // slices between a tile's global load and its LDS store
 };
 
 template <int D, bool CAUSAL>
@@ -503,30 +515,41 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   const int qstart = CAUSAL ? kblk0 : 0;
   const int nslice = (a.S - qstart + BM - 1) / BM;
   const int total = nslice * group;
-  TileRegs<BM, D, 256> qr, dr;
-  float rcv = 0.f;
-  auto load = [&](int it) {
+  // Q / dO tiles and the row constants of a slice are register-staged.  D = 64: TWO register
+  // sets, each slice loaded two slices before its LDS store (one slice of MFMAs -- ~0.4 us --
+  // does not cover the loads' latency; the forward's D = 64 path does the same), and the
+  // barrier after the store waits for LDS only (__syncthreads' fence would also wait for the
+  // other set's loads in flight).  D = 128: one set, one slice ahead (register budget).
+  constexpr int AHEAD = DkdvCfg<D>::kAhead;
+  struct Stage {
+    TileRegs<BM, D, 256> q, d;
+    float rc = 0.f;
+  };
+  Stage sA, sB;
+  auto load = [&](int it, Stage& st) {
     const int hq = hk * group + it / nslice;
     const int q0 = qstart + (it % nslice) * BM;
-    tile_load(qr, static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, q0, a.S, tid);
-    tile_load(dr, static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, q0, a.S, tid);
+    tile_load(st.q, static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, q0, a.S, tid);
+    tile_load(st.d, static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, q0, a.S, tid);
     if (tid < 2 * BM) {
       const int qq = q0 + tid % BM;
       const int64_t ri = ((int64_t)b * a.H + hq) * a.S + qq;
-      if (tid < BM) rcv = qq < a.S ? -a.lse[ri] * inv_scale : kNegBig;  // q >= S: P = 0
-      else rcv = qq < a.S ? -a.delta[ri] : 0.f;
+      if (tid < BM) st.rc = qq < a.S ? -a.lse[ri] * inv_scale : kNegBig;  // q >= S: P = 0
+      else st.rc = qq < a.S ? -a.delta[ri] : 0.f;
     }
   };
-  load(0);
-  for (int it = 0; it < total; ++it) {
+  load(0, sA);
+  if (AHEAD == 2 && total > 1) load(1, sB);
+  auto slice_it = [&](int it, Stage& cur) {
     const int buf = it & 1;
-    tile_store(qr, Qs[buf], tid);
-    tile_store(dr, dOs[buf], tid);
-    if (tid < 2 * BM) rc[buf][tid / BM][tid % BM] = rcv;
-    __syncthreads();
-    if (it + 1 < total) load(it + 1);
+    tile_store(cur.q, Qs[buf], tid);
+    tile_store(cur.d, dOs[buf], tid);
+    if (tid < 2 * BM) rc[buf][tid / BM][tid % BM] = cur.rc;
+    if constexpr (AHEAD == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+    if (it + AHEAD < total) load(it + AHEAD, cur);
     const int q0s = qstart + (it % nslice) * BM;
-    if (CAUSAL && q0s + BM - 1 < kw0) continue;  // all of this wave's keys are after the slice
+    if (CAUSAL && q0s + BM - 1 < kw0) return;  // all of this wave's keys are after the slice
     const bf16* Qb = Qs[buf];
     const bf16* Db = dOs[buf];
     // The slice as one software-pipelined stream of MFMA ops, per 32-query tile: NA ops of
@@ -608,6 +631,14 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       compute(oc);
       __builtin_amdgcn_sched_barrier(0);
     });
+  };
+  if constexpr (AHEAD == 2) {
+    for (int it = 0; it < total; it += 2) {
+      slice_it(it, sA);
+      if (it + 1 < total) slice_it(it + 1, sB);
+    }
+  } else {
+    for (int it = 0; it < total; ++it) slice_it(it, sA);
   }
   // ---- epilogue: dK = (dK^T)^T * scale, dV = (dV^T)^T ----
   if (key < a.S) {
@@ -633,6 +664,7 @@ template <int D>
 struct DqCfg {
   static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
   static constexpr int kPrefetch = DTA_DQ_PF;
+  static constexpr int kAhead = D == 64 ? 2 : 1;
 };
 
 template <int D, bool CAUSAL, int NW>
@@ -684,7 +716,7 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
       for (int j = 0; j < 8; ++j) dsum += bf2f(ov[j]) * bf2f(df[ks][j]);
     }
   }
-  dsum += __shfl_xor(dsum, 32, kWave);
+  dsum = xor32_sum(dsum);
   const int64_t ri = ((int64_t)b * a.H + h) * a.S + qrow;
   if (qrow < a.S && hh == 0) a.delta[ri] = dsum;
   const float s_init = qrow < a.S ? -a.lse[ri] / a.scale : kNegBig;
@@ -695,20 +727,30 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
 
   const int kv_end = CAUSAL ? min(qb * QB + QB, a.S) : a.S;
   const int nblk = (kv_end + BN - 1) / BN;
-  TileRegs<BN, D, NT> kr, vr;
-  tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
-  tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
-  for (int j = 0; j < nblk; ++j) {
+  // K / V register staging as the dK/dV kernel's Q / dO: two sets two blocks ahead at D = 64
+  constexpr int AHEAD = DqCfg<D>::kAhead;
+  struct Stage {
+    TileRegs<BN, D, NT> k, v;
+  };
+  Stage sA, sB;
+  tile_load(sA.k, kbase, a.k_ss, 0, a.S, tid);
+  tile_load(sA.v, vbase, a.v_ss, 0, a.S, tid);
+  if (AHEAD == 2 && nblk > 1) {
+    tile_load(sB.k, kbase, a.k_ss, BN, a.S, tid);
+    tile_load(sB.v, vbase, a.v_ss, BN, a.S, tid);
+  }
+  auto block_it = [&](int j, Stage& cur) {
     const int buf = j & 1;
-    tile_store(kr, Ks[buf], tid);
-    tile_store(vr, Vs[buf], tid);
-    __syncthreads();
-    if (j + 1 < nblk) {
-      tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
-      tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
+    tile_store(cur.k, Ks[buf], tid);
+    tile_store(cur.v, Vs[buf], tid);
+    if constexpr (AHEAD == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+    if (j + AHEAD < nblk) {
+      tile_load(cur.k, kbase, a.k_ss, (j + AHEAD) * BN, a.S, tid);
+      tile_load(cur.v, vbase, a.v_ss, (j + AHEAD) * BN, a.S, tid);
     }
     const int k0 = j * BN;
-    if (CAUSAL && k0 > q0w + 31) continue;
+    if (CAUSAL && k0 > q0w + 31) return;
     const bf16* Kb = Ks[buf];
     const bf16* Vb = Vs[buf];
     const bool need_mask = CAUSAL && k0 + BN - 1 > q0w;
@@ -772,6 +814,14 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
       compute(oc);
       __builtin_amdgcn_sched_barrier(0);
     });
+  };
+  if constexpr (AHEAD == 2) {
+    for (int j = 0; j < nblk; j += 2) {
+      block_it(j, sA);
+      if (j + 1 < nblk) block_it(j + 1, sB);
+    }
+  } else {
+    for (int j = 0; j < nblk; ++j) block_it(j, sA);
   }
   if (qrow < a.S) {
     bf16* dqr = static_cast<bf16*>(a.dq) + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * D;

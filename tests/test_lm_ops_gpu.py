@@ -18,7 +18,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal", [(2, 256, 4, 4, 64, True), (1, 200, 4, 2, 128, True),
                                                  (2, 128, 2, 2, 64, False), (1, 333, 8, 1, 64, True),
-                                                 (1, 1024, 2, 2, 128, True)])
+                                                 (1, 1024, 2, 2, 128, True), (1, 320, 4, 2, 128, False),
+                                                 (1, 600, 4, 2, 64, False)])
 @pytest.mark.parametrize("fwd_waves", ["4", "8"])
 def test_flash_attention_fwd_bwd(B, S, H, Hkv, D, causal, fwd_waves, monkeypatch):
     monkeypatch.setenv("DTA_ATTN_FWD_WAVES", fwd_waves)  # both forward workgroup shapes
