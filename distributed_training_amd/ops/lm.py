@@ -291,6 +291,10 @@ def _save_cache() -> None:
 # implementation ids in _GEMM_CHOICE: 0 = hipBLASLt (torch), 1..3 = csrc/gemm_bf16.hip tile (round-2
 # kernel, 32-deep stages; kept for K % 64 != 0), 10 + t = csrc/gemm_k64.hip tile t (64-deep stages)
 K64 = 10
+# csrc/gemm_k64.hip tiles the dispatcher times: 5 / 6 / 8 = the 8-wave 256x256 / 256x128 / 128x256
+# tiles with the two-phase K loop (3-11 % faster than their four-phase forms 1 / 2 / 4 at every
+# GPT-2 and Llama shape: profiles/gemm_k64_vs_hipblaslt.txt), 3 / 7 = 128x128 in both forms
+K64_TILES = (5, 6, 3, 7, 8)
 # a hand-written candidate wins a shape when it is at most this much slower than the library (1.0: the
 # faster one; a 2 % preference measured 0.25 ms/step slower on the GPT-2 DDP step, same-box A/B)
 _PREFER_DTA = 1.0
@@ -304,7 +308,7 @@ def _k64_on() -> bool:
 def gemm_candidates(M: int, N: int, K: int) -> list:
     """Hand-written GEMM implementations that cover an M x N x K problem (ids as in _GEMM_CHOICE)."""
     C = native()
-    k64 = [K64 + t for t in (1, 2, 3, 4) if _k64_on() and C.gemm64_tile(M, N, K, t)]
+    k64 = [K64 + t for t in K64_TILES if _k64_on() and C.gemm64_tile(M, N, K, t)]
     if k64:
         return k64
     return [t for t in (1, 2, 3) if C.gemm_tile(M, N, K, t)]
@@ -405,7 +409,7 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     impl = 0
     if _gemm_ok(x2, w, b) and N % 8 == 0:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in (1, 2, 3, 4):
+        for t in K64_TILES:
             if _k64_on() and C.gemm64_tile(M, N, K, t):
                 cands[K64 + t] = (lambda t=t: run_k64(t))
         impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands)

@@ -78,7 +78,7 @@ def main():
                 if old_t:
                     fns[f"r2_t{old_t}"] = (lambda t=old_t: old(t))
                 errs = {}
-                for t in (1, 2, 3, 4):
+                for t in range(1, 9):  # 5-8: tiles 1-4 with the two-phase K loop
                     if C.gemm64_tile(M, N, K, t):
                         fns[f"k64_t{t}"] = (lambda t=t: new(t))
                         errs[f"k64_t{t}"] = float(f"{relerr(new(t), ref):.2e}")
@@ -102,7 +102,7 @@ def main():
                     return hh, C.gelu_fwd(hh, -1)
 
                 fns = {"torch+gelu_fwd": lib_fwd}
-                for t in (1, 2, 3, 4):
+                for t in range(1, 9):
                     if C.gemm64_tile(T, nout, nin, t):
                         fns[f"k64_t{t}_dual"] = (lambda t=t: C.gemm64(x, w, bias=bias, epi=2, out=h, out2=a, tile=t))
                 times = bench(fns, rounds)
@@ -112,7 +112,7 @@ def main():
                 dy2 = torch.randn(T, nin, device="cuda").bfloat16()
                 fns = {"torch+gelu_bwd": lambda: C.gelu_bwd(torch.mm(dy2, w2), h, -1),
                        "r2_dgelu": lambda: C.gemm(dy2, w2, False, True, None, False, 1.0, None, 16, h, 0)}
-                for t in (1, 2, 3, 4):
+                for t in range(1, 9):
                     if C.gemm64_tile(T, nout, nin, t):
                         fns[f"k64_t{t}_dgelu"] = (lambda t=t: C.gemm64(dy2, w2, False, True, epi=16, res=h, tile=t))
                 times = bench(fns, rounds)

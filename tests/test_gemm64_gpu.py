@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 
 LAYOUTS = [(False, False), (False, True), (True, True), (True, False)]
 TILES = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 256)}
+TILES.update({t + 4: TILES[t] for t in (1, 2, 3, 4)})  # 5-8: the two-phase K loop
 
 
 def _ops(M, N, K, a_t, b_t, gen, scale=1.0):
@@ -30,7 +31,7 @@ def _close(got, want, K):
 
 
 @pytest.mark.parametrize("a_t,b_t", LAYOUTS)
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm64_exact_small_integers(a_t, b_t, tile):
     """Small integers: every product and partial sum is exact in fp32 -- any fragment-order,
     swizzle or pipeline-staging mistake shows as a mismatch (asymmetric operands)."""
@@ -49,7 +50,8 @@ def test_gemm64_exact_small_integers(a_t, b_t, tile):
 
 @pytest.mark.parametrize("a_t,b_t", LAYOUTS)
 @pytest.mark.parametrize("tile,M,N,K", [(1, 512, 512, 256), (2, 512, 384, 192), (3, 384, 256, 1088),
-                                        (4, 256, 768, 768), (0, 1024, 768, 768)])
+                                        (4, 256, 768, 768), (0, 1024, 768, 768), (5, 512, 512, 256),
+                                        (7, 384, 256, 1088), (8, 256, 768, 768)])
 def test_gemm64_random(a_t, b_t, tile, M, N, K):
     from distributed_training_amd.ops import native
 
@@ -62,7 +64,7 @@ def test_gemm64_random(a_t, b_t, tile, M, N, K):
     _close(got, want, K)
 
 
-@pytest.mark.parametrize("tile", [1, 3])
+@pytest.mark.parametrize("tile", [1, 3, 7])
 def test_gemm64_epilogues(tile):
     from distributed_training_amd.ops import native
 
