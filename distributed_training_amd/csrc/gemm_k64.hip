@@ -85,6 +85,9 @@ struct Args {
   int tiles_m, tiles_n;
   float alpha;
   int epi;
+#ifdef DTA_K64_STAMP
+  unsigned long long* stamps;  // diagnostic build only: per-wave cycle sums of the two-phase loop's segments
+#endif
 };
 
 // GELU (tanh form) as x * sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of tanhf
@@ -107,6 +110,28 @@ __device__ __forceinline__ void vm_wait() {
 }
 __device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
+
+#ifdef DTA_K64_STAMP
+// s_memtime with its lgkmcnt(0) in ONE statement (cdna_hip_programming.md "In-kernel stamps"); the
+// diagnostic build's run time is never quoted, only the segment shares
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define K64_STAMP(i)                \
+  do {                              \
+    const unsigned long long n_ = stamp_now(); \
+    seg[i] += n_ - t_prev;          \
+    t_prev = n_;                    \
+  } while (0)
+#else
+#define K64_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 
 __device__ __forceinline__ bf16x4 tr4(const char* lds, int byte_off) {
   typedef short s4 __attribute__((ext_vector_type(4)));
@@ -327,28 +352,49 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   if constexpr (STAG) {
     if (wr == 1) bar();
   }
+#ifdef DTA_K64_STAMP
+  unsigned long long seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_prev = stamp_now();
+#endif
   for (int kt = 0; kt < nk; ++kt) {
     read_a(af, kt, 0);
     read_b(b0, kt, 0);
     read_b(b1, kt, 1);
     dma_a(1, kt + 1);
+    K64_STAMP(0);
     bar();
+    K64_STAMP(1);
     lgkm0();
     mma(af, b0, 0, 0);
     mma(af, b1, 0, 1);
+    K64_STAMP(2);
     vm_wait<2 * LA + 2 * LB>();  // bottom (t)
+    K64_STAMP(3);
     bar();
+    K64_STAMP(4);
     read_a(af, kt, 1);
     dma_a(0, kt + 2);
     dma_b(0, kt + 2);
     dma_b(1, kt + 2);
+    K64_STAMP(5);
     bar();
+    K64_STAMP(6);
     lgkm0();
     mma(af, b1, 1, 1);
     mma(af, b0, 1, 0);
+    K64_STAMP(7);
     vm_wait<2 * LA + 2 * LB>();  // top, left, right (t+1)
+    K64_STAMP(8);
     bar();
+    K64_STAMP(9);
   }
+#ifdef DTA_K64_STAMP
+  if (lane == 0) {
+    unsigned long long* o = g.stamps + ((int64_t)blockIdx.x * NW + wave) * 10;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) o[i] = seg[i];
+  }
+#endif
   }
   vm_wait<0>();  // the tail's dummy DMAs land before the workgroup's LDS is released
   if constexpr (STAG) {
@@ -459,6 +505,10 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   return best && best != 3 ? best + k64::kTiles : best;
 }
 
+#ifdef DTA_K64_STAMP
+unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k64_stamps.hip)
+#endif
+
 // epi: 0 none, 2 GELU (c2 != nullptr: c = pre-activation, c2 = gelu), 16 x gelu'(res), 32 + res
 hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
                         int64_t ldc, void* c2, int64_t ldc2, float* c32, int M, int N, int K, float alpha,
@@ -484,6 +534,9 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   g.K = K;
   g.alpha = alpha;
   g.epi = epi;
+#ifdef DTA_K64_STAMP
+  g.stamps = dta_k64_stamp_buf;
+#endif
   // K-loop phases per 64-deep stage: 4, or 2 for the ids past kTiles
   const int ph = tile > k64::kTiles ? 2 : 4;
   if (tile > k64::kTiles) tile -= k64::kTiles;
