@@ -54,8 +54,8 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   std::vector<unsigned long long> h((size_t)blocks * nw * 10);
   CK(hipMemcpy(h.data(), dta_k64_stamp_buf, h.size() * 8, hipMemcpyDeviceToHost));
-  const char* names[10] = {"S1 read+dma issue (+read wait)", "S1 barrier", "S1 32 mfma", "S1 vmcnt", "S1 end barrier",
-                           "S3 read+dma issue (+read wait)", "S3 barrier", "S3 32 mfma", "S3 vmcnt", "S3 end barrier"};
+  const char* names[10] = {"S1 read+dma issue (+read wait)", "S1 lgkm+vmcnt", "S1 barrier", "S1 32 mfma", "S1 end barrier",
+                           "S3 read+dma issue (+read wait)", "S3 lgkm+vmcnt", "S3 barrier", "S3 32 mfma", "S3 end barrier"};
   for (int grp = 0; grp < 2; ++grp) {
     double sum[10] = {0}, tot = 0;
     for (int bl = 0; bl < blocks; ++bl)
