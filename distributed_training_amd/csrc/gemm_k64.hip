@@ -60,6 +60,13 @@
 //    scheduling freedom.)
 //  * Tile order: XCD-aware bijective remap, then groups of 8 tile rows walked
 //    column by column (L2 panel reuse on each XCD).
+//  * Measured and dropped (round 3): a 4-wave 256x256 tile, one wave per SIMD with a 128x128 output each
+//    (256 AGPR accumulators, two thirds of the LDS read bytes per FLOP), 32-deep stages in a 4- or
+//    5-buffer LDS ring, the next stage's fragment reads and the DMA interleaved between the 64 MFMAs of
+//    a stage: 989-1145 TF/s vs 1303-1413 for the 8-wave two-phase tile at Llama shapes.  In-kernel stamps
+//    put 88 % of its stage in the MFMA stream at ~22 cycles per 16-cycle MFMA: the LDS-DMA pieces'
+//    issue cost (8 per stage, ~60 cycles each: MI355X_MICROARCH.md) lands on the only wave of the
+//    SIMD, where the 8-wave form hands it to the partner wave.
 #include "common.h"
 
 #include <cstdlib>
@@ -462,118 +469,6 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   }
 }
 
-// ======================================================================================================
-// W4: 256 x 256 tile, FOUR waves (one per SIMD, 2 x 2), each wave a 128 x 128 output (256 accumulator
-// registers) -- two thirds of the 8-wave tiles' LDS read bytes per FLOP (scripts/k64_stamps.hip: in the
-// 8-wave two-phase loop the read phase plus its barrier is as long as the partner's 32-MFMA cluster, so
-// the MFMA pipe idles ~30 % of the loop).  A and B K-major (the forward x W^T).
-//  * 32-deep stages in a ring of NB LDS buffers (32 KiB each: A then B, 256 rows x 64 B as 128
-//    "pair rows" of 128 B -- logical rows 2R, 2R+1 -- with chunk C of pair row R at C ^ (R & 7): the
-//    ds_read_b128 fragment reads are conflict-free and the DMA stays lane-linear, swizzle on the source).
-//  * Per stage and wave: 64 MFMAs (16x16x32) on the fragments read during the previous stage, with the
-//    NEXT stage's 16 fragment reads and the DMA of stage s + NB (8 x 1 KiB) interleaved between them in a
-//    pinned order; then lgkmcnt(0), a counted vmcnt that retires stage s + 2 (NB - 2 stages stay in
-//    flight), ONE barrier.  Stage X's DMA goes into buffer X % NB during stage X - NB, after the barrier
-//    that follows every wave's last read of stage X - NB's fragments.
-//  * Fragments double-buffered in registers: the K loop is unrolled by two stages (static indices).
-template <int NB>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) gemm_w4_kernel(Args g) {
-  constexpr int STG = 32768, HALF = 16384, BKS = 32;
-  __shared__ __attribute__((aligned(1024))) char lds[NB * STG];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-
-  const int t = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
-  const int per_group = kGroupM * g.tiles_n;
-  const int grp = t / per_group, in_g = t - grp * per_group;
-  const int gm0 = grp * kGroupM, gh = min(kGroupM, g.tiles_m - gm0);
-  const int m0 = (gm0 + in_g % gh) * 256, n0 = (in_g / gh) * 256;
-  const int ns = g.K / BKS;
-
-  // DMA sources: piece i (1 KiB = 8 pair rows) of the A / B image, i = 4 j + wave
-  const bf16* srcA[4];
-  const bf16* srcB[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int i = 4 * j + wave;
-    const int R = 8 * i + (lane >> 3), C = (lane & 7) ^ (R & 7);
-    const int r = 2 * R + (C >> 2), c = C & 3;
-    srcA[j] = g.a + (int64_t)(m0 + r) * g.lda + 8 * c;
-    srcB[j] = g.b + (int64_t)(n0 + r) * g.ldb + 8 * c;
-  }
-  auto dma = [&](int st, int q) {  // piece q (0-3 A, 4-7 B) of stage st (past the end: the last stage)
-    const int ks = min(st, ns - 1);
-    char* dst = lds + (st % NB) * STG + (q >> 2) * HALF + (4 * (q & 3) + wave) * 1024;
-    glds16((q < 4 ? srcA[q & 3] : srcB[q & 3]) + ks * BKS, dst);
-  };
-  // fragment read offsets: row r0 + (lane & 15), chunk lane >> 4 -> pair row, swizzled chunk
-  const int fr = lane & 15, fc = lane >> 4;
-  const int foff = (fr >> 1) * 128 + 16 * ((((fr & 1) << 2) | fc) ^ ((fr >> 1) & 7));
-  auto rd = [&](int st, int q) -> bf16x8 {  // fragment q: 0-7 A rows wr*128 + 16q, 8-15 B cols wc*128 + 16(q-8)
-    const char* img = lds + (st % NB) * STG + (q >> 3) * HALF;
-    const int r0 = (q < 8 ? wr : wc) * 128 + 16 * (q & 7);
-    return *reinterpret_cast<const bf16x8*>(img + r0 * 64 + foff);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 f0[16], f1[16];
-
-  // prologue: stages 0 .. NB-1 in flight; retire 0 and 1; stage 0's fragments; everyone done reading
-#pragma unroll
-  for (int st = 0; st < NB; ++st)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(st, q);
-  vm_wait<8 * (NB - 2)>();
-  bar();
-#pragma unroll
-  for (int q = 0; q < 16; ++q) f0[q] = rd(0, q);
-  lgkm0();
-  bar();
-
-  // one stage: MFMAs on cur, reads of stage s+1 into nxt, DMA of stage s+NB, in a pinned interleave
-  auto stage = [&](int s, bf16x8 (&cur)[16], bf16x8 (&nxt)[16]) {
-#pragma unroll
-    for (int idx = 0; idx < 64; ++idx) {
-      const int ii = idx >> 3, jj = idx & 7;
-      __builtin_amdgcn_sched_barrier(0);
-      acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[8 + ii], cur[jj], acc[ii][jj], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (idx % 3 == 2 && idx < 48) nxt[idx / 3] = rd(s + 1, idx / 3);
-      if (idx % 8 == 5) dma(s + NB, idx / 8);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    lgkm0();
-    vm_wait<8 * (NB - 2)>();
-    bar();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  for (int s = 0; s < ns; s += 2) {
-    stage(s, f0, f1);
-    stage(s + 1, f1, f0);
-  }
-  vm_wait<0>();  // the tail's dummy DMAs land before the workgroup's LDS is released
-
-#pragma unroll
-  for (int ii = 0; ii < 8; ++ii) {
-    const int n = n0 + wc * 128 + 16 * ii + 4 * (lane >> 4);
-    float bv[4];
-    load_bias4(g, n, bv);
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) store4(g, m0 + wr * 128 + 16 * jj + (lane & 15), n, acc[ii][jj], bv);
-  }
-}
-
-template <int NB>
-static hipError_t launch_w4(const Args& g, hipStream_t st) {
-  hipLaunchKernelGGL(gemm_w4_kernel<NB>, dim3(g.tiles_m * g.tiles_n), dim3(256), 0, st, g);
-  return hipGetLastError();
-}
-
 template <int BM, int BN, int WC, bool AT, bool BT>
 static hipError_t launch(const Args& g, int ph, hipStream_t st) {
   if (ph == 2)
@@ -608,7 +503,6 @@ using namespace dta;
 int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   if (K % k64::BK || K < k64::BK) return 0;
   auto fits = [&](int t) { return M % k64::tile_bm(t) == 0 && N % k64::tile_bn(t) == 0; };
-  if (tile == 9 || tile == 10) return M % 256 == 0 && N % 256 == 0 ? tile : 0;  // W4 (NT only)
   if (tile) {
     const int base = tile > k64::kTiles ? tile - k64::kTiles : tile;
     return (tile >= 1 && tile <= 2 * k64::kTiles && fits(base)) ? tile : 0;
@@ -664,12 +558,6 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
 #ifdef DTA_K64_STAMP
   g.stamps = dta_k64_stamp_buf;
 #endif
-  if (tile == 9 || tile == 10) {  // W4: 4 / 5 LDS buffers, A and B K-major only
-    if (a_t || b_t) return hipErrorInvalidValue;
-    g.tiles_m = M / 256;
-    g.tiles_n = N / 256;
-    return tile == 9 ? k64::launch_w4<4>(g, st) : k64::launch_w4<5>(g, st);
-  }
   // K-loop phases per 64-deep stage: 4, or 2 for the ids past kTiles
   const int ph = tile > k64::kTiles ? 2 : 4;
   if (tile > k64::kTiles) tile -= k64::kTiles;
