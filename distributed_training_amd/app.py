@@ -120,6 +120,7 @@ def training_config_from(cfg: Any, model: Any = None) -> TrainingConfig:
         desync_check_every=int(_get(t, "desync_check_every", 0) or 0),
         fault_injection=_get(t, "fault_injection", None),
         cpu_offload=bool(_get(t, "cpu_offload", False)),
+        reduce_dtype=_get(t, "reduce_dtype", None),
         optimizer_in_backward=bool(_get(t, "optimizer_in_backward", False)),
         step_graph=bool(_get(t, "step_graph", False)),
     )

@@ -82,6 +82,8 @@ class FlatParamGroup:
         self.direct_claimed: set = set()
         for i, p in enumerate(self.params):
             p.data = self.param_view(i)
+            if self.grad_dtype != param_dtype and hasattr(p, "grad_dtype"):
+                p.grad_dtype = None  # fp32 gradients of bf16 compute copies (FSDP reduce_dtype=fp32)
             p.grad = self.grad_view(i)
             p._dta_flat = (self, i)  # noqa: SLF001 - tag read by the fused optimizers
 

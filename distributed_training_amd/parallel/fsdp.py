@@ -277,6 +277,8 @@ class _Unit:
             # keeping: reduce-scatter straight into this unit's slice of it
             fg = own.shards
             i = fg.index_of(self.shard_param)
+            if g.dtype != own.reduce_dtype:
+                g = g.to(own.reduce_dtype)
             direct = (own._grad_fresh and fg.grad_dtype == g.dtype and self.index not in own._written
                       and fg.grad.device == g.device)
             out = fg.grad_view(i) if direct else torch.empty(self.shard_size, dtype=g.dtype, device=g.device)
@@ -297,7 +299,8 @@ class FullyShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Communicator] = None,
                  device: Optional[torch.device] = None, wrap_policy: WrapPolicy = None,
                  param_dtype: torch.dtype = torch.float32, reshard_after_forward: bool = True,
-                 prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False) -> None:
+                 prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False,
+                 reduce_dtype: Optional[torch.dtype] = None) -> None:
         super().__init__()
         self.cpu_offload = bool(cpu_offload)
         if self.cpu_offload and param_dtype != torch.float32:
@@ -308,6 +311,11 @@ class FullyShardedDataParallel(nn.Module):
         self.rank = self.comm.rank
         self.device = device or next(module.parameters()).device
         self.param_dtype = param_dtype
+        # gradient reduce-scatter dtype (torch MixedPrecision.reduce_dtype): the compute dtype by default, as
+        # torch FSDP with param_dtype = reduce_dtype = bf16; float32 converts each unit gradient once before
+        # its reduce-scatter (twice the bytes on the wire, no bf16 rounding at the ring's hops) and keeps the
+        # shard gradients in fp32 for the optimizer
+        self.reduce_dtype = reduce_dtype or param_dtype
         self.reshard_after_forward = reshard_after_forward
         self.reshard_root_after_backward = True
         self.prefetch = prefetch
@@ -392,7 +400,8 @@ class FullyShardedDataParallel(nn.Module):
             for u, sp in zip(self.units, shard_params):
                 u.shard_param = sp
         self.shards = FlatParamGroup(shard_params, shard_dev, param_dtype=param_dtype, names=names,
-                                     pin_memory=self.cpu_offload)
+                                     pin_memory=self.cpu_offload,
+                                     grad_dtype=None if self.reduce_dtype == param_dtype else self.reduce_dtype)
         self.shards.fresh_hook = self._mark_grads_fresh
         self.shard_params = nn.ParameterList(shard_params)
         if sync_module_states and self.world_size > 1:

@@ -101,13 +101,14 @@ class DDPStrategy(DistributedStrategy):
 class FSDPStrategy(DistributedStrategy):
     def __init__(self, is_gpu: bool, wrap_policy: Any = None, mixed_precision: Optional[str] = None,
                  reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None,
-                 cpu_offload: bool = False) -> None:
+                 cpu_offload: bool = False, reduce_dtype: Optional[str] = None) -> None:
         self.is_gpu = is_gpu
         # the reference offloads only when there is no GPU (fsdp_strategy.py:23-25), where this
         # engine's shards live on the host anyway; on a GPU run it is an explicit opt-in
         self.cpu_offload = cpu_offload
         self.wrap_policy = wrap_policy
         self.param_dtype = _DTYPES[mixed_precision] if mixed_precision else torch.float32
+        self.reduce_dtype = _DTYPES[reduce_dtype] if reduce_dtype else None  # None: the compute dtype
         self.reshard_after_forward = reshard_after_forward
         self.prefetch = prefetch
         self.comm = comm
@@ -121,7 +122,8 @@ class FSDPStrategy(DistributedStrategy):
         return FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=self.wrap_policy,
                                         param_dtype=self.param_dtype,
                                         reshard_after_forward=self.reshard_after_forward, prefetch=self.prefetch,
-                                        cpu_offload=self.cpu_offload and dev.type == "cuda")
+                                        cpu_offload=self.cpu_offload and dev.type == "cuda",
+                                        reduce_dtype=self.reduce_dtype)
 
     def model_state(self, model: Module) -> Dict[str, torch.Tensor]:
         # FULL_STATE_DICT, offload_to_cpu=True, rank0_only=True (fsdp_strategy.py:31-35) -- on all ranks

@@ -488,3 +488,64 @@ def _routed_cpu(rank, ws):
 
 def test_routed_comm_cpu():
     run_gloo(_routed_cpu, 2)
+
+
+
+def _fsdp_reduce_dtype_worker(rank, ws, out):
+    """bf16 FSDP gradients after one backward, reduce-scattered in bf16 (the default: torch
+    MixedPrecision(param_dtype=reduce_dtype=bf16)) and with reduce_dtype=fp32, against the fp64 mean of
+    every rank's local bf16 gradients (each rank recomputes all ranks' local gradients with a plain bf16
+    copy of the model)."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    base = Net()
+    g = torch.Generator().manual_seed(11)
+    B = 16
+    X, Y = torch.randn(B * ws, 20, generator=g), torch.randn(B * ws, 1, generator=g)
+    ref = {}
+    for r in range(ws):
+        m = copy.deepcopy(base).bfloat16()
+        F.mse_loss(m(X[r * B:(r + 1) * B].bfloat16()).float(), Y[r * B:(r + 1) * B]).backward()
+        for n, p in m.named_parameters():
+            ref[n] = ref.get(n, 0) + p.grad.double() / ws
+    errs = {}
+    for rd in (None, torch.float32):
+        fs = FullyShardedDataParallel(copy.deepcopy(base), TorchComm(), torch.device("cpu"), wrap_policy={Block},
+                                      param_dtype=torch.bfloat16, reduce_dtype=rd)
+        assert fs.shards.grad_dtype == (rd or torch.bfloat16)
+        F.mse_loss(fs(X[rank * B:(rank + 1) * B].bfloat16()).float(), Y[rank * B:(rank + 1) * B]).backward()
+        err = scale = 0.0
+        for u in fs.units:
+            full = torch.zeros(u.total, dtype=torch.float64)
+            for (_, _, name, _), o, n in zip(u.entries, u.offsets, u.numels):
+                full[o:o + n] = ref[name].reshape(-1)
+            want = full[rank * u.shard_size:(rank + 1) * u.shard_size]
+            got = fs.shards.grad_view(fs.shards.index_of(u.shard_param)).double()
+            err = max(err, (got - want).abs().max().item())
+            scale = max(scale, want.abs().max().item())
+        t = torch.tensor([err, scale], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        errs["bf16" if rd is None else "fp32"] = t[0].item() / t[1].item()
+    if rank == 0:
+        out.put(errs)
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+def test_fsdp_reduce_dtype_pins_bf16_reduction_error(ws):
+    """FSDP reduce_dtype (torch MixedPrecision.reduce_dtype): with fp32 the reduce-scattered gradient is
+    the fp64 mean of the ranks' bf16 gradients up to fp32 rounding; the default bf16 reduction's extra
+    error (a rounding per partial sum: RCCL's ring rounds at every hop, gloo here) stays within a few
+    bf16 ulps of the largest gradient at 8 ranks -- the bound this test pins."""
+    import multiprocessing as mp
+
+    q = mp.get_context("spawn").SimpleQueue()
+    run_gloo(_fsdp_reduce_dtype_worker, ws, q)
+    errs = q.get()
+    print(f"ws={ws} max rel. gradient error vs the fp64 mean: {errs}")
+    assert errs["fp32"] < 1e-6, errs
+    assert errs["bf16"] < 2 ** -7, errs
+    assert errs["fp32"] < errs["bf16"], errs
