@@ -49,8 +49,8 @@ def parse() -> Any:
                     help="native DDP: launch the step's kernels eagerly instead of replaying the whole step as one "
                          "hipGraph (engine/step_graph.py)")
     ap.add_argument("--overlap-opt", action="store_true",
-                    help="native DDP: AdamW per bucket inside the backward (DistributedDataParallel.overlap_optimizer) "
-                         "instead of after it; bit-identical, measured neutral at one rank (README)")
+                    help="native DDP / FSDP: AdamW per bucket / unit inside the backward (overlap_optimizer of "
+                         "DistributedDataParallel / FullyShardedDataParallel) instead of after it; bit-identical")
     ap.add_argument("--tunableop", action="store_true",
                     help="let PyTorch's TunableOp pick the hipBLASLt/rocBLAS solution per GEMM shape (tuned in warmup)")
     return ap.parse_args()
@@ -132,7 +132,7 @@ def main() -> None:
             wrapped = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=lm_wrap_policy(model),
                                                param_dtype=torch.bfloat16)
         opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
-        overlap_opt = args.strategy == "ddp" and args.overlap_opt and wrapped.overlap_optimizer(opt)
+        overlap_opt = args.overlap_opt and wrapped.overlap_optimizer(opt)
 
         def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> Any:
             return lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))

@@ -44,7 +44,7 @@ hipError_t dta_attn_bwd(const dta::AttnArgs*, int, bool, hipStream_t);
 hipError_t dta_flat_sgd(const float*, float*, const float*, float*, void*, int64_t, float, float, float, float, float,
                         int, int, int, hipStream_t);
 hipError_t dta_flat_adam(float*, const void*, int, float*, float*, float*, void*, int64_t, float*, float, float, float,
-                         float, float, float, int, int, int, int, hipStream_t);
+                         float, float, float, int, int, int, int, int, hipStream_t);
 hipError_t dta_step_inc(float*, hipStream_t);
 hipError_t dta_mt_scale_copy(const void* const*, void* const*, const int64_t*, int, int, int, float, hipStream_t);
 hipError_t dta_flat_sumsq(const float*, int64_t, float*, hipStream_t);
@@ -130,7 +130,7 @@ void flat_sgd(torch::Tensor p_in, torch::Tensor p_out, torch::Tensor g, c10::opt
 void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> vmax,
                c10::optional<torch::Tensor> p_bf16, torch::Tensor step, double lr, double beta1, double beta2,
                double eps, double wd, double grad_scale, bool adamw, bool maximize, bool amsgrad, bool bump_step,
-               int64_t stream) {
+               int64_t stream, int64_t max_blocks) {
   check_f32(p, "param", false);
   check_gpu(g, "grad");
   TORCH_CHECK(g.is_contiguous() && (g.scalar_type() == torch::kFloat32 || g.scalar_type() == torch::kBFloat16),
@@ -155,7 +155,7 @@ void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor 
   }
   hip_ok(dta_flat_adam(p.data_ptr<float>(), g.data_ptr(), g_bf16, m.data_ptr<float>(), v.data_ptr<float>(), fptr(vmax),
                        pb, n, step.data_ptr<float>(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd,
-                       (float)grad_scale, adamw, maximize, amsgrad, bump_step, pick_stream(stream)),
+                       (float)grad_scale, adamw, maximize, amsgrad, bump_step, (int)max_blocks, pick_stream(stream)),
          "flat_adam");
 }
 
@@ -1069,7 +1069,10 @@ PYBIND11_MODULE(_C, m) {
   dta_register_ext(m);
   m.doc() = "distributed_training_amd native runtime (gfx950 HIP kernels + RCCL communicator)";
   m.def("flat_sgd", &flat_sgd);
-  m.def("flat_adam", &flat_adam);
+  m.def("flat_adam", &flat_adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("vmax"),
+        py::arg("p_bf16"), py::arg("step"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("wd"), py::arg("grad_scale"), py::arg("adamw"), py::arg("maximize"), py::arg("amsgrad"),
+        py::arg("bump_step"), py::arg("stream") = -1, py::arg("max_blocks") = 0);
   m.def("step_inc", &step_inc);
   m.def("mt_scale_copy", &mt_scale_copy);
   m.def("flat_sumsq", &flat_sumsq);

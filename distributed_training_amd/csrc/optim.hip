@@ -258,17 +258,21 @@ hipError_t dta_flat_sgd(const float* p_in, float* p_out, const float* g, float* 
 
 hipError_t dta_flat_adam(float* p, const void* g, int g_bf16, float* m, float* v, float* vmax, void* p_bf16,
                          int64_t n, float* step, float lr, float beta1, float beta2, float eps, float wd,
-                         float grad_scale, int adamw, int maximize, int amsgrad, int bump_step, hipStream_t st) {
+                         float grad_scale, int adamw, int maximize, int amsgrad, int bump_step, int max_blocks,
+                         hipStream_t st) {
   if (bump_step) hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
   if (n <= 0) return hipGetLastError();
+  // max_blocks > 0: a narrow grid (grid-stride) for an update running BESIDE compute-bound kernels on
+  // another stream (optimizer inside the backward) -- it then takes a bounded share of the CUs' slots
+  const int nb = max_blocks > 0 ? min(grid_for((n + 3) / 4), max_blocks) : grid_for((n + 3) / 4);
   auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) % a) == 0; };
   const int vec = al(p, 16) && al(g, g_bf16 ? 8 : 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
   AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad, vec};
   if (g_bf16)
-    hipLaunchKernelGGL(flat_adam_kernel<bf16>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p,
+    hipLaunchKernelGGL(flat_adam_kernel<bf16>, dim3(nb), dim3(256), 0, st, p,
                        reinterpret_cast<const bf16*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
   else
-    hipLaunchKernelGGL(flat_adam_kernel<float>, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, p,
+    hipLaunchKernelGGL(flat_adam_kernel<float>, dim3(nb), dim3(256), 0, st, p,
                        reinterpret_cast<const float*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
   return hipGetLastError();
 }

@@ -175,10 +175,11 @@ class FusedSGD(torch.optim.Optimizer):
         return len(self.param_groups) == 1 and _covers(self.param_groups[0]["params"], fg)
 
     @torch.no_grad()
-    def step_range(self, fg: Any, lo: int, hi: int, first: bool) -> None:
+    def step_range(self, fg: Any, lo: int, hi: int, first: bool, max_blocks: int = 0) -> None:
         """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
         current stream): the same per-element math as :meth:`step` over the whole buffer,
-        so a step split into ranges is bit-identical.  ``first``: the step's first range."""
+        so a step split into ranges is bit-identical.  ``first``: the step's first range
+        (``max_blocks``: accepted for the interface, the SGD update keeps its grid)."""
         g = self.param_groups[0]
         st = self._flat_state.setdefault(id(fg), {"first": True})
         if g["momentum"] and "mom" not in st:
@@ -349,9 +350,10 @@ class FusedAdamW(torch.optim.Optimizer):
     range_capable = FusedSGD.range_capable
 
     @torch.no_grad()
-    def step_range(self, fg: Any, lo: int, hi: int, first: bool) -> None:
-        """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket, on the
-        current stream); ``first`` bumps the device step counter (the step's first range).
+    def step_range(self, fg: Any, lo: int, hi: int, first: bool, max_blocks: int = 0) -> None:
+        """Update elements ``[lo, hi)`` of the flat group ``fg`` (one DDP bucket / FSDP unit, on
+        the current stream); ``first`` bumps the device step counter (the step's first range);
+        ``max_blocks`` > 0 caps the grid (an update running beside the backward's kernels).
         Element-wise math identical to :meth:`step`: a split step is bit-identical."""
         g = self.param_groups[0]
         (b1, b2), ams = g["betas"], g["amsgrad"]
@@ -359,7 +361,7 @@ class FusedAdamW(torch.optim.Optimizer):
         native().flat_adam(fg.master[lo:hi], fg.grad[lo:hi], st["m"][lo:hi], st["v"][lo:hi],
                            None if st["vmax"] is None else st["vmax"][lo:hi],
                            fg.compute[lo:hi] if fg.mixed else None, st["step"], g["lr"], b1, b2, g["eps"],
-                           g["weight_decay"], 1.0, g["adamw"], g["maximize"], ams, first, -1)
+                           g["weight_decay"], 1.0, g["adamw"], g["maximize"], ams, first, -1, max_blocks)
 
     def end_ranges(self, fg: Any) -> None:
         pass

@@ -40,6 +40,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import functools
+import os
 import logging
 from typing import Any, Callable, Dict, List, Optional, Sequence, Set, Tuple, Type, Union
 
@@ -290,6 +291,8 @@ class _Unit:
             with prof.range_(f"fsdp.unit{self.index}.reduce_scatter"):
                 work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
             own._pending_rs.append((self, work, out, g))
+        if own._ov is not None:
+            own._ov_unit(self)
         self.in_backward = False
         if not self.is_root or own.reshard_root_after_backward:
             self.free()
@@ -423,6 +426,9 @@ class FullyShardedDataParallel(nn.Module):
         # copies) each unit's gradient in place of accumulating into zeros
         self._grad_fresh = False
         self._written: Set[int] = set()
+        self._ov: Any = None  # optimizer stepped unit by unit inside the backward (overlap_optimizer)
+        self._ov_done: Set[int] = set()
+        self._ov_first = True
         logger.debug("FSDP: %d unit(s), shard sizes %s", len(self.units), [u.shard_size for u in self.units])
 
     # ------------------------------------------------------------ forward
@@ -506,6 +512,63 @@ class FullyShardedDataParallel(nn.Module):
         return out
 
     # ------------------------------------------------------------ backward
+    # ------------------------------------------------------------ optimizer in backward
+    def overlap_optimizer(self, optimizer: Any) -> bool:
+        """Run ``optimizer``'s update unit by unit INSIDE the backward, on a side HIP stream:
+        a unit's shard is updated as soon as its gradient is final (its reduce-scatter done
+        at world size > 1, written in place at one rank), so the memory-bound update of the
+        late units overlaps the compute-bound backward of the early ones instead of
+        following the whole backward (Llama-3 8B at one rank: AdamW over 8 B fp32 master
+        weights and moments is ~40 ms per step).  ``optimizer.step()`` then has nothing left
+        to do for this engine's shards.  Same contract as the DDP engine's
+        :meth:`~.ddp.DistributedDataParallel.overlap_optimizer`: one backward per step, no
+        gradient edits between ``backward()`` and ``step()`` (clipping, unscaling); the update
+        per element is the fused kernel's, so it is bit-identical to ``step()``.  Returns False
+        (nothing changed) unless the optimizer is a fused SGD / AdamW with one param group over
+        exactly this engine's shards, on the GPU (no CPU offload).
+        Reference: the optimizer step of src/distributed_trainer.py:165 after the FSDP backward
+        of src/dist_strategy/fsdp_strategy.py:20."""
+        fg = self.shards
+        if optimizer is None:
+            self._ov = None
+            return False
+        if not (fg.grad.is_cuda and hasattr(optimizer, "step_range") and optimizer.range_capable(fg)):
+            return False
+        self._ov = optimizer
+        self._ov_stream = torch.cuda.Stream(self.device)
+        self._ov_first = True
+        self._ov_done = set()
+        # grid cap of the in-backward updates (DTA_OV_OPT_BLOCKS; 0 = the full grid)
+        self._ov_blocks = int(os.environ.get("DTA_OV_OPT_BLOCKS", "0"))
+        return True
+
+    def _ov_step(self, u: "_Unit", work: Any = None) -> None:
+        fg = self.shards
+        i = fg.index_of(u.shard_param)
+        lo = fg.offsets[i]
+        s = self._ov_stream
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            if work is not None:
+                work.wait(s)
+            with prof.range_(f"fsdp.unit{u.index}.optimizer"):
+                self._ov.step_range(fg, lo, lo + fg.numels[i], self._ov_first, self._ov_blocks)
+        self._ov_first = False
+        self._ov_done.add(u.index)
+
+    def _ov_unit(self, u: "_Unit") -> None:
+        """Post-backward of unit ``u``: step its shard now if its gradient is final in place
+        (fresh gradients; reduce-scattered / written straight into the shard's gradient slice),
+        else leave it to the end of the backward."""
+        if not self._grad_fresh or u.index in self._ov_done:
+            return
+        fg = self.shards
+        gv = fg.grad_view(fg.index_of(u.shard_param))
+        _, work, out, _g = self._pending_rs[-1]
+        if out.data_ptr() != gv.data_ptr() or out.dtype != gv.dtype:
+            return
+        self._ov_step(u, work if self.world_size > 1 else None)
+
     def _queue_final_callback(self) -> None:
         if not self._cb_queued:
             Variable._execution_engine.queue_callback(self._finalize_backward)
@@ -547,6 +610,15 @@ class FullyShardedDataParallel(nn.Module):
             self._written = set()
         self._pending_rs = []
         self._cb_queued = False
+        if self._ov is not None:
+            for u in self.units:  # units whose gradient was not final in place: stepped now
+                if u.index not in self._ov_done:
+                    self._ov_step(u)
+            torch.cuda.current_stream(self.device).wait_stream(self._ov_stream)
+            self._ov.end_ranges(fg)
+            self._ov_first = True
+            self._ov_done = set()
+            fg.stepped_in_backward = True
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()
         if self.cpu_offload and self.device.type == "cuda":

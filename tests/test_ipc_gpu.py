@@ -566,3 +566,42 @@ def _graph_multirank_worker(rank, ws):
 @pytest.mark.parametrize("ws", [2, 4])
 def test_step_graph_multirank_matches_eager(ws):
     run_gloo(_graph_multirank_worker, ws)
+
+
+def _fsdp_overlap_bitwise_worker(rank, ws):
+    """FSDP with AdamW stepped unit by unit inside the backward (overlap_optimizer) vs backward +
+    step(), both at this world size over the IPC collectives: identical losses and shards."""
+    from distributed_training_amd.models.gpt2 import GPT2
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    B, T, steps = 2, 64, 3
+    g = torch.Generator(device="cpu").manual_seed(8)
+    local = [torch.randint(0, 512, (ws * B, T + 1), generator=g)[rank * B:(rank + 1) * B].to(dev)
+             for _ in range(steps)]
+    comm = IpcComm(rank, ws, dev)
+    finals = []
+    for overlap in (False, True):
+        w = FullyShardedDataParallel(_tiny_gpt2().to(dev), comm=comm, device=dev, wrap_policy={GPT2.block_class},
+                                     param_dtype=torch.bfloat16)
+        opt = FusedAdamW(w.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+        if overlap:
+            assert w.overlap_optimizer(opt)
+        losses = _train(w, opt, local, steps)
+        comm.poll_errors()
+        torch.cuda.synchronize()
+        finals.append((losses, w.shards.master.clone(), w.shards.compute.clone()))
+    assert finals[0][0] == finals[1][0]
+    assert torch.equal(finals[0][1], finals[1][1]) and torch.equal(finals[0][2], finals[1][2])
+    comm.destroy()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_fsdp_optimizer_in_backward_multi_rank_shared_gpu(ws):
+    """FSDP overlap_optimizer across ranks: each unit's shard updated on a side stream after its
+    reduce-scatter, bit-identical to the plain step; and the same trajectory as the one-rank
+    global-batch reference (_engine_worker)."""
+    run_gloo(_fsdp_overlap_bitwise_worker, ws)
+    run_gloo(_engine_worker, ws, "fsdp", True)

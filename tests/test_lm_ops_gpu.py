@@ -811,3 +811,40 @@ def test_fsdp_weight_used_twice_first_claim():
         upd = w0[name] - sd[name].float().cpu()
         assert _rel(upd, rp[name].grad.float().cpu()) < 3e-2, name
 
+
+
+@pytest.mark.parametrize("opt_name", ["adamw", "sgd"])
+def test_fsdp_optimizer_in_backward_bit_identical(opt_name):
+    """FSDP overlap_optimizer at one rank (each unit's shard, aliased by the unit, updated on a
+    side stream right after the unit's backward; the Llama-style lm_wrap_policy units with the
+    tied GPT-2 embedding) gives the same bits as backward + step()."""
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW, FusedSGD
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    data = [torch.randint(0, 1024, (2, 257), generator=g).to(dev) for _ in range(4)]
+    finals = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=3, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        fs = FullyShardedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, wrap_policy=lm_wrap_policy(model),
+                                      param_dtype=torch.bfloat16)
+        assert len(fs.units) >= 4
+        opt = (FusedAdamW(fs.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1) if opt_name == "adamw"
+               else FusedSGD(fs.parameters(), lr=0.05, momentum=0.9))
+        assert fs.overlap_optimizer(opt) if overlap else True
+        losses = []
+        for x in data:
+            opt.zero_grad(set_to_none=True)
+            loss = fs(x[:, :-1], x[:, 1:])
+            loss.backward()
+            opt.step()
+            losses.append(loss.float())
+        torch.cuda.synchronize()
+        finals.append((torch.stack(losses).cpu(), fs.shards.master.clone(), fs.shards.compute.clone()))
+    assert torch.equal(finals[0][0], finals[1][0])
+    assert torch.equal(finals[0][1], finals[1][1])
+    assert torch.equal(finals[0][2], finals[1][2])
