@@ -566,7 +566,9 @@ def _queue_end_join() -> None:
 # 200: two GPT-2 layers = 216 tiles) ONE grouped launch computes all of them over the full
 # token reduction -- no split, no slabs, bias gradients from the same MFMA pipe
 # (csrc/gemm_bf16.hip gemm_group_kernel).  The queue is flushed before every DDP bucket
-# launch and at the end of the backward (same stream: no further synchronisation).
+# launch and at the end of the backward (same stream: no further synchronisation); under the
+# FSDP engine (unit pieces, ``_dta_defer_ok``) a unit's reduce-scatter waits for the flush that
+# writes its pieces (parallel/fsdp.py ``_launch_waiting``).
 _DEFER: list = []
 _DEFER_TILES = [0]
 # called after every flush launched its groups (the DDP engine's per-bucket optimizer
@@ -631,7 +633,8 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
         split = _side_split()
         cb = _grad_dest(b) if with_bias else None
         thr = _group_threshold()
-        if thr and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
+        if thr and cw is not None and (cb is not None or not with_bias) \
+                and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
                 and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0 \
                 and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
             # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue

@@ -78,6 +78,12 @@ def lm_wrap_policy(model: nn.Module) -> Callable[[nn.Module], bool]:
     return lambda m: (block is not None and isinstance(m, block)) or id(m) in extra
 
 
+def _lm() -> Any:
+    from ..ops import lm  # (GPU engines only: the CPU path never imports the kernel bindings)
+
+    return lm
+
+
 def _align(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
@@ -232,6 +238,7 @@ class _Unit:
         for e, ((mod, attr, name, _), k, shp) in enumerate(zip(self.entries, self._piece_index, self.shapes)):
             view = pieces[k].view(shp)
             view._dta_gdest = functools.partial(self.piece_dest, e)
+            view._dta_defer_ok = self.owner._defer_wgrad  # its weight gradient may join a grouped launch
             for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
                 setattr(m2, a2, view)
 
@@ -271,6 +278,18 @@ class _Unit:
         full.grad = None
         self._dest = None
         self._claimed = set()
+        if own.world_size > 1 and own._defer_wgrad and _lm().wgrad_pending():
+            # weight gradients of this unit (or an earlier one) still queued for a grouped launch
+            # (ops/lm.py _DEFER): reduce-scattered right after that launch (_launch_waiting)
+            own._rs_waiting.append((self, g))
+        else:
+            self._launch_rs(g)
+        self.in_backward = False
+        if not self.is_root or own.reshard_root_after_backward:
+            self.free()
+
+    def _launch_rs(self, g: torch.Tensor) -> None:
+        own = self.owner
         if own.world_size == 1:  # the whole gradient is this rank's shard: no collective, no copy
             own._pending_rs.append((self, CommWork(), g, g))
         else:
@@ -293,9 +312,6 @@ class _Unit:
             own._pending_rs.append((self, work, out, g))
         if own._ov is not None:
             own._ov_unit(self)
-        self.in_backward = False
-        if not self.is_root or own.reshard_root_after_backward:
-            self.free()
 
 
 class FullyShardedDataParallel(nn.Module):
@@ -426,6 +442,27 @@ class FullyShardedDataParallel(nn.Module):
         # copies) each unit's gradient in place of accumulating into zeros
         self._grad_fresh = False
         self._written: Set[int] = set()
+        # Deferred, grouped weight gradients (ops/lm.py _DEFER, as under the DDP engine): the native
+        # Linear queues a single-use weight's gradient and one grouped launch computes several layers'
+        # (GPT-2: 0.58-0.81x hipBLASLt per weight gradient at its small output shapes, ~1 PF/s grouped).
+        # A unit's reduce-scatter waits for the launch that writes its pieces; DTA_FSDP_WGRAD_DEFER=0: off.
+        self._defer_wgrad = (self.device.type == "cuda" and not self.cpu_offload
+                             and os.environ.get("DTA_FSDP_WGRAD_DEFER", "1") != "0")
+        self._rs_waiting: List[Tuple[_Unit, torch.Tensor]] = []
+        if self._defer_wgrad:
+            import weakref
+
+            ref = weakref.ref(self)
+
+            def on_flush() -> None:
+                me = ref()
+                if me is None:
+                    if on_flush in _lm().FLUSH_LISTENERS:
+                        _lm().FLUSH_LISTENERS.remove(on_flush)
+                else:
+                    me._launch_waiting()
+
+            _lm().FLUSH_LISTENERS.append(on_flush)
         self._ov: Any = None  # optimizer stepped unit by unit inside the backward (overlap_optimizer)
         self._ov_done: Set[int] = set()
         self._ov_first = True
@@ -497,6 +534,8 @@ class FullyShardedDataParallel(nn.Module):
                 t.register_hook(hook)
 
     def forward(self, *args: Any, **kwargs: Any) -> Any:
+        if self._defer_wgrad and torch.is_grad_enabled():
+            _lm().new_forward_generation()  # (native Linear counts weight uses per forward: single-use -> deferrable)
         if self.prefetch and not self._record_order and self._fwd_order:
             self._fwd_order[0].unshard(async_op=True)  # the first unit (the embedding) in flight with the root's
         if self.root_unit is not None:
@@ -560,7 +599,7 @@ class FullyShardedDataParallel(nn.Module):
         """Post-backward of unit ``u``: step its shard now if its gradient is final in place
         (fresh gradients; reduce-scattered / written straight into the shard's gradient slice),
         else leave it to the end of the backward."""
-        if not self._grad_fresh or u.index in self._ov_done:
+        if not self._grad_fresh or u.index in self._ov_done or (self._defer_wgrad and _lm().wgrad_pending()):
             return
         fg = self.shards
         gv = fg.grad_view(fg.index_of(u.shard_param))
@@ -568,6 +607,12 @@ class FullyShardedDataParallel(nn.Module):
         if out.data_ptr() != gv.data_ptr() or out.dtype != gv.dtype:
             return
         self._ov_step(u, work if self.world_size > 1 else None)
+
+    def _launch_waiting(self) -> None:
+        """Reduce-scatter the units whose gradients waited for a grouped weight-gradient launch."""
+        waiting, self._rs_waiting = self._rs_waiting, []
+        for u, g in waiting:
+            u._launch_rs(g)
 
     def _queue_final_callback(self) -> None:
         if not self._cb_queued:
@@ -579,6 +624,9 @@ class FullyShardedDataParallel(nn.Module):
             self._finalize_backward_impl()
 
     def _finalize_backward_impl(self) -> None:
+        if self._defer_wgrad:
+            _lm().wgrad_join(self.device)  # every queued weight gradient written (-> _launch_waiting)
+            self._launch_waiting()
         fg = self.shards
         fresh = self._grad_fresh
         done: Set[int] = set()
@@ -619,6 +667,8 @@ class FullyShardedDataParallel(nn.Module):
             self._ov_first = True
             self._ov_done = set()
             fg.stepped_in_backward = True
+        if self._defer_wgrad:
+            _lm().close_forward_generations()
         if self.world_size > 1 and hasattr(self.comm, "poll_errors"):
             self.comm.poll_errors()
         if self.cpu_offload and self.device.type == "cuda":

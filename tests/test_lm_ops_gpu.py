@@ -848,3 +848,47 @@ def test_fsdp_optimizer_in_backward_bit_identical(opt_name):
     assert torch.equal(finals[0][0], finals[1][0])
     assert torch.equal(finals[0][1], finals[1][1])
     assert torch.equal(finals[0][2], finals[1][2])
+
+
+@pytest.mark.parametrize("ckpt", [False, True])
+def test_fsdp_deferred_grouped_weight_gradients(ckpt, monkeypatch):
+    """Under the FSDP engine the single-use weights' gradients are deferred into grouped launches
+    (ops/lm.py _DEFER) and written into the unit pieces before the unit's gradient is used: the same
+    training trajectory as with deferral off (DTA_FSDP_WGRAD_DEFER=0: per-weight kernels), within
+    bf16 rounding of the two reduction orders; with activation checkpointing too."""
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    data = [torch.randint(0, 1024, (2, 257), generator=g).to(dev) for _ in range(3)]
+    runs = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("DTA_FSDP_WGRAD_DEFER", defer)
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=3, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        if ckpt:
+            model.enable_activation_checkpointing()
+        fs = FullyShardedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, wrap_policy=lm_wrap_policy(model),
+                                      param_dtype=torch.bfloat16)
+        assert fs._defer_wgrad == (defer == "1")
+        opt = FusedAdamW(fs.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+        before = lm.GEMM_STATS["deferred_wgrad"]
+        losses = []
+        for x in data:
+            opt.zero_grad(set_to_none=True)
+            loss = fs(x[:, :-1], x[:, 1:])
+            loss.backward()
+            opt.step()
+            losses.append(loss.float().item())
+        torch.cuda.synchronize()
+        runs.append((losses, fs.shards.master.clone(), lm.GEMM_STATS["deferred_wgrad"] - before))
+    (l1, m1, d1), (l0, m0, d0) = runs
+    assert d0 == 0 and (ckpt or d1 >= 3 * 4 * 3), (d1, d0)  # every block's four Linear weights, every step
+    # (under activation checkpointing the recomputed forward counts each weight a second time: not
+    # single-use, so nothing is deferred -- the per-weight path, the same trajectory)
+    for a, b in zip(l1, l0):
+        assert abs(a - b) < 2e-3 * abs(b), (l1, l0)
+    assert _rel(m1, m0) < 1e-3
