@@ -121,6 +121,8 @@ def training_config_from(cfg: Any, model: Any = None) -> TrainingConfig:
         fault_injection=_get(t, "fault_injection", None),
         cpu_offload=bool(_get(t, "cpu_offload", False)),
         reduce_dtype=_get(t, "reduce_dtype", None),
+        fsdp_sharding=str(_get(t, "fsdp_sharding", "full") or "full"),
+        hybrid_shard_size=_get(t, "hybrid_shard_size", None),
         optimizer_in_backward=bool(_get(t, "optimizer_in_backward", False)),
         step_graph=bool(_get(t, "step_graph", False)),
     )

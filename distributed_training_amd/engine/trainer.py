@@ -72,6 +72,8 @@ class TrainingConfig:
     fault_injection: Optional[Dict[str, int]] = None
     cpu_offload: bool = False        # FSDP: fp32 shards, gradients and optimizer on the host
     reduce_dtype: Optional[str] = None  # FSDP gradient reduce-scatter dtype: None = compute dtype, "fp32"
+    fsdp_sharding: str = "full"      # FSDP: "full" (FULL_SHARD) or "hybrid" (HSDP: shard per node, replicate)
+    hybrid_shard_size: Optional[int] = None  # HSDP shard group size (default: LOCAL_WORLD_SIZE)
     optimizer_in_backward: bool = False  # DDP on GPU: fused update per bucket inside the backward (no grad_clip)
     step_graph: bool = False         # DDP on GPU: whole step replayed as one hipGraph (engine/step_graph.py)
     extra: Dict[str, Any] = field(default_factory=dict)
@@ -132,7 +134,8 @@ class Trainer:
         c = self.config
         if c.parallel_strategy.lower() == "fsdp":
             return FSDPStrategy(self.env.is_gpu, wrap_policy=c.fsdp_wrap, mixed_precision=c.mixed_precision,
-                                cpu_offload=c.cpu_offload, reduce_dtype=c.reduce_dtype)
+                                cpu_offload=c.cpu_offload, reduce_dtype=c.reduce_dtype, sharding=c.fsdp_sharding,
+                                hybrid_shard_size=c.hybrid_shard_size)
         return DDPStrategy(self.env.local_rank, self.env.is_gpu, bucket_cap_mb=c.bucket_cap_mb,
                            first_bucket_mb=c.first_bucket_mb, mixed_precision=c.mixed_precision)
 

@@ -152,7 +152,10 @@ class TorchComm(Communicator):
     def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
         if self.world_size == 1:
             return CommWork() if async_op else None
-        work = dist.broadcast(t, src=src, group=self.group, async_op=async_op)
+        if self.group is not None:  # ``src`` is a rank of this communicator's group, as for every backend here
+            work = dist.broadcast(t, group_src=src, group=self.group, async_op=async_op)
+        else:
+            work = dist.broadcast(t, src=src, async_op=async_op)
         return self._w(work, async_op)
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> None:
@@ -456,3 +459,28 @@ def make_comm(device: torch.device, prefer: str = "auto", group: Any = None, bul
                 return RoutedComm(rccl, ipc)
             return rccl
     return TorchComm(group=group, device=device)
+
+
+def make_hybrid_comms(device: torch.device, shard_size: int) -> Tuple[Communicator, Communicator]:
+    """The two communicators of HYBRID sharding (HSDP): ranks ``[g S, (g + 1) S)`` form shard group
+    ``g`` (S = ``shard_size``: one node's GPUs under torchrun's rank order, so the FSDP gathers and
+    reduce-scatters stay on xGMI) and the ranks with the same index in every shard group form a
+    replica group (the inter-node gradient all-reduce).  GPU: RCCL communicators of their own
+    (IPC ones when several ranks share one GPU); CPU: gloo subgroups (every rank creates every
+    group, in one order, as torch.distributed.new_group requires)."""
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    ws = dist.get_world_size() if dist.is_initialized() else 1
+    if shard_size < 1 or ws % shard_size:
+        raise ValueError(f"hybrid shard size {shard_size} must divide the world size {ws}")
+    g, i, reps = rank // shard_size, rank % shard_size, ws // shard_size
+    if device.type == "cuda" and os.environ.get("DTA_COMM", "") != "torch":
+        from .ipc import IpcComm, shared_gpu
+
+        if shared_gpu():
+            return (IpcComm(i, shard_size, device, tag=f"hsdp_shard{g}"),
+                    IpcComm(g, reps, device, tag=f"hsdp_rep{i}"))
+        return (RcclComm(i, shard_size, device, tag=f"hsdp_shard{g}"),
+                RcclComm(g, reps, device, tag=f"hsdp_rep{i}"))
+    shard_groups = [dist.new_group(list(range(k * shard_size, (k + 1) * shard_size))) for k in range(reps)]
+    rep_groups = [dist.new_group(list(range(j, ws, shard_size))) for j in range(shard_size)]
+    return TorchComm(shard_groups[g], device), TorchComm(rep_groups[i], device)

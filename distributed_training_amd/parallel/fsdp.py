@@ -319,7 +319,7 @@ class FullyShardedDataParallel(nn.Module):
                  device: Optional[torch.device] = None, wrap_policy: WrapPolicy = None,
                  param_dtype: torch.dtype = torch.float32, reshard_after_forward: bool = True,
                  prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False,
-                 reduce_dtype: Optional[torch.dtype] = None) -> None:
+                 reduce_dtype: Optional[torch.dtype] = None, replicate_comm: Optional[Communicator] = None) -> None:
         super().__init__()
         self.cpu_offload = bool(cpu_offload)
         if self.cpu_offload and param_dtype != torch.float32:
@@ -328,6 +328,11 @@ class FullyShardedDataParallel(nn.Module):
         self.comm = comm or TorchComm()
         self.world_size = self.comm.world_size
         self.rank = self.comm.rank
+        # HYBRID sharding (torch ShardingStrategy.HYBRID_SHARD, HSDP): ``comm`` is the shard group (one
+        # node's GPUs over xGMI: the per-unit all-gathers / reduce-scatters), ``replicate_comm`` the
+        # replica group (the same local rank on every node: one all-reduce of the gradient shards per
+        # step over the inter-node fabric).  parallel/comm.py make_hybrid_comms builds both.
+        self.rep = replicate_comm if replicate_comm is not None and replicate_comm.world_size > 1 else None
         self.device = device or next(module.parameters()).device
         self.param_dtype = param_dtype
         # gradient reduce-scatter dtype (torch MixedPrecision.reduce_dtype): the compute dtype by default, as
@@ -427,6 +432,19 @@ class FullyShardedDataParallel(nn.Module):
             for b in module.buffers():
                 if b.numel():
                     self.comm.broadcast(b.data, src=0)
+        if self.rep is not None and sync_module_states:
+            # replicas start from replica 0's shards (and buffers): one broadcast per shard buffer
+            fgs = self.shards
+            master = fgs.master if fgs.master.device.type == self.device.type else fgs.master.to(self.device)
+            self.rep.broadcast(master, src=0)
+            if master is not fgs.master:
+                fgs.master.copy_(master.cpu())
+            with torch.no_grad():
+                if fgs.mixed:
+                    fgs.compute.copy_(fgs.master.to(fgs.compute.device))
+            for b in module.buffers():
+                if b.numel():
+                    self.rep.broadcast(b.data, src=0)
 
         # ---- hooks ----
         for u in self.units:
@@ -599,7 +617,8 @@ class FullyShardedDataParallel(nn.Module):
         """Post-backward of unit ``u``: step its shard now if its gradient is final in place
         (fresh gradients; reduce-scattered / written straight into the shard's gradient slice),
         else leave it to the end of the backward."""
-        if not self._grad_fresh or u.index in self._ov_done or (self._defer_wgrad and _lm().wgrad_pending()):
+        if not self._grad_fresh or u.index in self._ov_done or (self._defer_wgrad and _lm().wgrad_pending()) \
+                or self.rep is not None:  # (HSDP: final only after the replica all-reduce)
             return
         fg = self.shards
         gv = fg.grad_view(fg.index_of(u.shard_param))
@@ -658,6 +677,15 @@ class FullyShardedDataParallel(nn.Module):
             self._written = set()
         self._pending_rs = []
         self._cb_queued = False
+        if self.rep is not None:
+            # HSDP: the shard-group reduce-scatters are done (waited above); average the gradient shards
+            # over the replicas -- ONE all-reduce of the whole flat shard gradient (the mean over every
+            # rank's micro-batch, as the shard group's average was over its own ranks)
+            with prof.range_("fsdp.replica_all_reduce"):
+                g = fg.grad if fg.grad.device.type == self.device.type else fg.grad.to(self.device)
+                self.rep.all_reduce(g, op="avg")
+                if g is not fg.grad:
+                    fg.grad.copy_(g.cpu())
         if self._ov is not None:
             for u in self.units:  # units whose gradient was not final in place: stepped now
                 if u.index not in self._ov_done:
@@ -682,7 +710,7 @@ class FullyShardedDataParallel(nn.Module):
         """The whole step can be captured as one hipGraph (engine/step_graph.py): at one rank without
         CPU offload every unit aliases its shard, so no storage is freed or re-allocated between
         units and no collective runs -- the replay repeats the same kernels on the same buffers."""
-        return self.world_size == 1 and not self.cpu_offload and all(u.alias for u in self.units)
+        return self.world_size == 1 and self.rep is None and not self.cpu_offload and all(u.alias for u in self.units)
 
     def _mark_grads_fresh(self) -> None:
         self._grad_fresh = True
@@ -710,7 +738,7 @@ class FullyShardedDataParallel(nn.Module):
         """Collective: every rank must call it (gathers each unit's fp32 master)."""
         out: Dict[str, torch.Tensor] = {}
         fg = self.shards
-        keep = (not rank0_only) or self.rank == 0
+        keep = (not rank0_only) or (self.rank == 0 and (self.rep is None or self.rep.rank == 0))
         for u in self.units:
             i = fg.index_of(u.shard_param)
             shard = fg.master_view(i).contiguous().to(self.device)
@@ -770,7 +798,7 @@ class FullyShardedDataParallel(nn.Module):
         parameter names (world-size independent, like ``FULL_STATE_DICT``).  Each
         shard-sized state tensor (momentum, Adam moments) is all-gathered per unit
         and cut into per-parameter tensors; scalars (step) are taken as they are."""
-        keep = (not rank0_only) or self.rank == 0
+        keep = (not rank0_only) or (self.rank == 0 and (self.rep is None or self.rep.rank == 0))
         out_state: Dict[str, Dict] = {}
         for u in self.units:
             st = optimizer.state.get(u.shard_param, {})

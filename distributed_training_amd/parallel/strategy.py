@@ -101,7 +101,8 @@ class DDPStrategy(DistributedStrategy):
 class FSDPStrategy(DistributedStrategy):
     def __init__(self, is_gpu: bool, wrap_policy: Any = None, mixed_precision: Optional[str] = None,
                  reshard_after_forward: bool = True, prefetch: bool = True, comm: Optional[Communicator] = None,
-                 cpu_offload: bool = False, reduce_dtype: Optional[str] = None) -> None:
+                 cpu_offload: bool = False, reduce_dtype: Optional[str] = None, sharding: str = "full",
+                 hybrid_shard_size: Optional[int] = None) -> None:
         self.is_gpu = is_gpu
         # the reference offloads only when there is no GPU (fsdp_strategy.py:23-25), where this
         # engine's shards live on the host anyway; on a GPU run it is an explicit opt-in
@@ -109,6 +110,13 @@ class FSDPStrategy(DistributedStrategy):
         self.wrap_policy = wrap_policy
         self.param_dtype = _DTYPES[mixed_precision] if mixed_precision else torch.float32
         self.reduce_dtype = _DTYPES[reduce_dtype] if reduce_dtype else None  # None: the compute dtype
+        # "full" (FULL_SHARD over all ranks, the reference's default) or "hybrid" (HYBRID_SHARD: shard
+        # within groups of hybrid_shard_size ranks -- default torchrun's LOCAL_WORLD_SIZE, one node --
+        # and replicate across them)
+        if sharding not in ("full", "hybrid"):
+            raise ValueError(f"FSDP sharding must be 'full' or 'hybrid', not {sharding!r}")
+        self.sharding = sharding
+        self.hybrid_shard_size = hybrid_shard_size
         self.reshard_after_forward = reshard_after_forward
         self.prefetch = prefetch
         self.comm = comm
@@ -118,8 +126,21 @@ class FSDPStrategy(DistributedStrategy):
 
         dev = _as_device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if self.is_gpu else torch.device("cpu"))
-        comm = self.comm or default_comm(dev)
+        rep = None
+        if self.sharding == "hybrid" and self.comm is None:
+            import os
+
+            import torch.distributed as dist
+
+            from .comm import make_hybrid_comms
+
+            ws = dist.get_world_size() if dist.is_initialized() else 1
+            size = int(self.hybrid_shard_size or os.environ.get("LOCAL_WORLD_SIZE", ws))
+            comm, rep = make_hybrid_comms(dev, size)
+        else:
+            comm = self.comm or default_comm(dev)
         return FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=self.wrap_policy,
+                                        replicate_comm=rep,
                                         param_dtype=self.param_dtype,
                                         reshard_after_forward=self.reshard_after_forward, prefetch=self.prefetch,
                                         cpu_offload=self.cpu_offload and dev.type == "cuda",

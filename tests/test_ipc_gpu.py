@@ -605,3 +605,46 @@ def test_fsdp_optimizer_in_backward_multi_rank_shared_gpu(ws):
     global-batch reference (_engine_worker)."""
     run_gloo(_fsdp_overlap_bitwise_worker, ws)
     run_gloo(_engine_worker, ws, "fsdp", True)
+
+
+def _hsdp_worker(rank, ws, shard_size):
+    """HYBRID sharding on the shared GPU (IPC communicators per shard / replica group): the same
+    trajectory as the one-rank reference on the global batch, replicas identical across groups."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.models.gpt2 import GPT2
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import make_hybrid_comms
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    B, T, steps = 2, 64, 3
+    g = torch.Generator(device="cpu").manual_seed(15)
+    glob = [torch.randint(0, 512, (ws * B, T + 1), generator=g).to(dev) for _ in range(steps)]
+    ref = FullyShardedDataParallel(_tiny_gpt2().to(dev), comm=IpcComm(0, 1, dev, tag="hsdp_ref"), device=dev,
+                                   wrap_policy={GPT2.block_class}, param_dtype=torch.bfloat16)
+    init_sd = {k: v.float().cpu().clone() for k, v in ref.full_state_dict(rank0_only=False).items()}
+    _train(ref, FusedSGD(ref.parameters(), lr=0.05, momentum=0.9), glob, steps)
+    ref_sd = {k: v.float().cpu() for k, v in ref.full_state_dict(rank0_only=False).items()}
+    shard, rep = make_hybrid_comms(dev, shard_size)
+    w = FullyShardedDataParallel(_tiny_gpt2().to(dev), comm=shard, device=dev, wrap_policy={GPT2.block_class},
+                                 param_dtype=torch.bfloat16, replicate_comm=rep)
+    assert w.rep is not None and w.world_size == shard_size
+    _train(w, FusedSGD(w.parameters(), lr=0.05, momentum=0.9), [x[rank * B:(rank + 1) * B] for x in glob], steps)
+    shard.poll_errors()
+    rep.poll_errors()
+    sd = {k: v.float().cpu() for k, v in w.full_state_dict(rank0_only=False).items()}
+    for k, v in sd.items():
+        moved = (ref_sd[k] - init_sd[k]).abs().max().item()
+        assert (v - ref_sd[k]).abs().max().item() <= 0.05 * moved + 1e-5, k
+    parts = _gather_cpu(torch.cat([v.reshape(-1) for v in sd.values()]))
+    assert all(torch.equal(parts[0], p) for p in parts), "replicas diverged"
+    dist.barrier()
+    shard.destroy()
+    rep.destroy()
+
+
+@pytest.mark.parametrize("ws,shard_size", [(4, 2)])
+def test_hybrid_shard_shared_gpu(ws, shard_size):
+    run_gloo(_hsdp_worker, ws, shard_size)

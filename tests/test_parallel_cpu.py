@@ -549,3 +549,73 @@ def test_fsdp_reduce_dtype_pins_bf16_reduction_error(ws):
     assert errs["fp32"] < 1e-6, errs
     assert errs["bf16"] < 2 ** -7, errs
     assert errs["fp32"] < errs["bf16"], errs
+
+
+def _hsdp_worker(rank, ws, shard_size, opt_name):
+    """HYBRID sharding over gloo: shard groups of ``shard_size`` ranks, replicas across them; every
+    rank trains on its own micro-batch and the result matches one process on the global batch."""
+    from distributed_training_amd.ops.optim import FusedAdamW, FusedSGD
+    from distributed_training_amd.parallel.comm import make_hybrid_comms
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.manual_seed(0)
+    ref = Net()
+    m = copy.deepcopy(ref)
+    if rank % 2:  # replicas start from replica 0 (sync_module_states), whatever their own init
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(0.25)
+        torch.manual_seed(0)
+        m = copy.deepcopy(ref) if shard_size > 1 and rank % shard_size else m
+    shard, rep = make_hybrid_comms(torch.device("cpu"), shard_size)
+    assert shard.world_size == shard_size and rep.world_size == ws // shard_size
+    fs = FullyShardedDataParallel(m, shard, torch.device("cpu"), wrap_policy={Block}, replicate_comm=rep)
+    assert (fs.rep is None) == (ws // shard_size == 1)
+    if opt_name == "adamw":
+        o1, o2 = torch.optim.AdamW(ref.parameters(), lr=1e-2), FusedAdamW(fs.parameters(), lr=1e-2)
+    else:
+        o1 = torch.optim.SGD(ref.parameters(), lr=1e-1, momentum=0.9)
+        o2 = FusedSGD(fs.parameters(), lr=1e-1, momentum=0.9)
+    for it in range(3):
+        g = torch.Generator().manual_seed(200 + it)
+        X, Y = torch.randn(8 * ws, 20, generator=g), torch.randn(8 * ws, 1, generator=g)
+        o1.zero_grad(set_to_none=True)
+        o2.zero_grad(set_to_none=True)
+        F.mse_loss(ref(X), Y).backward()
+        F.mse_loss(fs(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+        o1.step()
+        o2.step()
+    sd = fs.full_state_dict(rank0_only=False)
+    for k, v in ref.state_dict().items():
+        torch.testing.assert_close(sd[k], v, rtol=1e-4, atol=1e-5, msg=k)
+    # rank0_only: only the global rank 0 keeps the state dict
+    sd0 = fs.full_state_dict(rank0_only=True)
+    assert (len(sd0) > 0) == (rank == 0)
+
+
+@pytest.mark.parametrize("ws,shard_size,opt_name", [(4, 2, "adamw"), (4, 2, "sgd"), (8, 4, "adamw"), (4, 1, "sgd"),
+                                                    (4, 4, "adamw")])
+def test_hybrid_shard_matches_single_process(ws, shard_size, opt_name):
+    """HSDP (torch HYBRID_SHARD): FSDP within shard groups (one node's GPUs: xGMI gathers and
+    reduce-scatters), one gradient all-reduce across the replica groups (the inter-node fabric);
+    also the degenerate sizes 1 (pure replication) and ws (plain FULL_SHARD)."""
+    run_gloo(_hsdp_worker, ws, shard_size, opt_name)
+
+
+def test_hybrid_shard_strategy_from_config():
+    """train.fsdp_sharding=hybrid / hybrid_shard_size map onto the FSDP strategy."""
+    from pathlib import Path
+
+    from distributed_training_amd.app import training_config_from
+    from distributed_training_amd.config import compose
+    from distributed_training_amd.parallel.strategy import FSDPStrategy
+
+    conf = Path(__file__).resolve().parent.parent / "conf"
+    cfg = compose(conf, "config", ["train.parallel_strategy=fsdp", "+train.fsdp_sharding=hybrid",
+                                   "+train.hybrid_shard_size=2"])
+    tc = training_config_from(cfg)
+    assert tc.fsdp_sharding == "hybrid" and int(tc.hybrid_shard_size) == 2
+    st = FSDPStrategy(False, sharding=tc.fsdp_sharding, hybrid_shard_size=tc.hybrid_shard_size)
+    assert st.sharding == "hybrid"
+    with pytest.raises(ValueError):
+        FSDPStrategy(False, sharding="hsdp2")
