@@ -554,6 +554,8 @@ class FullyShardedDataParallel(nn.Module):
     def forward(self, *args: Any, **kwargs: Any) -> Any:
         if self._defer_wgrad and torch.is_grad_enabled():
             _lm().new_forward_generation()  # (native Linear counts weight uses per forward: single-use -> deferrable)
+            if self._rs_waiting and not any(u.in_backward for u in self.units):
+                self._rs_waiting = []  # left by a backward that raised before its end: never reduce-scattered
         if self.prefetch and not self._record_order and self._fwd_order:
             self._fwd_order[0].unshard(async_op=True)  # the first unit (the embedding) in flight with the root's
         if self.root_unit is not None:
