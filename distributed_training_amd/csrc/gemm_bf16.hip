@@ -118,7 +118,7 @@ __device__ __forceinline__ void lds_bar() { asm volatile("s_barrier" ::: "memory
 // One BM x BN output tile `t` (row-major tile index of the problem, already
 // XCD-remapped) of the problem `g`: the body of gemm_bf16_kernel and of
 // gemm_group_kernel.
-template <int BM, int BN, bool AT, bool BT, bool PP, bool CS>
+template <int BM, int BN, bool AT, bool BT, bool PP, bool CS, bool BUF>
 __device__ __forceinline__ void gemm_tile(const GemmBfArgs& g, const int t) {
   constexpr int A_BYTES = BM * kGbBK * 2, B_BYTES = BN * kGbBK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int WTM = BM / 2, WTN = BN / 4, MT = WTM / 16, NT = WTN / 16;
@@ -165,13 +165,32 @@ __device__ __forceinline__ void gemm_tile(const GemmBfArgs& g, const int t) {
   }
   const int64_t stepA = AT ? (int64_t)kGbBK * g.lda : kGbBK;
   const int64_t stepB = BT ? (int64_t)kGbBK * g.ldb : kGbBK;
+  // BUF: the pieces through buffer descriptors (32-bit lane offsets, scalar stage step: gemm_k64.hip
+  // kFlatDma note); the host takes it when every operand byte lies within 2 GiB of its base
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.a), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.b), 0, 0x7fffffff, 0x00020000);
+  unsigned voA[AL], voB[BL];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int j = 0; j < AL; ++j) voA[j] = (unsigned)((srcA[j] - g.a) * 2);
+#pragma unroll
+    for (int j = 0; j < BL; ++j) voB[j] = (unsigned)((srcB[j] - g.b) * 2);
+  }
   auto issue = [&](int s) {
     char* sa = lds + (s & (kGbStages - 1)) * STAGE;
     char* sb = sa + A_BYTES;
+    if constexpr (BUF) {
+      const unsigned soa = (unsigned)(s * stepA * 2), sob = (unsigned)(s * stepB * 2);
 #pragma unroll
-    for (int j = 0; j < AL; ++j) glds16(srcA[j] + s * stepA, sa + (wave * AL + j) * 1024);
+      for (int j = 0; j < AL; ++j) bglds16(rsA, voA[j], soa, sa + (wave * AL + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < BL; ++j) glds16(srcB[j] + s * stepB, sb + (wave * BL + j) * 1024);
+      for (int j = 0; j < BL; ++j) bglds16(rsB, voB[j], sob, sb + (wave * BL + j) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < AL; ++j) glds16(srcA[j] + s * stepA, sa + (wave * AL + j) * 1024);
+#pragma unroll
+      for (int j = 0; j < BL; ++j) glds16(srcB[j] + s * stepB, sb + (wave * BL + j) * 1024);
+    }
   };
 
   f32x4 acc[NT][MT];
@@ -378,9 +397,14 @@ __device__ __forceinline__ void gemm_tile(const GemmBfArgs& g, const int t) {
   }
 }
 
-template <int BM, int BN, bool AT, bool BT, bool PP>
+template <int BM, int BN, bool AT, bool BT, bool PP, bool BUF>
 __global__ void __launch_bounds__(512) gemm_bf16_kernel(GemmBfArgs g) {
-  gemm_tile<BM, BN, AT, BT, PP, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  gemm_tile<BM, BN, AT, BT, PP, false, BUF>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+}
+
+// every byte an operand spans within 2 GiB of its base: the buffer-descriptor DMA form applies
+static inline bool bf_fits_2g(int64_t rows_minus1, int64_t ld, int64_t cols) {
+  return 2 * (rows_minus1 * ld + cols) < 0x7fffffffLL;
 }
 
 // Grouped weight gradients: several independent problems (dW_i = dy_i^T x_i, each with
@@ -396,18 +420,24 @@ struct GemmGroupArgs {
   GemmBfArgs p[kGroupMax];
 };
 
+template <bool BUF>
 __global__ void __launch_bounds__(512) gemm_group_kernel(GemmGroupArgs ga) {
   const int t = xcd_remap(blockIdx.x, ga.tile_start[ga.n]);
   int q = 0;
   while (q + 1 < ga.n && t >= ga.tile_start[q + 1]) ++q;
-  gemm_tile<256, 256, true, true, true, true>(ga.p[q], t - ga.tile_start[q]);
+  gemm_tile<256, 256, true, true, true, true, BUF>(ga.p[q], t - ga.tile_start[q]);
 }
 
 template <int BM, int BN, bool AT, bool BT>
 static hipError_t launch_bf(const GemmBfArgs& g, hipStream_t st) {
   // static LDS: 4 x (BM + BN) x 64 B (128 KiB at 256 x 256: one workgroup per CU)
   constexpr bool PP = BM == 256 && BN == 256;  // ping-pong schedule for the big tile
-  hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
+  const bool buf = (AT ? bf_fits_2g(g.K - 1, g.lda, g.M) : bf_fits_2g(g.M - 1, g.lda, g.K)) &&
+                   (BT ? bf_fits_2g(g.K - 1, g.ldb, g.N) : bf_fits_2g(g.N - 1, g.ldb, g.K));
+  if (buf)
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP, true>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, AT, BT, PP, false>), dim3(g.tiles_m * g.tiles_n), dim3(512), 0, st, g);
   return hipGetLastError();
 }
 
@@ -518,6 +548,12 @@ hipError_t dta_gemm_wgrad_group(int n, const void* const* a, const int64_t* lda,
     total += g.tiles_m * g.tiles_n;
   }
   ga.tile_start[n] = total;
-  hipLaunchKernelGGL(gemm_group_kernel, dim3(total), dim3(512), 0, st, ga);
+  bool buf = true;
+  for (int i = 0; i < n; ++i)
+    buf = buf && bf_fits_2g(K[i] - 1, lda[i], M[i]) && bf_fits_2g(K[i] - 1, ldb[i], N[i]);
+  if (buf)
+    hipLaunchKernelGGL(gemm_group_kernel<true>, dim3(total), dim3(512), 0, st, ga);
+  else
+    hipLaunchKernelGGL(gemm_group_kernel<false>, dim3(total), dim3(512), 0, st, ga);
   return hipGetLastError();
 }

@@ -225,7 +225,7 @@ struct Cfg {
   static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
 };
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH>
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF>
 __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   using C = Cfg<BM, BN, WC, AT, BT>;
   constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
@@ -277,17 +277,43 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   }
   const int64_t stepA = AT ? (int64_t)BK * g.lda : BK;
   const int64_t stepB = BT ? (int64_t)BK * g.ldb : BK;
+  // BUF: the same pieces through buffer descriptors (32-bit lane offsets, scalar K-step); the host
+  // takes this form only when every operand byte lies within 4 GiB of its base
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.a), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.b), 0, 0x7fffffff, 0x00020000);
+  unsigned voA[2][LA], voB[2][LB];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < LA; ++j) voA[h][j] = (unsigned)((srcA[h][j] - g.a) * 2);
+#pragma unroll
+      for (int j = 0; j < LB; ++j) voB[h][j] = (unsigned)((srcB[h][j] - g.b) * 2);
+    }
+  }
   auto dma_a = [&](int h, int kt) {  // A half h of K-tile kt (past the end: the last K-tile, never read)
     const int ks = min(kt, nk - 1);
     char* dst = lds + (kt & 1) * C::BUF + h * C::A_HALF;
+    if constexpr (BUF) {
+      const unsigned so = (unsigned)(ks * stepA * 2);
 #pragma unroll
-    for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
+      for (int j = 0; j < LA; ++j) bglds16(rsA, voA[h][j], so, dst + (j * NW + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
+    }
   };
   auto dma_b = [&](int h, int kt) {
     const int ks = min(kt, nk - 1);
     char* dst = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+    if constexpr (BUF) {
+      const unsigned so = (unsigned)(ks * stepB * 2);
 #pragma unroll
-    for (int j = 0; j < LB; ++j) glds16(srcB[h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
+      for (int j = 0; j < LB; ++j) bglds16(rsB, voB[h][j], so, dst + (j * NW + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int j = 0; j < LB; ++j) glds16(srcB[h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
+    }
   };
 
   // ---- fragment reads: the wave's quadrant of a half ----
@@ -469,26 +495,39 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   }
 }
 
-template <int BM, int BN, int WC, bool AT, bool BT>
+template <int BM, int BN, int WC, bool AT, bool BT, bool BUF>
 static hipError_t launch(const Args& g, int ph, hipStream_t st) {
   if (ph == 2)
-    hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st, g);
+    hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st,
+                       g);
   else
-    hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 4>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st, g);
+    hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 4, BUF>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st,
+                       g);
   return hipGetLastError();
 }
 
+template <int BM, int BN, int WC, bool BUF>
+static hipError_t launch_l(const Args& g, bool at, bool bt, int ph, hipStream_t st) {
+  if (!at && !bt) return launch<BM, BN, WC, false, false, BUF>(g, ph, st);
+  if (!at && bt) return launch<BM, BN, WC, false, true, BUF>(g, ph, st);
+  if (at && bt) return launch<BM, BN, WC, true, true, BUF>(g, ph, st);
+  return launch<BM, BN, WC, true, false, BUF>(g, ph, st);
+}
+
 template <int BM, int BN, int WC>
-static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, hipStream_t st) {
-  if (!at && !bt) return launch<BM, BN, WC, false, false>(g, ph, st);
-  if (!at && bt) return launch<BM, BN, WC, false, true>(g, ph, st);
-  if (at && bt) return launch<BM, BN, WC, true, true>(g, ph, st);
-  return launch<BM, BN, WC, true, false>(g, ph, st);
+static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, bool buf, hipStream_t st) {
+  return buf ? launch_l<BM, BN, WC, true>(g, at, bt, ph, st) : launch_l<BM, BN, WC, false>(g, at, bt, ph, st);
 }
 
 // tile ids: 1 = 256x256 (8 waves), 2 = 256x128 (8 waves), 3 = 128x128 (4 waves), 4 = 128x256 (8 waves);
 // id + kTiles: the same tile with the two-phase K loop
 constexpr int kTiles = 4;
+// LDS-DMA form: buffer descriptors (bglds16) by default wherever every operand byte lies within 2 GiB
+// of its base -- 1-5 % faster than flat global_load_lds at the GPT-2 / Llama shapes, never slower
+// beyond noise (scripts/bench_k64buf.py, profiles/k64_buffer_dma.jsonl); tile-id bit kFlatDma forces
+// the flat form (A/B), kBufDma is accepted for compatibility (= the default)
+constexpr int kBufDma = 16;
+constexpr int kFlatDma = 32;
 __host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
 __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
 
@@ -502,6 +541,11 @@ using namespace dta;
 // relative efficiency (bigger tiles reuse more per byte).
 int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   if (K % k64::BK || K < k64::BK) return 0;
+  if (tile & (k64::kBufDma | k64::kFlatDma)) {  // the same tile, DMA form chosen explicitly
+    const int bits = tile & (k64::kBufDma | k64::kFlatDma);
+    const int t = dta_gemm_k64_tile(M, N, K, tile & ~bits);
+    return t ? (t | bits) : 0;
+  }
   auto fits = [&](int t) { return M % k64::tile_bm(t) == 0 && N % k64::tile_bn(t) == 0; };
   if (tile) {
     const int base = tile > k64::kTiles ? tile - k64::kTiles : tile;
@@ -536,6 +580,13 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
                         const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st) {
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
+  bool buf = (tile & k64::kFlatDma) == 0;
+  tile &= ~(k64::kBufDma | k64::kFlatDma);
+  if (buf) {  // 32-bit offsets: every byte of A and B within 2 GiB of its base (descriptor range)
+    const int64_t a_bytes = 2 * (a_t ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
+    const int64_t b_bytes = 2 * (b_t ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);
+    buf = a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL;
+  }
   if (c32 && epi != k64::EPI_NONE) return hipErrorInvalidValue;
   k64::Args g{};
   g.a = static_cast<const bf16*>(a);
@@ -564,9 +615,9 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   g.tiles_m = M / k64::tile_bm(tile);
   g.tiles_n = N / k64::tile_bn(tile);
   switch (tile) {
-    case 1: return k64::launch_t<256, 256, 4>(g, a_t, b_t, ph, st);
-    case 2: return k64::launch_t<256, 128, 4>(g, a_t, b_t, ph, st);
-    case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, ph, st);
-    default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, ph, st);
+    case 1: return k64::launch_t<256, 256, 4>(g, a_t, b_t, ph, buf, st);
+    case 2: return k64::launch_t<256, 128, 4>(g, a_t, b_t, ph, buf, st);
+    case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, ph, buf, st);
+    default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, ph, buf, st);
   }
 }
