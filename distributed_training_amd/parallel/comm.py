@@ -201,6 +201,7 @@ class CommWatchdog:
         self.error: Optional[str] = None
         self._pending: Deque[Tuple[object, float, str]] = collections.deque()
         self._lock = threading.Lock()
+        self._fire = threading.Lock()  # held by the one thread that runs the abort
         self._stop = threading.Event()
         self._reported = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -230,19 +231,26 @@ class CommWatchdog:
             head = self._pending[0] if self._pending else None
         if head is None or now - head[1] <= self.timeout_s:
             return False
-        self.error = (f"{self.name}: collective '{head[2]}' not complete {now - head[1]:.1f} s after its enqueue "
-                      f"(DTA_COMM_TIMEOUT_S={self.timeout_s:g}); communicator aborted")
-        print(f"[dta watchdog] {self.error}", file=sys.stderr, flush=True)
+        if not self._fire.acquire(blocking=False):
+            return True  # another thread is aborting; its error is published when the abort returned
+        msg = (f"{self.name}: collective '{head[2]}' not complete {now - head[1]:.1f} s after its enqueue "
+               f"(DTA_COMM_TIMEOUT_S={self.timeout_s:g}); communicator aborted")
+        print(f"[dta watchdog] {msg}", file=sys.stderr, flush=True)
         try:
             self.on_timeout()
         except Exception as e:  # noqa: BLE001 - the error is reported either way
             print(f"[dta watchdog] abort failed: {e}", file=sys.stderr, flush=True)
+        # published AFTER the abort: a training thread that raises has an aborted communicator (a test
+        # saw the RuntimeError before the abort had run when the error was set first)
+        self.error = msg
         return True
 
     def _run(self) -> None:
         while not self._stop.wait(self.poll_s):
             if self.check():
                 break
+        while self.error is None and not self._stop.wait(0.01):  # (the other thread's abort still running)
+            pass
         if self.error is None or self._stop.is_set():
             return
         if os.environ.get("DTA_COMM_TIMEOUT_EXIT", "1") != "0" and not self._reported.wait(self.exit_grace_s):
