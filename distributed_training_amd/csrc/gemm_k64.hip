@@ -92,6 +92,7 @@ struct Args {
   int tiles_m, tiles_n;
   float alpha;
   int epi;
+  bf16* db;  // weight-gradient groups: the bias gradient db[m] = sum_k A(m, k) (nullptr: none)
 #ifdef DTA_K64_STAMP
   unsigned long long* stamps;  // diagnostic build only: per-wave cycle sums of the two-phase loop's segments
 #endif
@@ -225,8 +226,9 @@ struct Cfg {
   static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
 };
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF>
-__global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS>
+__device__ __forceinline__ void k64_body(const Args& g, const int t) {
+  static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
   using C = Cfg<BM, BN, WC, AT, BT>;
   constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
   constexpr bool STAG = WC == 4;  // two waves per SIMD: stagger the halves
@@ -236,8 +238,7 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WC, wc = wave % WC;
 
-  // ---- tile ----
-  const int t = xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n);
+  // ---- tile (t: this problem's tile index, XCD-remapped by the caller) ----
   const int per_group = kGroupM * g.tiles_n;
   const int grp = t / per_group, in_g = t - grp * per_group;
   const int gm0 = grp * kGroupM, gh = min(kGroupM, g.tiles_m - gm0);
@@ -360,6 +361,27 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
+  // CS (tile column 0 of a weight-gradient problem): db[m] = sum_k A(m, k) from MFMAs against an
+  // all-ones B fragment -- the four waves sharing A rows split the row fragments (wave wc takes
+  // fragment jj = wc of each half: 4 extra MFMAs per K-tile, +6 % on those workgroups only)
+  const bool do_cs = CS && g.db != nullptr && n0 == 0;
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  auto mma_cs = [&](const bf16x8 (&af)[MTH][2], int mh) {
+    if constexpr (CS) {
+      if (do_cs) {
+        const bf16 one = f2bf(1.f);
+        const bf16x8 ones = {one, one, one, one, one, one, one, one};
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jj = 0; jj < MTH; ++jj)
+          if (jj == wc) {
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) accb[mh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[jj][kk], accb[mh], 0, 0, 0);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
 
   bf16x8 af[MTH][2], b0[NTH][2], b1[NTH][2];
   if constexpr (PH == 4) {
@@ -447,6 +469,7 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
     K64_STAMP(2);
     mma(af, b0, 0, 0);
     mma(af, b1, 0, 1);
+    mma_cs(af, 0);
     K64_STAMP(3);
     bar();
     K64_STAMP(4);
@@ -462,6 +485,7 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
     K64_STAMP(7);
     mma(af, b1, 1, 1);
     mma(af, b0, 1, 0);
+    mma_cs(af, 1);
     K64_STAMP(8);
     bar();
     K64_STAMP(9);
@@ -479,6 +503,12 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
     if (wr == 0) bar();  // equal barrier counts for both halves
   }
 
+  if constexpr (CS) {
+    if (do_cs && wc < MTH && (lane >> 4) == 0) {  // (the four columns of accb are equal)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) g.db[m0 + h * HA + wr * (HA / 2) + 16 * wc + lane] = f2bf(accb[h][0]);
+    }
+  }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment ----
 #pragma unroll
   for (int i = 0; i < 2 * NTH; ++i) {
@@ -493,6 +523,30 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
       store4(g, m, n, acc[i][j], bv);
     }
   }
+}
+
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF>
+__global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
+  k64_body<BM, BN, WC, AT, BT, PH, BUF, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+}
+
+// Grouped weight gradients (csrc/gemm_bf16.hip gemm_group_kernel's contract on this kernel's 64-deep
+// two-phase loop): dW_i = A_i^T B_i for several problems in ONE launch of 256 x 256 tiles over the
+// full token reduction, the bias gradients from the same MFMA pipe (CS); the tiles of all problems
+// form one list, XCD-remapped so each XCD takes a contiguous run.
+constexpr int kGroupMax = 16;
+struct GroupArgs {
+  int n;
+  int tile_start[kGroupMax + 1];
+  Args p[kGroupMax];
+};
+
+template <bool BUF>
+__global__ void __launch_bounds__(512) gemm_k64_group_kernel(GroupArgs ga) {
+  const int t = xcd_remap(blockIdx.x, ga.tile_start[ga.n]);
+  int q = 0;
+  while (q + 1 < ga.n && t >= ga.tile_start[q + 1]) ++q;
+  k64_body<256, 256, 4, true, true, 2, BUF, true>(ga.p[q], t - ga.tile_start[q]);
 }
 
 template <int BM, int BN, int WC, bool AT, bool BT, bool BUF>
@@ -620,4 +674,46 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
     case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, ph, buf, st);
     default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, ph, buf, st);
   }
+}
+
+// n problems dW_i[M_i][N_i] (bf16, row stride ldc_i) = A_i^T B_i, A_i = dy [K_i][M_i] (lda_i), B_i = x [K_i][N_i]
+// (ldb_i); db_i (bf16 [M_i] or nullptr) = column sums of A_i.  M_i, N_i multiples of 256, K_i of 64.
+int dta_gemm_k64_group_max() { return k64::kGroupMax; }
+
+hipError_t dta_gemm_k64_wgrad_group(int n, const void* const* a, const int64_t* lda, const void* const* b,
+                                    const int64_t* ldb, void* const* c, const int64_t* ldc, const int* M, const int* N,
+                                    const int* K, void* const* db, hipStream_t st) {
+  if (n < 1 || n > k64::kGroupMax) return hipErrorInvalidValue;
+  k64::GroupArgs ga{};
+  ga.n = n;
+  int total = 0;
+  bool buf = true;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] % 256 || N[i] % 256 || K[i] % k64::BK || K[i] < k64::BK) return hipErrorInvalidValue;
+    k64::Args& g = ga.p[i];
+    g.a = static_cast<const bf16*>(a[i]);
+    g.b = static_cast<const bf16*>(b[i]);
+    g.c = static_cast<bf16*>(c[i]);
+    g.lda = lda[i];
+    g.ldb = ldb[i];
+    g.ldc = ldc[i];
+    g.M = M[i];
+    g.N = N[i];
+    g.K = K[i];
+    g.tiles_m = M[i] / 256;
+    g.tiles_n = N[i] / 256;
+    g.alpha = 1.f;
+    g.epi = k64::EPI_NONE;
+    g.db = static_cast<bf16*>(db[i]);
+    ga.tile_start[i] = total;
+    total += g.tiles_m * g.tiles_n;
+    buf = buf && 2 * ((int64_t)(K[i] - 1) * lda[i] + M[i]) < 0x7fffffffLL &&
+          2 * ((int64_t)(K[i] - 1) * ldb[i] + N[i]) < 0x7fffffffLL;
+  }
+  ga.tile_start[n] = total;
+  if (buf)
+    hipLaunchKernelGGL(k64::gemm_k64_group_kernel<true>, dim3(total), dim3(512), 0, st, ga);
+  else
+    hipLaunchKernelGGL(k64::gemm_k64_group_kernel<false>, dim3(total), dim3(512), 0, st, ga);
+  return hipGetLastError();
 }

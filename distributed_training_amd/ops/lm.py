@@ -597,11 +597,14 @@ def wgrad_flush() -> None:
     _DEFER.clear()
     _DEFER_TILES[0] = 0
     C = native()
-    gmax = C.gemm_group_max()
+    # csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop) when every reduction is a multiple of
+    # 64 tokens (DTA_WGRAD_GROUP_K64=0: the round-2 kernel), else csrc/gemm_bf16.hip's
+    k64 = os.environ.get("DTA_WGRAD_GROUP_K64", "1") != "0" and all(it[0].shape[0] % 64 == 0 for it in items)
+    gmax = C.gemm64_group_max() if k64 else C.gemm_group_max()
     for i in range(0, len(items), gmax):
         part = items[i:i + gmax]
         C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
-                           [it[3] for it in part], -1)
+                           [it[3] for it in part], -1, k64)
     GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
     for fn in list(FLUSH_LISTENERS):
         fn()

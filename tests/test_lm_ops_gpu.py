@@ -518,13 +518,17 @@ def test_ddp_deferred_grouped_weight_gradients(threshold, monkeypatch):
             assert _rel(p.grad, rp[name].grad) < 2e-2, (threshold, it, name)
 
 
-def test_gemm_wgrad_group_vs_fp32():
+@pytest.mark.parametrize("k64", [False, True])
+def test_gemm_wgrad_group_vs_fp32(k64):
     """The grouped weight-gradient launch (256 x 256 tiles, full token reduction, bias gradient
-    on the MFMA pipe) on problems of different shapes and K, strided operands, vs fp32 torch."""
+    on the MFMA pipe) on problems of different shapes and K, strided operands, vs fp32 torch --
+    the round-2 kernel (32-deep stages, K multiples of 32) and csrc/gemm_k64.hip's (64-deep
+    two-phase loop; the bias columns split over the waves sharing A rows)."""
     from distributed_training_amd.ops import native
 
     torch.manual_seed(12)
-    shapes = [(1024, 512, 256), (2048, 256, 768), (512, 768, 512), (96, 256, 256)]  # (K, M, N)
+    shapes = [(1024, 512, 256), (2048, 256, 768), (512, 768, 512), (96 if not k64 else 192, 256, 256),
+              (8192, 768, 768)]  # (K, M, N)
     A, B, Cs, D = [], [], [], []
     for K, M, N in shapes:
         wide = torch.randn(K, M + 64, device=DEV).bfloat16()
@@ -533,7 +537,7 @@ def test_gemm_wgrad_group_vs_fp32():
         Cs.append(torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
         D.append(torch.empty(M, device=DEV, dtype=torch.bfloat16))
     D[1] = None  # a problem without bias
-    native().gemm_wgrad_group(A, B, Cs, D)
+    native().gemm_wgrad_group(A, B, Cs, D, -1, k64)
     for i in range(len(shapes)):
         assert _rel(Cs[i], A[i].float().t() @ B[i].float()) < 1e-2, i
         if D[i] is not None:
