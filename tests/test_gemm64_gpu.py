@@ -138,8 +138,9 @@ def test_gemm64_busy_chip(a_t, b_t, tile):
     """Llama-sized problems (1024-2048 workgroups, 64 K-steps, every CU busy), where DMA latency
     varies: a wait placed one barrier too late for the leading wave group of the staggered 8-wave
     loops read stale LDS here (rel. error 0.17 on the 256 x 128 two-phase tile before the fix) while
-    every small-shape test passed (profiles/k64_twophase_race_fix.txt).  Random N(0,1) operands, three launches each, against an fp32
-    product of the same bf16 inputs.  Tile ids | 32: the flat global_load_lds DMA form (default: buffer descriptors)."""
+    every small-shape test passed (profiles/k64_twophase_race_fix.txt).  Random N(0,1) operands, three
+    launches each, against an fp32 product of the same bf16 inputs.  Tile ids | 32: the flat
+    global_load_lds DMA form (default: buffer descriptors)."""
     from distributed_training_amd.ops import native
 
     gen = torch.Generator(device="cuda").manual_seed(tile * 7 + 2 * a_t + b_t)
