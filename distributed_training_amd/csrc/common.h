@@ -178,9 +178,9 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_base) {
 // to the wave-uniform LDS address `lds_base` + 16 * lane.  Against global_load_lds (a 64-bit flat
 // address per lane, advanced by a 64-bit VALU add per piece and K-step) the lane supplies a 32-bit
 // offset fixed for the whole K loop and the K-step moves the scalar soffset.
-__device__ __forceinline__ void bglds16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, char* lds_base) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_base);
+// `dst`: the wave-uniform LDS byte address itself (lds_addr of the staging array + offsets in
+// scalar registers: no per-piece generic -> LDS pointer conversion with its null check)
+__device__ __forceinline__ void bglds16(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned dst) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
@@ -188,6 +188,11 @@ __device__ __forceinline__ void bglds16(__amdgpu_buffer_rsrc_t rsrc, unsigned vo
       : "=&s"(keep)
       : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
       : "memory");
+}
+
+// LDS byte address of a __shared__ object (wave-uniform)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) char*)p);
 }
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU_TANH = 2, ACT_SILU = 3 };

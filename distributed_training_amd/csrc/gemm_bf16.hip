@@ -181,10 +181,11 @@ __device__ __forceinline__ void gemm_tile(const GemmBfArgs& g, const int t) {
     char* sb = sa + A_BYTES;
     if constexpr (BUF) {
       const unsigned soa = (unsigned)(s * stepA * 2), sob = (unsigned)(s * stepB * 2);
+      const unsigned da = lds_addr(lds) + (s & (kGbStages - 1)) * STAGE, db = da + A_BYTES;
 #pragma unroll
-      for (int j = 0; j < AL; ++j) bglds16(rsA, voA[j], soa, sa + (wave * AL + j) * 1024);
+      for (int j = 0; j < AL; ++j) bglds16(rsA, voA[j], soa, da + (wave * AL + j) * 1024);
 #pragma unroll
-      for (int j = 0; j < BL; ++j) bglds16(rsB, voB[j], sob, sb + (wave * BL + j) * 1024);
+      for (int j = 0; j < BL; ++j) bglds16(rsB, voB[j], sob, db + (wave * BL + j) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < AL; ++j) glds16(srcA[j] + s * stepA, sa + (wave * AL + j) * 1024);

@@ -292,13 +292,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
       for (int j = 0; j < LB; ++j) voB[h][j] = (unsigned)((srcB[h][j] - g.b) * 2);
     }
   }
+  const unsigned lds0 = lds_addr(lds);
   auto dma_a = [&](int h, int kt) {  // A half h of K-tile kt (past the end: the last K-tile, never read)
     const int ks = min(kt, nk - 1);
     char* dst = lds + (kt & 1) * C::BUF + h * C::A_HALF;
     if constexpr (BUF) {
-      const unsigned so = (unsigned)(ks * stepA * 2);
+      const unsigned so = (unsigned)(ks * stepA * 2), d0 = lds0 + (kt & 1) * C::BUF + h * C::A_HALF;
 #pragma unroll
-      for (int j = 0; j < LA; ++j) bglds16(rsA, voA[h][j], so, dst + (j * NW + wave) * 1024);
+      for (int j = 0; j < LA; ++j) bglds16(rsA, voA[h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
@@ -308,9 +309,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     const int ks = min(kt, nk - 1);
     char* dst = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
     if constexpr (BUF) {
-      const unsigned so = (unsigned)(ks * stepB * 2);
+      const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
 #pragma unroll
-      for (int j = 0; j < LB; ++j) bglds16(rsB, voB[h][j], so, dst + (j * NW + wave) * 1024);
+      for (int j = 0; j < LB; ++j) bglds16(rsB, voB[h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < LB; ++j) glds16(srcB[h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
