@@ -70,6 +70,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dta {
 namespace k64 {
@@ -293,11 +294,24 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     }
   }
   const unsigned lds0 = lds_addr(lds);
+  // LDS layout ILV: [A-top p0 | A-top p1 | A-bottom p0 | A-bottom p1 | B-left p0 | B-left p1 | B-right p0
+  // | B-right p1] (p = K-tile parity): with the two-phase loop unrolled by two K-tiles the parity is a
+  // compile-time constant and every fragment read is a loop-invariant lane base + an immediate offset
+  // (no per-K-tile address arithmetic: 36 VALU per K-tile in the M/N-major layouts before); otherwise
+  // [p0: A-top | A-bottom | B-left | B-right][p1: ...] with runtime parity
+  // (the 256 x 256 tile with buffer-descriptor DMA only: measured 0-9 % faster there at every GPT-2 /
+  // Llama shape and up to 14 % on the long-K weight gradients, while the 128-wide tiles lost ~10 % at
+  // K = 768 and the flat-DMA 256 x 256 form spilled; profiles/k64_buffer_dma.jsonl notes)
+  constexpr bool ILV = BM == 256 && BN == 256 && BUF;
+  auto aoff = [&](int h, int par) { return ILV ? (2 * h + par) * C::A_HALF : par * C::BUF + h * C::A_HALF; };
+  auto boff = [&](int h, int par) {
+    return ILV ? 4 * C::A_HALF + (2 * h + par) * C::B_HALF : par * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+  };
   auto dma_a = [&](int h, int kt) {  // A half h of K-tile kt (past the end: the last K-tile, never read)
     const int ks = min(kt, nk - 1);
-    char* dst = lds + (kt & 1) * C::BUF + h * C::A_HALF;
+    char* dst = lds + aoff(h, kt & 1);
     if constexpr (BUF) {
-      const unsigned so = (unsigned)(ks * stepA * 2), d0 = lds0 + (kt & 1) * C::BUF + h * C::A_HALF;
+      const unsigned so = (unsigned)(ks * stepA * 2), d0 = lds0 + aoff(h, kt & 1);
 #pragma unroll
       for (int j = 0; j < LA; ++j) bglds16(rsA, voA[h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
@@ -307,9 +321,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   };
   auto dma_b = [&](int h, int kt) {
     const int ks = min(kt, nk - 1);
-    char* dst = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+    char* dst = lds + boff(h, kt & 1);
     if constexpr (BUF) {
-      const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+      const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + boff(h, kt & 1);
 #pragma unroll
       for (int j = 0; j < LB; ++j) bglds16(rsB, voB[h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
@@ -320,7 +334,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 
   // ---- fragment reads: the wave's quadrant of a half ----
   auto read_a = [&](bf16x8 (&af)[MTH][2], int kt, int h) {
-    const char* img = lds + (kt & 1) * C::BUF + h * C::A_HALF;
+    const char* img = lds + aoff(h, kt & 1);
 #pragma unroll
     for (int jj = 0; jj < MTH; ++jj)
 #pragma unroll
@@ -331,7 +345,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
       }
   };
   auto read_b = [&](bf16x8 (&bf)[NTH][2], int kt, int h) {
-    const char* img = lds + (kt & 1) * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
+    const char* img = lds + boff(h, kt & 1);
 #pragma unroll
     for (int ii = 0; ii < NTH; ++ii)
 #pragma unroll
@@ -457,11 +471,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   unsigned long long seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = stamp_now();
 #endif
-  for (int kt = 0; kt < nk; ++kt) {
-    read_a(af, kt, 0);
-    read_b(b0, kt, 0);
-    read_b(b1, kt, 1);
-    dma_a(1, kt + 1);
+  // kt2: kt with its parity as a compile-time constant (P = 0 / 1), so (kt2 & 1) folds into immediates;
+  // P = -1: runtime parity (every tile but the buffer-DMA 256 x 256 one)
+  auto ktile = [&](const int kt, auto P) {
+    const int kt2 = decltype(P)::value < 0 ? kt : ((kt & ~1) | decltype(P)::value);
+    read_a(af, kt2, 0);
+    read_b(b0, kt2, 0);
+    read_b(b1, kt2, 1);
+    dma_a(1, kt2 + 1);
     K64_STAMP(0);
     lgkm0();
     vm_wait<2 * LA + 2 * LB>();  // bottom (t)
@@ -474,10 +491,10 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     K64_STAMP(3);
     bar();
     K64_STAMP(4);
-    read_a(af, kt, 1);
-    dma_a(0, kt + 2);
-    dma_b(0, kt + 2);
-    dma_b(1, kt + 2);
+    read_a(af, kt2, 1);
+    dma_a(0, kt2 + 2);
+    dma_b(0, kt2 + 2);
+    dma_b(1, kt2 + 2);
     K64_STAMP(5);
     lgkm0();
     vm_wait<2 * LA + 2 * LB>();  // top, left, right (t+1)
@@ -490,6 +507,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     K64_STAMP(8);
     bar();
     K64_STAMP(9);
+  };
+  if constexpr (ILV) {
+    for (int kt = 0; kt < nk; kt += 2) {
+      ktile(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nk) ktile(kt + 1, std::integral_constant<int, 1>{});
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) ktile(kt, std::integral_constant<int, -1>{});
   }
 #ifdef DTA_K64_STAMP
   if (lane == 0) {
