@@ -34,7 +34,7 @@ from ..ops import native
 
 logger = logging.getLogger(__name__)
 _TRACE = bool(os.environ.get("DTA_BENCH_TRACE"))
-_ONE_FIRST_LAUNCH = os.environ.get("DTA_SPLIT_FIRST_LAUNCH", "0") == "0"  # opt-in (=1) until measured on the GPU
+_ONE_FIRST_LAUNCH = os.environ.get("DTA_SPLIT_FIRST_LAUNCH", "1") == "0"  # A/B switch (profiles/headline_split_first_launch.txt)
 
 
 def fused_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, device: torch.device) -> Optional[str]:
