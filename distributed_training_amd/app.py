@@ -30,6 +30,9 @@ def _get(node: Any, key: str, default: Any = None) -> Any:
     return getattr(node, key, default)
 
 
+_LM_NAMES = ("gpt2", "gpt2_small", "llama", "llama3", "llama3_8b")
+
+
 def build_model(cfg_model: Any) -> torch.nn.Module:
     name = str(_get(cfg_model, "name", "") or "")
     if name in ("gpt2", "gpt2_small"):
@@ -61,7 +64,14 @@ def load_train_objs(cfg: Any) -> Tuple[Dataset, torch.nn.Module, torch.optim.Opt
     seed = _get(cfg.train, "seed", None)
     if seed is not None:
         torch.manual_seed(int(seed))
-    model = build_model(cfg.model)
+    name = str(_get(cfg.model, "name", "") or "")
+    if name in _LM_NAMES and bool(_get(cfg.train, "meta_init", True)):
+        # shapes only: the Trainer materialises on the device (DDP) or unit by unit into the shards
+        # (FSDP) -- never 32 GB of fp32 per rank on the host at 8B (models/init.py)
+        with torch.device("meta"):
+            model = build_model(cfg.model)
+    else:
+        model = build_model(cfg.model)
     if hasattr(model, "vocab_size"):
         train_set = SyntheticTokens(int(cfg.train.dataset_size), int(_get(cfg.train, "seq_len", 1024)),
                                     model.vocab_size, seed=int(seed or 0))

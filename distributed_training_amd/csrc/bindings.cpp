@@ -719,8 +719,12 @@ class PyRcclComm {
   }
   void group_start() { comm_->group_start(); }
   void group_end() { comm_->group_end(); }
-  void abort() { comm_->abort(); }
-  void destroy() { comm_.reset(); }
+  // the RcclComm object lives as long as this wrapper: abort / destroy only release the RCCL handle
+  // (under the communicator's own lock), so a concurrent call on another thread raises
+  // "communicator aborted" instead of touching freed memory
+  bool abort(int drain_ms) { return comm_->abort(drain_ms); }
+  void destroy() { comm_->destroy(); }
+  bool aborted() const { return comm_->aborted(); }
   int rank() const { return comm_->rank(); }
   int size() const { return comm_->size(); }
 
@@ -1161,17 +1165,20 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("max_elems", &PyP2PAllReduce::max_elems);
   py::class_<PyRcclComm>(m, "RcclComm")
       .def(py::init<py::bytes, int, int, int>())
-      .def("all_reduce", &PyRcclComm::all_reduce)
-      .def("all_gather", &PyRcclComm::all_gather)
-      .def("reduce_scatter", &PyRcclComm::reduce_scatter)
-      .def("broadcast", &PyRcclComm::broadcast)
-      .def("send", &PyRcclComm::send)
-      .def("recv", &PyRcclComm::recv)
-      .def("all_to_all", &PyRcclComm::all_to_all)
+      // the GIL is released around every enqueue, so the watchdog thread's abort can run while the
+      // training thread is inside RCCL (the communicator's own lock orders the two)
+      .def("all_reduce", &PyRcclComm::all_reduce, py::call_guard<py::gil_scoped_release>())
+      .def("all_gather", &PyRcclComm::all_gather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &PyRcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &PyRcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("send", &PyRcclComm::send, py::call_guard<py::gil_scoped_release>())
+      .def("recv", &PyRcclComm::recv, py::call_guard<py::gil_scoped_release>())
+      .def("all_to_all", &PyRcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
       .def("group_start", &PyRcclComm::group_start)
-      .def("group_end", &PyRcclComm::group_end)
-      .def("abort", &PyRcclComm::abort)
-      .def("destroy", &PyRcclComm::destroy)
+      .def("group_end", &PyRcclComm::group_end, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &PyRcclComm::abort, py::arg("drain_ms") = 10000, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &PyRcclComm::destroy, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &PyRcclComm::aborted)
       .def_property_readonly("rank", &PyRcclComm::rank)
       .def_property_readonly("size", &PyRcclComm::size);
 }

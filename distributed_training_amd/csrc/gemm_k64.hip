@@ -68,6 +68,7 @@
 //    issue cost (8 per stage, ~60 cycles each: MI355X_MICROARCH.md) lands on the only wave of the
 //    SIMD, where the 8-wave form hands it to the partner wave.
 #include "common.h"
+#include "gemm_epi.h"
 
 #include <cstdlib>
 #include <type_traits>
@@ -75,91 +76,6 @@
 namespace dta {
 namespace k64 {
 
-constexpr int BK = 64;
-constexpr int kGroupM = 8;
-
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 2, EPI_DGELU = 16, EPI_RES = 32 };
-
-struct Args {
-  const bf16* a;
-  const bf16* b;
-  bf16* c;          // bf16 output (EPI_GELU with c2: the pre-activation)
-  bf16* c2;         // EPI_GELU: the activation gelu(c) (nullptr: c holds the activation)
-  float* c32;       // fp32 output instead of c (EPI_NONE only)
-  const bf16* bias; // [N] or nullptr
-  const bf16* res;  // EPI_DGELU: the GELU input; EPI_RES: added after rounding
-  int64_t lda, ldb, ldc, ldc2, ldr;
-  int M, N, K;
-  int tiles_m, tiles_n;
-  float alpha;
-  int epi;
-  bf16* db;  // weight-gradient groups: the bias gradient db[m] = sum_k A(m, k) (nullptr: none)
-#ifdef DTA_K64_STAMP
-  unsigned long long* stamps;  // diagnostic build only: per-wave cycle sums of the two-phase loop's segments
-#endif
-};
-
-// GELU (tanh form) as x * sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of tanhf
-__device__ __forceinline__ float gelu_fast(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  return x * __frcp_rn(1.f + __expf(-2.f * u));
-}
-__device__ __forceinline__ float gelu_grad_fast(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float s = __frcp_rn(1.f + __expf(-2.f * u));  // sigmoid(2u) = (1 + tanh u) / 2
-  // d/dx [x s] = s + x s (1 - s) 2 du/dx
-  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
-}
-
-// ---- shared epilogue: bias of columns n .. n+3, and one lane's four accumulators (row m, columns n .. n+3) ----
-__device__ __forceinline__ void load_bias4(const Args& g, int n, float (&bv)[4]) {
-  bv[0] = bv[1] = bv[2] = bv[3] = 0.f;
-  if (g.bias) {
-    const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(g.bias + n);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[r] = bf2f(b4[r]);
-  }
-}
-
-__device__ __forceinline__ void store4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4]) {
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
-  if (g.c32) {
-    *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-    return;
-  }
-  if (g.epi == EPI_GELU) {
-    if (g.c2) {  // dual store: pre-activation h (for the backward) and gelu(h) (the next GEMM's input)
-      const bf16x4 h4 = pk4_bf16(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = h4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gelu_fast(bf2f(h4[r]));  // gelu of the stored (rounded) h
-      *reinterpret_cast<bf16x4*>(g.c2 + (int64_t)m * g.ldc2 + n) = pk4_bf16(v[0], v[1], v[2], v[3]);
-      return;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
-  } else if (g.epi == EPI_DGELU) {  // dgrad through the GELU: one rounding (of the product)
-    const bf16x4 h4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_fast(bf2f(h4[r]));
-  } else if (g.epi == EPI_RES) {  // residual stream: round(round(linear) + res), as two bf16 ops give
-    const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);
-  }
-  *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = pk4_bf16(v[0], v[1], v[2], v[3]);
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
 
 #ifdef DTA_K64_STAMP
 // s_memtime with its lgkmcnt(0) in ONE statement (cdna_hip_programming.md "In-kernel stamps"); the
@@ -551,6 +467,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   }
 }
 
+
 template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF>
 __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   k64_body<BM, BN, WC, AT, BT, PH, BUF, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
@@ -607,6 +524,8 @@ constexpr int kTiles = 4;
 // beyond noise (scripts/bench_k64buf.py, profiles/k64_buffer_dma.jsonl); tile-id bit kFlatDma forces
 // the flat form (A/B), kBufDma is accepted for compatibility (= the default)
 constexpr int kBufDma = 16;
+// the 4-wave 256 x 256 tile with intra-wave read / MFMA overlap (w4_body): NT only (A [M][K], B [N][K])
+constexpr int kW4 = 9;
 constexpr int kFlatDma = 32;
 __host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
 __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
@@ -616,11 +535,14 @@ __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128
 
 using namespace dta;
 
+hipError_t dta_gemm_w4_launch(const k64::Args& g, hipStream_t st);  // csrc/gemm_w4.hip
+
 // 0 if the tile does not cover the problem, else the tile id (1-4, or 5-8 for the same tiles with
 // the two-phase K loop).  tile = 0: the fewest rounds of resident workgroups weighted by the tile's
 // relative efficiency (bigger tiles reuse more per byte).
 int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   if (K % k64::BK || K < k64::BK) return 0;
+  if (tile == k64::kW4) return K % (2 * k64::BK) == 0 ? tile : 0;  // (any M, N: clamped DMA rows, predicated stores)
   if (tile & (k64::kBufDma | k64::kFlatDma)) {  // the same tile, DMA form chosen explicitly
     const int bits = tile & (k64::kBufDma | k64::kFlatDma);
     const int t = dta_gemm_k64_tile(M, N, K, tile & ~bits);
@@ -660,6 +582,33 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
                         const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st) {
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
+  if (tile == k64::kW4) {
+    // buffer-descriptor DMA with 32-bit offsets: every operand byte within 2 GiB of its base
+    if (a_t || b_t || 2 * ((int64_t)(M - 1) * lda + K) >= 0x7fffffffLL || 2 * ((int64_t)(N - 1) * ldb + K) >= 0x7fffffffLL)
+      return hipErrorInvalidValue;
+    if (c32 && epi != k64::EPI_NONE) return hipErrorInvalidValue;
+    k64::Args g{};
+    g.a = static_cast<const bf16*>(a);
+    g.b = static_cast<const bf16*>(b);
+    g.c = static_cast<bf16*>(c);
+    g.c2 = static_cast<bf16*>(c2);
+    g.c32 = c32;
+    g.bias = static_cast<const bf16*>(bias);
+    g.res = static_cast<const bf16*>(res);
+    g.lda = lda;
+    g.ldb = ldb;
+    g.ldc = ldc;
+    g.ldc2 = ldc2;
+    g.ldr = ldr;
+    g.M = M;
+    g.N = N;
+    g.K = K;
+    g.alpha = alpha;
+    g.epi = epi;
+    g.tiles_m = (M + 255) / 256;
+    g.tiles_n = (N + 255) / 256;
+    return dta_gemm_w4_launch(g, st);
+  }
   bool buf = (tile & k64::kFlatDma) == 0;
   tile &= ~(k64::kBufDma | k64::kFlatDma);
   if (buf) {  // 32-bit offsets: every byte of A and B within 2 GiB of its base (descriptor range)

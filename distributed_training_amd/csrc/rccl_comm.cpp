@@ -13,7 +13,9 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 
 namespace dta {
@@ -76,37 +78,64 @@ RcclComm::RcclComm(const std::string& unique_id, int nranks, int rank, int devic
   check(g_api.CommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
 }
 
-RcclComm::~RcclComm() {
-  if (comm_ && g_api.CommDestroy) g_api.CommDestroy(comm_);
-  comm_ = nullptr;
+RcclComm::~RcclComm() { destroy(); }
+
+std::shared_lock<std::shared_timed_mutex> RcclComm::use() {
+  std::shared_lock<std::shared_timed_mutex> lk(mu_);
+  if (aborted_.load() || comm_ == nullptr) throw std::runtime_error("RCCL communicator aborted");
+  return lk;
 }
 
-void RcclComm::abort() {
-  if (comm_) g_api.CommAbort(comm_);
+bool RcclComm::abort(int drain_ms) {
+  if (aborted_.exchange(true)) return true;  // (a second abort: the first one owns the handle)
+  std::unique_lock<std::shared_timed_mutex> lk(mu_, std::defer_lock);
+  const bool drained = lk.try_lock_for(std::chrono::milliseconds(drain_ms > 0 ? drain_ms : 0));
+  ncclComm_t c = comm_;
+  if (c) g_api.CommAbort(c);
+  if (drained) comm_ = nullptr;  // else the stuck call still references it: leaked, never freed twice
+  return drained;
+}
+
+void RcclComm::destroy() {
+  if (aborted_.exchange(true)) return;
+  std::unique_lock<std::shared_timed_mutex> lk(mu_);
+  if (comm_ && g_api.CommDestroy) g_api.CommDestroy(comm_);
   comm_ = nullptr;
 }
 
 void RcclComm::all_reduce(const void* src, void* dst, size_t count, ncclDataType_t dt, ncclRedOp_t op,
                           hipStream_t st) {
+  auto lk = use();
   check(g_api.AllReduce(src, dst, count, dt, op, comm_, st), "ncclAllReduce");
 }
 void RcclComm::all_gather(const void* src, void* dst, size_t count, ncclDataType_t dt, hipStream_t st) {
+  auto lk = use();
   check(g_api.AllGather(src, dst, count, dt, comm_, st), "ncclAllGather");
 }
 void RcclComm::reduce_scatter(const void* src, void* dst, size_t count, ncclDataType_t dt, ncclRedOp_t op,
                               hipStream_t st) {
+  auto lk = use();
   check(g_api.ReduceScatter(src, dst, count, dt, op, comm_, st), "ncclReduceScatter");
 }
 void RcclComm::broadcast(const void* src, void* dst, size_t count, ncclDataType_t dt, int root, hipStream_t st) {
+  auto lk = use();
   check(g_api.Broadcast(src, dst, count, dt, root, comm_, st), "ncclBroadcast");
 }
 void RcclComm::send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t st) {
+  auto lk = use();
   check(g_api.Send(buf, count, dt, peer, comm_, st), "ncclSend");
 }
 void RcclComm::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t st) {
+  auto lk = use();
   check(g_api.Recv(buf, count, dt, peer, comm_, st), "ncclRecv");
 }
-void RcclComm::group_start() { check(g_api.GroupStart(), "ncclGroupStart"); }
-void RcclComm::group_end() { check(g_api.GroupEnd(), "ncclGroupEnd"); }
+void RcclComm::group_start() {
+  auto lk = use();
+  check(g_api.GroupStart(), "ncclGroupStart");
+}
+void RcclComm::group_end() {
+  auto lk = use();
+  check(g_api.GroupEnd(), "ncclGroupEnd");
+}
 
 }  // namespace dta

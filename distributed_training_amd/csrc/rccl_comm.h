@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <shared_mutex>
 #include <string>
 
 namespace dta {
@@ -37,6 +39,16 @@ std::string rccl_load(const std::string& path);
 bool rccl_loaded();
 const RcclApi& rccl_api();
 
+// Thread safety (the c10d watchdog contract of the reference's init_process_group,
+// src/distributed_trainer.py:61-62): a watchdog thread may call abort() while the
+// training thread is enqueueing a collective.  Every op holds a SHARED lock on the
+// handle for the duration of its ncclXxx call; abort()/destroy() first flag the
+// communicator (new calls raise "communicator aborted" without touching it), then
+// take the EXCLUSIVE lock, so the handle is released only after every in-flight
+// enqueue has returned.  An enqueue stuck inside RCCL (a dead peer during a
+// connection setup) would hold its shared lock forever: after `drain_ms` abort()
+// calls ncclCommAbort without the lock -- the documented way to unblock such a call
+// -- and the handle is left to that call (never destroyed here).
 class RcclComm {
  public:
   RcclComm(const std::string& unique_id, int nranks, int rank, int device);
@@ -50,12 +62,19 @@ class RcclComm {
   void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t st);
   void group_start();
   void group_end();
-  void abort();
+  // returns true if every in-flight enqueue drained before the abort
+  bool abort(int drain_ms = 10000);
+  void destroy();
+  bool aborted() const { return aborted_.load(); }
   int rank() const { return rank_; }
   int size() const { return nranks_; }
 
  private:
+  // shared lock on a live handle, or throws "communicator aborted"
+  std::shared_lock<std::shared_timed_mutex> use();
   ncclComm_t comm_ = nullptr;
+  std::shared_timed_mutex mu_;
+  std::atomic<bool> aborted_{false};
   int rank_, nranks_, device_;
 };
 

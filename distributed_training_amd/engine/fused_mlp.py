@@ -34,7 +34,6 @@ from ..ops import native
 
 logger = logging.getLogger(__name__)
 _TRACE = bool(os.environ.get("DTA_BENCH_TRACE"))
-_ONE_FIRST_LAUNCH = os.environ.get("DTA_SPLIT_FIRST_LAUNCH", "1") == "0"  # A/B switch (profiles/headline_split_first_launch.txt)
 
 
 def fused_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, device: torch.device) -> Optional[str]:
@@ -473,10 +472,12 @@ class FusedMLPProgram:
             self._ensure(min(2 * self.chunk_steps, self.R - self.steps_per_epoch))
         while self.launched < end:
             k = min(end - self.launched, self.chunk_steps)
-            if self.launched == 0 and n > 1 and not _ONE_FIRST_LAUNCH:
+            if self.launched == 0 and n > 1:
                 # the first call (the warm-up) runs its steps as two launches, 1 + rest: on the
                 # gpurun boxes the SECOND launch of the program paid ~14-17 us inside
-                # hipLaunchKernel (the third ~1 us), which otherwise lands on the first timed call
+                # hipLaunchKernel (the third ~1 us), which otherwise lands on the first timed call.
+                # Warm-up accounting only -- the per-step kernel time is unchanged
+                # (profiles/headline_split_first_launch.txt)
                 k = 1
             self._ensure(self.launched + k)
             if self._up_done is not None:

@@ -141,8 +141,18 @@ class Trainer:
 
     def _setup_model(self, model: torch.nn.Module) -> torch.nn.Module:
         device = self.env.torch_device.index if self.env.is_gpu else self.env.device
-        model = model.to(self.device)
         self._strategy = self._make_strategy()
+        from ..models.init import init_buffers_, is_meta, materialize_
+
+        if is_meta(model):
+            # built on the meta device (app.load_train_objs, LM configs): never initialised on the host.
+            # FSDP materialises unit by unit into its shards; DDP allocates and initialises on the device
+            if isinstance(self._strategy, FSDPStrategy):
+                init_buffers_(model, self.device)
+            else:
+                materialize_(model, self.device)
+        else:
+            model = model.to(self.device)
         self.checkpoint = ModelCheckpoint(Path(self.config.snapshot_path), self.env, self._strategy)
         original_params = [p for g in self.optimizer.param_groups for p in g["params"]]
         model = self._strategy.prepare_model(model, self.device)
@@ -262,6 +272,7 @@ class Trainer:
         sampler = self.train_data.sampler
         assert isinstance(sampler, (DtaSampler, torch.utils.data.distributed.DistributedSampler))
         t0 = time.perf_counter()
+        loss_sum: Optional[torch.Tensor] = None  # this rank's epoch loss, summed on the device (no per-step sync)
         if self._fused is not None:
             steps = self._fused.run_epoch(epoch)
         else:
@@ -271,7 +282,10 @@ class Trainer:
             for source, targets in self.train_data:
                 source = source.to(dev, non_blocking=True)
                 targets = targets.to(dev, non_blocking=True)
-                self._run_batch(source, targets)
+                loss = self._run_batch(source, targets)
+                if self.config.log_throughput and loss is not None:
+                    lf = loss.detach().float()
+                    loss_sum = lf if loss_sum is None else loss_sum + lf
                 steps += 1
                 self._maybe_inject_fault(epoch, steps)
         if self.config.log_throughput or self.config.desync_check_every:
@@ -281,7 +295,11 @@ class Trainer:
             samples = len(sampler) * self.env.world_size
             self.last_epoch_stats = {"epoch": epoch, "steps": steps, "seconds": dt, "samples_per_s": samples / dt}
             if self.config.log_throughput:
-                logger.info(f"Epoch {epoch} | {steps} steps | {dt * 1e3:.2f} ms | {samples / dt:,.0f} samples/s")
+                msg = f"Epoch {epoch} | {steps} steps | {dt * 1e3:.2f} ms | {samples / dt:,.0f} samples/s"
+                if loss_sum is not None and steps:
+                    self.last_epoch_stats["loss"] = float(loss_sum.item()) / steps
+                    msg += f" | loss {self.last_epoch_stats['loss']:.4f}"
+                logger.info(msg)
         if self.config.desync_check_every and (epoch + 1) % self.config.desync_check_every == 0:
             from ..utils.desync import check_replicas_in_sync
 

@@ -137,6 +137,18 @@ class GPT2(nn.Module):
         elif isinstance(m, nn.Embedding):
             nn.init.normal_(m.weight, 0.0, 0.02)
 
+    def init_param(self, name: str, t: torch.Tensor, gen: torch.Generator) -> None:
+        """The initial value of parameter ``name`` (the same distributions as ``__init__``) drawn into
+        ``t`` -- materialisation of a model built on the meta device (models/init.py)."""
+        if name.endswith("c_proj.weight"):
+            t.normal_(0.0, 0.02 / math.sqrt(2 * self.cfg.n_layer), generator=gen)
+        elif t.dim() >= 2:  # embeddings and Linear weights
+            t.normal_(0.0, 0.02, generator=gen)
+        elif name.endswith("bias"):
+            t.zero_()
+        else:  # LayerNorm weights
+            t.fill_(1.0)
+
     def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 

@@ -120,6 +120,21 @@ class Llama(nn.Module):
                 s = std / math.sqrt(2 * cfg.n_layer) if n.endswith(("wo.weight", "w2.weight")) else std
                 nn.init.normal_(p, 0.0, s)
 
+    def init_param(self, name: str, t: torch.Tensor, gen: torch.Generator) -> None:
+        """The initial value of parameter ``name`` (the distributions of ``__init__``) drawn into ``t``:
+        materialisation of a model built on the meta device (models/init.py)."""
+        if t.dim() >= 2:
+            std = 0.02 / math.sqrt(2 * self.cfg.n_layer) if name.endswith(("wo.weight", "w2.weight")) else 0.02
+            t.normal_(0.0, std, generator=gen)
+        else:  # RMSNorm weights
+            t.fill_(1.0)
+
+    def init_buffers(self, device: torch.device) -> None:
+        """The RoPE tables (non-persistent buffers), computed on the host in fp64 and moved."""
+        cos, sin = lm.rope_tables(self.cfg.block_size, self.cfg.n_embd // self.cfg.n_head, self.cfg.rope_theta,
+                                  device=device)
+        self.rope_cos, self.rope_sin = cos, sin
+
     def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 

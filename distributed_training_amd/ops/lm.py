@@ -228,7 +228,7 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
 
 # ------------------------------------------------------------------ GEMM dispatch
 _GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 0 = hipBLASLt
-GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "side_wgrad": 0, "deferred_wgrad": 0, "group_launches": 0}
+GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "deferred_wgrad": 0, "group_launches": 0}
 
 
 def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 4) -> Dict[int, float]:
@@ -451,29 +451,14 @@ def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return group.grad_view(i)
 
 
-# ------------------------------------------------------------------ side-stream weight gradients
-# Nothing on the backward's critical path reads a weight gradient: the chain is
-# dgrad -> norm / activation / attention backward -> the next layer's dgrad.  With
-# ``DTA_WGRAD_STREAM=2`` (opt-in; 0 = off) the weight (and bias) gradients that go straight into a DDP
-# flat-buffer slice run on a second HIP stream, concurrently with that chain, on the
-# split-K kernel at split 2 (half the fp32 slab traffic of its own chip-filling split:
-# the chain's kernels fill the CUs it leaves free).
-# Joins: every DDP bucket launch and the end of the backward make the current
-# stream wait for the side stream (:func:`wgrad_join`).  Only a weight used ONCE
-# in the forward takes this path (a second use's gradient would be summed with
-# the side stream's result by autograd on the current stream): the DDP engine
-# opens a forward generation per call (:func:`new_forward_generation`) and the
-# native Linear counts its uses in it; without a DDP engine (no generations) no
-# weight qualifies.  Measured on the GPT-2 small DDP step (one MI355X,
-# same-box A/B pairs, round 2): 11.9-12.45 -> 11.4-12.2 ms with the 128 x 128
-# split-K kernel at split 2 on one side stream in 6 of 8 pairs, but 12.4 -> 15.6 / 18.2 ms
-# on one box (the hardware scheduler's interleaving of the two queues is not under
-# this code's control), so it is not the default; its own split 11.5, split 1 12.3 ms; the
-# general GEMM's 256 x 256 tile at split 1 serialises on the side stream (17.9 ms); a
-# second stream for the attention dQ kernel (concurrent with dK/dV) lost 0.1-0.25 ms.
-_SIDE: Dict[int, torch.cuda.Stream] = {}
-_SIDE_PENDING: Dict[int, bool] = {}
-_SIDE_CB = [False]
+# ------------------------------------------------------------------ end-of-backward join
+# Nothing on the backward's critical path reads a weight gradient (the chain is dgrad -> norm /
+# activation / attention backward -> the next layer's dgrad), so weight gradients may be deferred
+# (below) and must be joined before anything reads them: every DDP bucket launch and the end of
+# the backward call :func:`wgrad_join`.  (Round 2 also ran them on a second HIP stream; it won in
+# 6 of 8 same-box pairs but lost 25-45 % on one box -- the hardware scheduler's interleaving of
+# two queues is not under this code's control -- and was removed in round 4.)
+_SIDE_CB = [False]  # the end-of-backward join callback is queued
 _FWD_GEN = [0]
 
 
@@ -485,10 +470,14 @@ def new_forward_generation() -> None:
     """Start counting native-Linear weight uses afresh (called per DDP forward)."""
     if _GEN_USES[0] == 0:  # (a no-grad forward: no backward will close it)
         _CLOSED_GEN[0] = _FWD_GEN[0]
-    if _CLOSED_GEN[0] == _FWD_GEN[0]:  # the previous step's backward ran to its end
-        _SIDE_CB[0] = False  # (a backward that raised never ran its end-of-backward join callback)
-        _DEFER.clear()  # (nor flushed what it deferred: those gradients belong to an abandoned step)
-        _DEFER_TILES[0] = 0
+    # After a normal backward the end-of-backward join has emptied the queue, so this reset is a
+    # no-op there; after a backward that RAISED (generation left open) it drops the abandoned step's
+    # deferred (dy, x, dest) entries and re-arms the join callback -- otherwise the next backward
+    # would never queue its flush (_SIDE_CB stuck) and would flush stale entries into the same
+    # flat-gradient slices as its own (two groups writing one destination in one launch).
+    _SIDE_CB[0] = False
+    _DEFER.clear()
+    _DEFER_TILES[0] = 0
     _FWD_GEN[0] += 1
     _GEN_USES[0] = 0
 
@@ -527,28 +516,15 @@ def _single_use(w: Optional[torch.Tensor]) -> bool:
         and getattr(w, "_dta_uses", 0) == 1
 
 
-def _side_split() -> int:
-    """``DTA_WGRAD_STREAM``: 0 = off (default); n > 0 = side stream with split n (2 measured best;
-    split 1 leaves too few workgroups, the kernel's own choice (~4-5) fills the chip the chain needs)."""
-    v = os.environ.get("DTA_WGRAD_STREAM", "0")
-    return max(0, int(v)) if v.strip() else 0
-
-
 def wgrad_join(device: Optional[torch.device] = None) -> None:
     """Every weight gradient of this backward written: the deferred ones launched
-    (:func:`wgrad_flush`) and the current stream made to wait for the side stream."""
+    (:func:`wgrad_flush`) on the current stream."""
     wgrad_flush()
-    idx = torch.cuda.current_device() if device is None else (device.index or 0)
-    if _SIDE_PENDING.get(idx):
-        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
-        _SIDE_PENDING[idx] = False
 
 
 def _end_of_backward_join() -> None:
     _SIDE_CB[0] = False
     wgrad_flush()
-    for idx in list(_SIDE_PENDING):
-        wgrad_join(torch.device("cuda", idx))
 
 
 def _queue_end_join() -> None:
@@ -610,16 +586,6 @@ def wgrad_flush() -> None:
         fn()
 
 
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    s = _SIDE.get(idx)
-    if s is None:
-        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
-    _queue_end_join()
-    _SIDE_PENDING[idx] = True
-    return s
-
-
 def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
                  b: Optional[torch.Tensor] = None) -> Any:
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
@@ -636,7 +602,6 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
         x2 = x2.contiguous() if x2.stride(0) % 8 else x2
         cw = _grad_dest(w)
-        split = _side_split()
         cb = _grad_dest(b) if with_bias else None
         thr = _group_threshold()
         if thr and cw is not None and (cb is not None or not with_bias) \
@@ -655,22 +620,6 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             _queue_end_join()
             if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm_group_max():
                 wgrad_flush()
-            return (cw, cb) if with_bias else cw
-        if split and cw is not None and (cb is not None or not with_bias) and getattr(w, "_dta_gdest", None) is None \
-                and _single_use(w):
-            # both results land in flat-buffer slices: nothing reads them before a join
-            main = torch.cuda.current_stream(dy2.device)
-            ss = _side_stream(dy2.device)
-            ss.wait_stream(main)
-            with torch.cuda.stream(ss):
-                split = min(split, K // 32)
-                if with_bias:
-                    native().gemm_tn_colsum(dy2, x2, False, split, -1, cw, cb)
-                else:
-                    native().gemm_tn(dy2, x2, False, split, -1, cw)
-            dy2.record_stream(ss)
-            x2.record_stream(ss)
-            GEMM_STATS["side_wgrad"] += 1
             return (cw, cb) if with_bias else cw
         if with_bias:
             dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
@@ -918,8 +867,9 @@ def swiglu(ab: torch.Tensor) -> Any:
 # ------------------------------------------------------------------ rotary
 def rope_tables(seq_len: int, head_dim: int, theta: float = 10000.0,
                 device: Any = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
-    t = torch.arange(seq_len, dtype=torch.float64)
+    # (on the host explicitly: under a ``torch.device("meta")`` build the tables still get values)
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64, device="cpu") / head_dim))
+    t = torch.arange(seq_len, dtype=torch.float64, device="cpu")
     f = torch.outer(t, inv)
     return f.cos().float().to(device), f.sin().float().to(device)
 

@@ -45,6 +45,17 @@ def _split_params(group_params: Any) -> Any:
     return [(flat_objs[k], v) for k, v in flats.items()], singles
 
 
+def _cpu_target(p: torch.Tensor) -> Any:
+    """The tensor a CPU-side update must write for parameter ``p``: under bf16 mixed precision a
+    DDP / FSDP flat-group parameter is the bf16 COMPUTE view, and the update belongs in its fp32
+    master (which checkpoints save), then copied back -- updating the compute view alone left the
+    master, and every snapshot of a CPU mixed-precision run, at the initial weights."""
+    tag = getattr(p, "_dta_flat", None)
+    if tag is not None and getattr(tag[0], "mixed", False):
+        return tag[0].master_view(tag[1]), True
+    return p, False
+
+
 def _sgd_ref(p: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor], lr: float, momentum: float,
              dampening: float, wd: float, nesterov: bool, maximize: bool, first: bool) -> None:
     d = -g if maximize else g
@@ -167,7 +178,10 @@ class FusedSGD(torch.optim.Optimizer):
                                       None if buf is None else buf.view(-1), None, lr, mom, damp, wd, 1.0, nest,
                                       maxi, first, -1)
                 else:
-                    _sgd_ref(p, p.grad, buf, lr, mom, damp, wd, nest, maxi, first)
+                    tgt, sync = _cpu_target(p)
+                    _sgd_ref(tgt, p.grad.to(tgt.dtype), buf, lr, mom, damp, wd, nest, maxi, first)
+                    if sync:
+                        p.copy_(tgt)
         return loss
 
     # -------------------------------------------------- step split over DDP buckets
@@ -325,8 +339,11 @@ class FusedAdamW(torch.optim.Optimizer):
                                        b1, b2, eps, wd, 1.0, adamw, maxi, ams, True, -1)
                 else:
                     state["step"] += 1
-                    _adam_ref(p, p.grad, state["exp_avg"], state["exp_avg_sq"], state.get("max_exp_avg_sq"),
-                              float(state["step"]), lr, b1, b2, eps, wd, adamw, maxi, ams)
+                    tgt, sync = _cpu_target(p)
+                    _adam_ref(tgt, p.grad.to(tgt.dtype), state["exp_avg"], state["exp_avg_sq"],
+                              state.get("max_exp_avg_sq"), float(state["step"]), lr, b1, b2, eps, wd, adamw, maxi, ams)
+                    if sync:
+                        p.copy_(tgt)
         return loss
 
     zero_grad = FusedSGD.zero_grad

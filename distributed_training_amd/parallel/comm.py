@@ -284,7 +284,19 @@ class _StreamComm(Communicator):
         self.raise_if_error()
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)
-        fn(int(self.stream.cuda_stream))
+        try:
+            fn(int(self.stream.cuda_stream))
+        except RuntimeError:
+            # the watchdog aborted the communicator while this enqueue raced it: report ITS error
+            # (and tell it the training thread has seen the timeout) rather than the bare abort --
+            # it is published once the abort call returns, so wait for that briefly
+            wd = self.watchdog
+            if wd is not None:
+                deadline = time.monotonic() + 30.0
+                while wd.error is None and wd._fire.locked() and time.monotonic() < deadline:
+                    time.sleep(0.005)
+            self.raise_if_error()
+            raise
         for t in tensors:  # keep the caching allocator from recycling the memory early
             t.record_stream(self.stream)
         ev = torch.cuda.Event()
@@ -388,7 +400,10 @@ class RcclComm(_StreamComm):
         self._enqueue(lambda s: self._comm.all_to_all(out, inp, s), False, [out, inp], "all_to_all")
 
     def abort(self) -> None:
-        """``ncclCommAbort``: ends this rank's pending RCCL kernels; every later collective raises."""
+        """``ncclCommAbort``: ends this rank's pending RCCL kernels; every later collective raises.
+        Safe from the watchdog thread while the training thread enqueues: the native communicator
+        flags itself first (new calls raise), then waits for in-flight enqueues before releasing the
+        handle (csrc/rccl_comm.h)."""
         self.aborted = True
         self._comm.abort()
 

@@ -275,7 +275,7 @@ class DistributedDataParallel(nn.Module):
             if not self._ov_pending:
                 return
         dev = self.flat.grad.device
-        lm.wgrad_join(dev)  # side-stream weight gradients (DTA_WGRAD_STREAM) joined into the current stream
+        lm.wgrad_join(dev)  # deferred weight gradients launched on the current stream
         s = self._ov_stream
         s.wait_stream(torch.cuda.current_stream(dev))
         pend, self._ov_pending = self._ov_pending, []
@@ -323,6 +323,11 @@ class DistributedDataParallel(nn.Module):
             self.comm.poll_errors()  # a timed-out peer exchange raises here, not silently later
 
     def forward(self, *args: Any, **kwargs: Any) -> Any:
+        if self._callback_queued:
+            # the previous backward started (a hook fired) but never reached its finalize
+            # callback -- it raised: forget its hook counts and queued buckets, or this step's
+            # backward would never queue a finalize of its own
+            self.reset_iteration()
         if self.broadcast_buffers and self.world_size > 1 and self.require_sync:
             self._broadcast_buffers()
         if self.flat.grad.is_cuda:

@@ -397,11 +397,22 @@ class FullyShardedDataParallel(nn.Module):
         # ---- build the full flat of each unit, sync from rank 0, keep this rank's shard ----
         shard_params = []
         names = []
+        # a model built on the meta device (models/init.py: the LM configs through the entrypoint) is
+        # materialised here, one unit at a time, straight into the unit's fp32 staging buffer on the
+        # device -- the full model never exists on the host, and on the device only one unit at once.
+        # When the unit is broadcast from rank 0 only rank 0 draws the values.
+        from ..models.init import init_param_
+
+        draw = not (sync_module_states and self.world_size > 1) or self.rank == 0
         with torch.no_grad():
             for u in self.units:
                 full = torch.zeros(u.total, dtype=torch.float32, device=self.device)
-                for (_, _, _, p), o, n in zip(u.entries, u.offsets, u.numels):
-                    full[o:o + n].copy_(p.detach().reshape(-1).float())
+                for (_, _, name, p), o, n, shp in zip(u.entries, u.offsets, u.numels, u.shapes):
+                    if p.is_meta:
+                        if draw:
+                            init_param_(module, name, full[o:o + n].view(shp))
+                    else:
+                        full[o:o + n].copy_(p.detach().reshape(-1).float())
                 if sync_module_states and self.world_size > 1:
                     self.comm.broadcast(full, src=0)
                 sp = nn.Parameter(full[self.rank * u.shard_size:(self.rank + 1) * u.shard_size].clone())
@@ -551,7 +562,35 @@ class FullyShardedDataParallel(nn.Module):
             if t.requires_grad:
                 t.register_hook(hook)
 
+    def reset_iteration(self) -> None:
+        """Forget a step that stopped midway -- a backward that raised, or a graph capture that
+        failed mid-backward (engine/step_graph.py): its queued final callback, pending and waiting
+        reduce-scatters, per-unit backward state and gathered copies.  Without this the next
+        backward never queues ``_finalize_backward`` (``_cb_queued`` stuck), so gradients are not
+        bound or zero-filled and ``_pending_rs`` grows without bound."""
+        for u in self.units:
+            u.wait()  # (a prefetch still in flight lands before its storage can be freed)
+            u.in_backward = False
+            u._bwd_ready = False
+            u._dest = None
+            u._claimed = set()
+            u.full.grad = None
+            if u.gathered and not u.alias:
+                u.free()
+        self._cb_queued = False
+        self._pending_rs = []
+        self._rs_waiting = []
+        self._ov_done = set()
+        self._ov_first = True
+        if self._grad_fresh:
+            self._written = set()  # (the abandoned step's in-place writes are overwritten by the next backward)
+
     def forward(self, *args: Any, **kwargs: Any) -> Any:
+        if self._cb_queued or any(u.in_backward for u in self.units):
+            # a backward started (a pre-backward hook ran, or a post-backward queued the final
+            # callback) but never finished -- it raised (this forward is never called from inside a
+            # backward: checkpoint recomputation re-runs the unit modules, not this wrapper)
+            self.reset_iteration()
         if self._defer_wgrad and torch.is_grad_enabled():
             _lm().new_forward_generation()  # (native Linear counts weight uses per forward: single-use -> deferrable)
             if self._rs_waiting and not any(u.in_backward for u in self.units):
@@ -753,8 +792,10 @@ class FullyShardedDataParallel(nn.Module):
                     for _, _, alias in self._aliases.get(name, [(None, None, name)]):
                         out[alias] = t
         if keep:
+            persistent = set(self._sd_keys)  # (non-persistent buffers, e.g. RoPE tables, are not state)
             for name, b in self.module.named_buffers():
-                out[name] = b.detach().cpu().clone() if offload_to_cpu else b.detach().clone()
+                if name in persistent:
+                    out[name] = b.detach().cpu().clone() if offload_to_cpu else b.detach().clone()
             ordered = {k: out[k] for k in self._sd_keys if k in out}
             ordered.update({k: v for k, v in out.items() if k not in ordered})
             return ordered

@@ -2,6 +2,8 @@
 
 Run on an MI355X: ``pytest -m gpu tests/test_kernels_gpu.py``.
 """
+import os
+
 import pytest
 import torch
 
@@ -191,8 +193,6 @@ def test_mlp2_fused_step_sgd_update_pingpong(C):
 
 
 def test_rccl_world1_collectives(C):
-    import os
-
     from distributed_training_amd.ops import ensure_rccl
 
     ensure_rccl()
@@ -216,3 +216,56 @@ def test_rccl_world1_collectives(C):
     torch.testing.assert_close(rs, x)
     torch.testing.assert_close(a2a, x)
     comm.destroy()
+    with pytest.raises(RuntimeError, match="aborted"):  # a destroyed handle is never touched again
+        comm.all_reduce(y, "sum", -1)
+
+
+_ABORT_RACE = r"""
+import sys, threading, time
+import torch
+from distributed_training_amd.parallel.comm import RcclComm
+
+dev = torch.device("cuda", 0)
+comm = RcclComm(0, 1, dev, timeout_s=0.3)   # watchdog armed at one rank (explicit timeout)
+t = torch.ones(1 << 16, device=dev)
+seen, calls = [], [0]
+
+def spam():
+    try:
+        while True:   # the training thread: collectives enqueued back to back
+            comm.all_reduce(t, "sum", async_op=True)
+            calls[0] += 1
+    except RuntimeError as e:
+        seen.append(str(e))
+
+class Never:      # an injected collective that never completes
+    def query(self):
+        return False
+
+th = threading.Thread(target=spam)
+th.start()
+time.sleep(0.05)
+comm.watchdog.track(Never(), "injected never-completing collective")
+th.join(timeout=20)
+assert not th.is_alive(), "enqueue thread never observed the abort"
+assert seen and ("aborted" in seen[0] or "not complete" in seen[0]), seen
+assert comm.aborted and comm._comm.aborted
+torch.cuda.synchronize()
+comm.destroy()
+print("OK", calls[0], seen[0][:80])
+"""
+
+
+def test_rccl_watchdog_abort_races_enqueue(tmp_path):
+    """the watchdog thread aborts the communicator while another thread enqueues
+    all_reduce in a tight loop -- the loop raises RuntimeError within the deadline and the process
+    exits 0 (no use of a freed handle, no segfault).  Run in a child process so a crash is a failed
+    exit status, not a dead test runner."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ABORT_RACE], cwd=root, capture_output=True, text=True, timeout=100,
+                       env=dict(os.environ, DTA_COMM_TIMEOUT_EXIT="1"))
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert "OK" in r.stdout

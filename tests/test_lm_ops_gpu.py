@@ -371,49 +371,6 @@ def test_gemm_tn_fused_bias_gradient(K, M, N, split):
     assert db16.dtype == torch.bfloat16 and _rel(db16, a.float().sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("mode", ["0", "2", "1", "5"])
-def test_ddp_side_stream_weight_gradients(mode, monkeypatch):
-    """Weight gradients on the side stream (DTA_WGRAD_STREAM): same gradients as an unwrapped
-    copy, the side path taken only by single-use weights (a weight used twice stays on the
-    current stream), and the stream joined before the gradients are read."""
-    import copy
-
-    from distributed_training_amd.parallel.comm import RcclComm
-    from distributed_training_amd.parallel.ddp import DistributedDataParallel
-
-    monkeypatch.setenv("DTA_WGRAD_STREAM", mode)
-    monkeypatch.setenv("DTA_WGRAD_GROUP", "0")
-
-    class Net(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.a = lm.Linear(256, 512)
-            self.b = lm.Linear(512, 256)
-            self.shared = lm.Linear(256, 256)
-
-        def forward(self, x):
-            return self.shared(self.shared(self.b(lm.gelu(self.a(x)))))
-
-    torch.manual_seed(4)
-    dev = torch.device(DEV, 0)
-    net = Net().to(dev).bfloat16()
-    ref = copy.deepcopy(net)
-    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
-    x = torch.randn(1024, 256, device=dev).bfloat16()
-    for it in range(3):
-        ddp.zero_grad(set_to_none=True)
-        n0 = lm.GEMM_STATS["side_wgrad"]
-        ddp(x).float().square().mean().backward()
-        side = lm.GEMM_STATS["side_wgrad"] - n0
-        assert side == (0 if mode == "0" else 2), side  # a and b; never `shared`
-        for p in ref.parameters():
-            p.grad = None
-        ref(x).float().square().mean().backward()
-        rp = dict(ref.named_parameters())
-        for name, p in net.named_parameters():
-            assert _rel(p.grad, rp[name].grad) < 2e-2, (mode, it, name)
-
-
 @pytest.mark.parametrize("mode", ["dta", "torch"])
 def test_gelu_linear_fused_backward(mode, monkeypatch):
     """gelu(h) W^T + b with the GELU backward in the input-gradient GEMM's epilogue (DTA_GEMM=dta)
@@ -516,6 +473,53 @@ def test_ddp_deferred_grouped_weight_gradients(threshold, monkeypatch):
         rp = dict(ref.named_parameters())
         for name, p in net.named_parameters():
             assert _rel(p.grad, rp[name].grad) < 2e-2, (threshold, it, name)
+
+
+def test_ddp_deferred_after_raised_backward(monkeypatch):
+    """A backward that RAISES after deferring weight gradients: the next step starts a
+    fresh generation -- the abandoned step's queue is dropped and the end-of-backward flush is queued
+    again, so the next step's gradients match an unwrapped copy (no stale entries, no unwritten
+    slices read by the optimizer)."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("DTA_WGRAD_GROUP", "200")  # one flush at the end of the backward
+
+    class Boom(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            raise RuntimeError("injected backward failure")
+
+    torch.manual_seed(9)
+    dev = torch.device(DEV, 0)
+    net = torch.nn.Sequential(*[lm.Linear(512, 512) for _ in range(3)]).to(dev).bfloat16()
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    x = torch.randn(2, 512, 512, device=dev).bfloat16()
+    ddp.zero_grad(set_to_none=True)
+    n0 = lm.GEMM_STATS["deferred_wgrad"]
+    # the failure sits BELOW the first layer, so layers 2 and 3 have deferred their weight gradients
+    with pytest.raises(RuntimeError, match="injected"):
+        ddp(Boom.apply(x.clone().requires_grad_())).float().square().mean().backward()
+    assert lm.GEMM_STATS["deferred_wgrad"] - n0 >= 1
+    assert lm.wgrad_pending()  # the raised backward never flushed
+    for it in range(2):
+        ddp.zero_grad(set_to_none=True)
+        x = torch.randn(2, 512, 512, device=dev).bfloat16()
+        ddp(x).float().square().mean().backward()
+        assert not lm.wgrad_pending()
+        for p in ref.parameters():
+            p.grad = None
+        ref(x).float().square().mean().backward()
+        rp = dict(ref.named_parameters())
+        for name, p in net.named_parameters():
+            assert _rel(p.grad, rp[name].grad) < 2e-2, (it, name)
 
 
 @pytest.mark.parametrize("k64", [False, True])
@@ -852,6 +856,65 @@ def test_fsdp_optimizer_in_backward_bit_identical(opt_name):
     assert torch.equal(finals[0][0], finals[1][0])
     assert torch.equal(finals[0][1], finals[1][1])
     assert torch.equal(finals[0][2], finals[1][2])
+
+
+def test_fsdp_step_graph_capture_failure_then_eager():
+    """a step-graph capture that fails MID-BACKWARD under the FSDP engine (one rank,
+    graph_capturable) resets the engine (FullyShardedDataParallel.reset_iteration) -- the eager steps
+    that follow bind / write every gradient and train exactly like a run that never tried to capture."""
+    from distributed_training_amd.engine.step_graph import GraphedStep
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = torch.device(DEV, 0)
+    g = torch.Generator(device="cpu").manual_seed(8)
+    data = [torch.randint(0, 1024, (2, 129), generator=g).to(dev) for _ in range(3)]
+    failing = [False]
+
+    class Boom(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.view_as(x)
+
+        @staticmethod
+        def backward(ctx, gr):
+            if failing[0]:
+                raise RuntimeError("op not capturable")
+            return gr
+
+    finals = []
+    for try_graph in (False, True):
+        torch.manual_seed(0)
+        model = GPT2(GPT2Config(n_layer=3, n_head=4, n_embd=256, vocab_size=1024, block_size=128)).to(dev)
+        model.h[1].register_forward_hook(lambda m, a, out: (Boom.apply(out[0]), out[1]))
+        fs = FullyShardedDataParallel(model, comm=RcclComm(0, 1, dev), device=dev, wrap_policy=lm_wrap_policy(model),
+                                      param_dtype=torch.bfloat16)
+        opt = FusedAdamW(fs.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+
+        def step(xb):
+            failing[0] = torch.cuda.is_current_stream_capturing()
+            opt.zero_grad(set_to_none=True)
+            loss = fs(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        if try_graph:
+            assert fs.graph_capturable()
+            gs = GraphedStep(step, [data[0].clone()], warmup=1, engine=fs)  # one real step, then the capture
+            assert not gs.ok and "not capturable" in str(gs.error)
+            failing[0] = False
+            assert not fs._cb_queued and not fs._pending_rs and not any(u.in_backward for u in fs.units)
+            rest = data[1:]
+        else:
+            rest = data
+        for x in rest:
+            step(x)
+        torch.cuda.synchronize()
+        finals.append(fs.shards.master.clone())
+    assert torch.equal(finals[0], finals[1])
 
 
 @pytest.mark.parametrize("ckpt", [False, True])
