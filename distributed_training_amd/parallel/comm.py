@@ -153,7 +153,8 @@ class TorchComm(Communicator):
         if self.world_size == 1:
             return CommWork() if async_op else None
         if self.group is not None:  # ``src`` is a rank of this communicator's group, as for every backend here
-            work = dist.broadcast(t, group_src=src, group=self.group, async_op=async_op)
+            # (mapped to its global rank: ``group_src=`` exists only from torch 2.6)
+            work = dist.broadcast(t, src=dist.get_global_rank(self.group, src), group=self.group, async_op=async_op)
         else:
             work = dist.broadcast(t, src=src, async_op=async_op)
         return self._w(work, async_op)

@@ -291,7 +291,8 @@ class _Unit:
     def _launch_rs(self, g: torch.Tensor) -> None:
         own = self.owner
         if own.world_size == 1:  # the whole gradient is this rank's shard: no collective, no copy
-            own._pending_rs.append((self, CommWork(), g, g))
+            work = CommWork() if own.rep is None else own._replicate(self, g, CommWork())
+            own._pending_rs.append((self, work, g, g))
         else:
             # after zero_grad(set_to_none) the flat gradient holds nothing worth
             # keeping: reduce-scatter straight into this unit's slice of it
@@ -309,6 +310,8 @@ class _Unit:
                 g.div_(own.world_size)
             with prof.range_(f"fsdp.unit{self.index}.reduce_scatter"):
                 work = own.comm.reduce_scatter_into(out, g, op=op, async_op=True)
+            if own.rep is not None:
+                work = own._replicate(self, out, work)
             own._pending_rs.append((self, work, out, g))
         if own._ov is not None:
             own._ov_unit(self)
@@ -492,6 +495,7 @@ class FullyShardedDataParallel(nn.Module):
                     me._launch_waiting()
 
             _lm().FLUSH_LISTENERS.append(on_flush)
+        self._rep_stream: Optional[torch.cuda.Stream] = None  # HSDP replica all-reduces (_replicate)
         self._ov: Any = None  # optimizer stepped unit by unit inside the backward (overlap_optimizer)
         self._ov_done: Set[int] = set()
         self._ov_first = True
@@ -668,6 +672,23 @@ class FullyShardedDataParallel(nn.Module):
             return
         self._ov_step(u, work if self.world_size > 1 else None)
 
+    def _replicate(self, u: "_Unit", out: torch.Tensor, rs_work: CommWork) -> CommWork:
+        """HSDP: average unit ``u``'s freshly reduce-scattered gradient shard over the replica group
+        (the same shard on every node) right behind its reduce-scatter -- per unit, overlapped with the
+        rest of the backward, instead of one blocking all-reduce of the whole flat shard gradient after
+        it (2 GB per rank at 8B / 8).  Ordered on a side stream that waits for the reduce-scatter's
+        event, so neither the compute stream nor the shard group's stream waits for the replicas."""
+        if not out.is_cuda:
+            rs_work.wait()  # (gloo: host-ordered)
+            with prof.range_(f"fsdp.unit{u.index}.replica_all_reduce"):
+                return self.rep.all_reduce(out, op="avg", async_op=True)
+        s = self._rep_stream
+        if s is None:
+            s = self._rep_stream = torch.cuda.Stream(self.device)
+        rs_work.wait(s)
+        with torch.cuda.stream(s), prof.range_(f"fsdp.unit{u.index}.replica_all_reduce"):
+            return self.rep.all_reduce(out, op="avg", async_op=True)
+
     def _launch_waiting(self) -> None:
         """Reduce-scatter the units whose gradients waited for a grouped weight-gradient launch."""
         waiting, self._rs_waiting = self._rs_waiting, []
@@ -718,15 +739,8 @@ class FullyShardedDataParallel(nn.Module):
             self._written = set()
         self._pending_rs = []
         self._cb_queued = False
-        if self.rep is not None:
-            # HSDP: the shard-group reduce-scatters are done (waited above); average the gradient shards
-            # over the replicas -- ONE all-reduce of the whole flat shard gradient (the mean over every
-            # rank's micro-batch, as the shard group's average was over its own ranks)
-            with prof.range_("fsdp.replica_all_reduce"):
-                g = fg.grad if fg.grad.device.type == self.device.type else fg.grad.to(self.device)
-                self.rep.all_reduce(g, op="avg")
-                if g is not fg.grad:
-                    fg.grad.copy_(g.cpu())
+        # (HSDP: every unit's shard was averaged over the replicas right after its reduce-scatter,
+        # _replicate; the works waited above were those replica all-reduces)
         if self._ov is not None:
             for u in self.units:  # units whose gradient was not final in place: stepped now
                 if u.index not in self._ov_done:

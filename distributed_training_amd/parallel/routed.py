@@ -13,8 +13,15 @@ when the communicator is built:
   over the ranks (so every rank takes the SAME decision: collectives are issued in the
   same order on every rank of each data plane), and the faster one (IPC only when it
   wins by ``margin``) serves every message of that class;
-* each message then goes to the route of the smallest class at least its size (the
-  largest class beyond).  Broadcast, all-to-all and barrier stay on the primary.
+* each message then goes to the route of the smallest class at least its size.  A message
+  LARGER than every class (FSDP units: 436 MB per Llama-3 8B layer, 1.05 GB for the embedding
+  / head) adds a class of its own on first use -- the next power of two -- calibrated on the
+  spot for every op and dtype (all ranks meet the same first such message: the engines issue
+  identical collective sequences), so the routes of the real message sizes are measured, not
+  extrapolated; inside a graph capture the largest class is used instead.  Broadcast,
+  all-to-all and barrier stay on the primary.
+* calibration failures are agreed on key by key (a MIN of the success flag over the ranks
+  after each timed key), so every rank stops timing the fast plane at the same key.
 
 The routes of the table are logged and exposed (:meth:`routes`: bench_lm.py emits
 them in its JSON).  Anything the router does not route -- the fused programs'
@@ -46,18 +53,23 @@ class RoutedComm(Communicator):
 
     def __init__(self, primary: Communicator, fast: Communicator, sizes: Tuple[int, ...] = SIZES,
                  margin: float = 0.9, calibrate: bool = True, iters: int = 5,
-                 table: Optional[Dict[Tuple[str, torch.dtype], List[str]]] = None) -> None:
+                 table: Optional[Dict[Tuple[str, torch.dtype], List[str]]] = None,
+                 lazy_max: int = 4 << 30) -> None:
         """``primary``: the default data plane (RCCL); ``fast``: the IPC push collectives.
-        ``table`` (tests): a fixed route table instead of the calibration."""
+        ``table`` (tests): a fixed route table instead of the calibration.  ``lazy_max``: the largest
+        class a message may add on first use (0: no lazy classes)."""
         self.primary, self.fast = primary, fast
         self.rank, self.world_size, self.device = primary.rank, primary.world_size, primary.device
-        self.sizes = tuple(sizes)
+        self.sizes = list(sizes)
         self.margin = float(margin)
+        self.iters = int(iters)
         self.timings: Dict[str, float] = {}
+        self.failed = False
+        self.lazy_max = int(lazy_max) if calibrate and table is None else 0
         if table is not None:
-            self.table = dict(table)
+            self.table = {k: list(v) for k, v in table.items()}
         elif calibrate:
-            self.table = self._calibrate(iters)
+            self.table = self._calibrate(self.sizes, iters)
         else:
             self.table = {(op, dt): ["primary"] * len(self.sizes) for op in OPS for dt in DTYPES}
         self.counts = {"primary": 0, "fast": 0}
@@ -67,10 +79,24 @@ class RoutedComm(Communicator):
         routes = self.table.get((op, dtype))
         if routes is None:
             return self.primary
+        if nbytes > self.sizes[-1] and self.lazy_max and nbytes <= self.lazy_max \
+                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self._add_class(1 << (int(nbytes) - 1).bit_length())
+            routes = self.table[(op, dtype)]
         k = next((i for i, s in enumerate(self.sizes) if nbytes <= s), len(self.sizes) - 1)
         r = routes[k]
         self.counts[r] += 1
         return self.fast if r == "fast" else self.primary
+
+    def _add_class(self, size: int) -> None:
+        """A new size class (every op and dtype calibrated at ``size``), kept in ascending order."""
+        new = self._calibrate([size], self.iters)
+        k = next((i for i, s in enumerate(self.sizes) if size < s), len(self.sizes))
+        self.sizes.insert(k, size)
+        for key, rs in self.table.items():
+            rs.insert(k, new.get(key, ["primary"])[0])
+        logger.info("routed comm: size class %d MiB added on first use (rank %d): %s", size // MiB, self.rank,
+                    {f"{op} {str(dt).replace('torch.', '')}": r[0] for (op, dt), r in new.items()})
 
     def routes(self) -> Dict[str, str]:
         """``"all_reduce bf16 <=4MiB" -> "ipc" | "rccl"`` for the log / bench JSON."""
@@ -112,37 +138,49 @@ class RoutedComm(Communicator):
         sync()
         return (time.perf_counter() - t0) / iters
 
-    def _calibrate(self, iters: int) -> Dict[Tuple[str, torch.dtype], List[str]]:
-        keys = [(op, dt, s) for op in OPS for dt in DTYPES for s in self.sizes]
-        t = torch.zeros(2 * len(keys), dtype=torch.float64)
-        ok = 1.0
-        try:
-            for i, (op, dt, s) in enumerate(keys):
-                t[2 * i] = self._time(self.primary, op, dt, s, iters)
-                t[2 * i + 1] = self._time(self.fast, op, dt, s, iters)
-        except Exception as e:  # noqa: BLE001 - a failing route: every rank falls back to the primary
-            logger.warning("routed comm calibration failed on rank %d (%s); primary data plane only", self.rank, e)
-            ok = 0.0
-        tt = torch.cat([t, torch.tensor([-ok], dtype=torch.float64)]).to(
-            self.device if self.device.type == "cuda" else "cpu")
-        self.primary.all_reduce(tt, "max")  # every rank: the slowest rank's time, and whether any failed
-        tt = tt.cpu()
+    def _calibrate(self, sizes: List[int], iters: int) -> Dict[Tuple[str, torch.dtype], List[str]]:
+        """Time every (op, dtype, size) on both planes; per key the ranks agree (MAX of the times, MIN
+        of the success flag) before the next key is timed, so a failure on one rank stops the timing
+        of the fast plane on every rank at that key (no rank left waiting inside an IPC collective)."""
+        keys = [(op, dt, s) for op in OPS for dt in DTYPES for s in sizes]
         table: Dict[Tuple[str, torch.dtype], List[str]] = {}
-        failed = float(tt[-1]) > -1.0
-        for i, (op, dt, s) in enumerate(keys):
-            tp, tf = float(tt[2 * i]), float(tt[2 * i + 1])
-            self.timings[f"{op} {str(dt).replace('torch.', '')} {s // MiB}MiB"] = (round(tp * 1e6, 1),
-                                                                                  round(tf * 1e6, 1))
-            r = "fast" if (not failed and tf < self.margin * tp) else "primary"
+        dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        for op, dt, s in keys:
+            tp = tf = float("inf")
+            ok = 0.0 if self.failed else 1.0
+            if ok:
+                try:
+                    tp = self._time(self.primary, op, dt, s, iters)
+                    tf = self._time(self.fast, op, dt, s, iters)
+                except Exception as e:  # noqa: BLE001 - a failing route: every rank falls back to the primary
+                    logger.warning("routed comm calibration failed on rank %d at %s %s %d MiB (%s); primary "
+                                   "data plane only", self.rank, op, dt, s // MiB, e)
+                    ok = 0.0
+                    tp = tf = 0.0
+            tt = torch.tensor([tp if ok else 0.0, tf if ok else 0.0, -ok], dtype=torch.float64, device=dev)
+            self.primary.all_reduce(tt, "max")  # the slowest rank's times, and whether any rank failed
+            tt = tt.cpu()
+            if float(tt[2]) > -1.0:
+                self.failed = True
+            tpa, tfa = float(tt[0]), float(tt[1])
+            self.timings[f"{op} {str(dt).replace('torch.', '')} {s // MiB}MiB"] = (round(tpa * 1e6, 1),
+                                                                                    round(tfa * 1e6, 1))
+            r = "fast" if (not self.failed and tfa < self.margin * tpa) else "primary"
             table.setdefault((op, dt), []).append(r)
-        logger.info("routed comm table (rank %d): %s", self.rank, self.routes_from(table))
+        if self.failed:  # (a failure at a later key also retracts the fast routes of earlier keys)
+            table = {k: ["primary"] * len(v) for k, v in table.items()}
+        logger.info("routed comm table (rank %d): %s", self.rank, self.routes_from(table, sizes))
         return table
 
-    def routes_from(self, table: Any) -> str:
+    def routes_from(self, table: Any, sizes: Optional[List[int]] = None) -> str:
         saved, self.table = getattr(self, "table", None), table
+        saved_sizes = self.sizes
+        if sizes is not None:
+            self.sizes = list(sizes)
         try:
             return ", ".join(f"{k}: {v}" for k, v in self.routes().items())
         finally:
+            self.sizes = saved_sizes
             if saved is not None:
                 self.table = saved
 

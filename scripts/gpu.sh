@@ -11,6 +11,7 @@
 #   bash scripts/gpu.sh pmc <tag> <ctrs> <python args>  one PMC pass (comma-separated counters)
 #   bash scripts/gpu.sh shared <n> <tag> <script args>  n ranks sharing this GPU (DTA_SHARED_GPU=1, IPC comm)
 #   bash scripts/gpu.sh gemm [models] [rounds]      scripts/bench_gemm64.py -> gpurun_out/gemm64_bench.jsonl
+#   bash scripts/gpu.sh w4 [models] [rounds] [tiles]  scripts/bench_w4.py (forward GEMMs) -> gpurun_out/w4_bench.jsonl
 #
 # Every GPU step runs under its own timeout; a failing step ends the script (set -e).
 set -euo pipefail
@@ -65,6 +66,10 @@ case "$task" in
     timeout -k 10 600 python scripts/bench_gemm64.py ${1:-gpt2,llama} ${2:-5} > gpurun_out/gemm64_bench.jsonl \
       2> gpurun_out/gemm64_bench.err || { tail -20 gpurun_out/gemm64_bench.err; exit 1; }
     python scripts/gemm64_table.py gpurun_out/gemm64_bench.jsonl ;;
+  w4)
+    timeout -k 10 600 python scripts/bench_w4.py ${1:-llama,gpt2} ${2:-5} ${3:-5,6,7,8,3} > gpurun_out/w4_bench.jsonl \
+      2> gpurun_out/w4_bench.err || { tail -20 gpurun_out/w4_bench.err; exit 1; }
+    cut -c1-240 gpurun_out/w4_bench.jsonl ;;
   *)
     echo "unknown task $task" >&2; exit 2 ;;
 esac

@@ -153,3 +153,46 @@ def test_gemm64_busy_chip(a_t, b_t, tile):
         got, = native().gemm64(a, b, a_t, b_t, tile=tile)
         err = (got.float() - want).abs().max().item() / scale
         assert err < 8e-3, (tile, a_t, b_t, err)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (300, 520, 384), (1000, 200, 1280),
+                                   (8192, 50304 // 16, 768), (64, 1000, 128)])
+def test_gemm_w4_exact_and_edges(M, N, K):
+    """Tile 9 (csrc/gemm_w4.hip: 4 waves, 256 x 256, intra-wave interleave; NT only): exact on small
+    integers at full tiles and at EDGE tiles in both dimensions (rows past M / N clamped in the DMA,
+    stores predicated), K from the shortest pipeline (two K-tiles) up."""
+    from distributed_training_amd.ops import native
+
+    gen = torch.Generator().manual_seed(M * 7 + N + K)
+    a = torch.randint(-3, 4, (M, K), generator=gen).float()
+    b = torch.randint(-3, 4, (N, K), generator=gen).float()
+    want = a @ b.t()
+    out = torch.full((M, N), float("nan"), device="cuda")
+    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), False, False, out, out_f32=True, tile=9)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), want), (M, N, K)
+
+
+@pytest.mark.parametrize("epi", [0, 2, 32])
+def test_gemm_w4_epilogues(epi):
+    """Tile 9 with bias / alpha and the fused epilogues (GELU dual store, + residual) vs fp32 torch."""
+    from distributed_training_amd.ops import native
+
+    gen = torch.Generator().manual_seed(90 + epi)
+    M, N, K = 520, 776, 512
+    a = torch.randn(M, K, generator=gen).bfloat16().cuda()
+    b = (torch.randn(N, K, generator=gen) * 0.05).bfloat16().cuda()
+    bias = torch.randn(N, generator=gen).bfloat16().cuda()
+    ref = a.float() @ b.float().t() + bias.float()
+    if epi == 2:
+        h, g = native().gemm64(a, b, False, False, torch.empty(M, N, device="cuda", dtype=torch.bfloat16),
+                               torch.empty(M, N, device="cuda", dtype=torch.bfloat16), False, 1.0, bias, 2, None, 9)
+        _close(h, ref, K)
+        _close(g, F.gelu(h.float(), approximate="tanh"), K)
+    elif epi == 32:
+        res = torch.randn(M, N, generator=gen).bfloat16().cuda()
+        y, = native().gemm64(a, b, False, False, None, None, False, 1.0, bias, 32, res, 9)
+        _close(y, ref + res.float(), K)
+    else:
+        y, = native().gemm64(a, b, False, False, None, None, False, 0.5, bias, 0, None, 9)
+        _close(y, 0.5 * (a.float() @ b.float().t()) + bias.float(), K)

@@ -495,6 +495,23 @@ def _routed_worker(rank, ws):
                 assert torch.equal(out.cpu(), torch.arange(1, ws + 1).repeat_interleave(m).to(dt))
                 assert torch.equal(o.cpu(), torch.full((m,), float(ws)).to(dt))
         assert rc.counts[route] == before + 12
+    # a message past every class (> 64 MiB, the size of an FSDP unit) adds a class calibrated on the
+    # spot on both planes; then each route is forced and checked exactly at that size
+    big = 36 << 20  # 36 Mi bf16 elements = 72 MiB
+    y = torch.full((big,), 1.0, dtype=torch.bfloat16, device=dev)
+    rc.all_reduce(y, "sum")
+    assert rc.sizes[-1] == 128 * MiB, rc.sizes
+    for route in ("primary", "fast"):
+        rc.table = {k: [route] * len(rc.sizes) for k in rc.table}
+        y.fill_(float(rank + 1))
+        rc.all_reduce(y, "sum")
+        o = torch.empty(big // ws, dtype=torch.bfloat16, device=dev)
+        rc.reduce_scatter_into(o, torch.ones(big, dtype=torch.bfloat16, device=dev), "sum")
+        torch.cuda.synchronize()
+        assert torch.equal(y[:: 1 << 16].cpu(), torch.full((big >> 16,), float(sum(range(1, ws + 1))),
+                                                          dtype=torch.bfloat16)), route
+        assert bool((o == float(ws)).all()), route
+    del y, o
     rc.poll_errors()
     rc.destroy()
 
@@ -645,6 +662,6 @@ def _hsdp_worker(rank, ws, shard_size):
     rep.destroy()
 
 
-@pytest.mark.parametrize("ws,shard_size", [(4, 2)])
+@pytest.mark.parametrize("ws,shard_size", [(4, 2), (8, 4)])
 def test_hybrid_shard_shared_gpu(ws, shard_size):
     run_gloo(_hsdp_worker, ws, shard_size)

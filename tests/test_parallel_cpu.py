@@ -459,7 +459,7 @@ def _routed_cpu(rank, ws):
     from distributed_training_amd.parallel.comm import TorchComm
     from distributed_training_amd.parallel.routed import MiB, RoutedComm
 
-    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB // 16, MiB // 4), iters=2)
+    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB // 16, MiB // 4), iters=2, lazy_max=0)
     sig = hashlib.sha256(repr(sorted(rc.routes().items())).encode()).digest()
     sigs = [None] * ws
     dist.all_gather_object(sigs, sig)
@@ -488,6 +488,42 @@ def _routed_cpu(rank, ws):
 
 def test_routed_comm_cpu():
     run_gloo(_routed_cpu, 2)
+
+
+def _routed_lazy_cpu(rank, ws):
+    """A message larger than every size class adds a class of its own on first use (calibrated for every
+    op / dtype on all ranks at the same point), kept sorted; the same table on every rank; a calibration
+    failure on ONE rank (at one key) sends every rank to the primary plane without a hang."""
+    import hashlib
+
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.routed import MiB, RoutedComm
+
+    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB // 16,), iters=1)
+    x = torch.ones(100_000) * (rank + 1)  # 400 KB > 64 KB: a 512 KB class
+    rc.all_reduce(x, "sum")
+    assert torch.equal(x, torch.full((100_000,), float(sum(range(1, ws + 1)))))
+    assert rc.sizes == [MiB // 16, MiB // 2] and all(len(v) == 2 for v in rc.table.values())
+    sig = hashlib.sha256(repr(sorted(rc.routes().items())).encode()).digest()
+    sigs = [None] * ws
+    dist.all_gather_object(sigs, sig)
+    assert all(s == sig for s in sigs)
+    out = torch.empty(ws * 30_000)  # 120 KB * ws: inside the new class, no further calibration
+    rc.all_gather_into(out, torch.full((30_000,), float(rank)))
+    assert rc.sizes == [MiB // 16, MiB // 2]
+
+    class Broken(TorchComm):
+        # rank 1's data plane fails; rank 0's bounded peer wait (IpcComm: timeout_iters) then fails the
+        # same collective -- emulated by raising on both ranks at that call
+        def all_gather_into(self, out, inp, async_op=False):
+            raise RuntimeError("injected data-plane failure" if rank == 1 else "peer wait timed out")
+
+    rb = RoutedComm(TorchComm(), Broken(), sizes=(MiB // 16,), iters=1)
+    assert rb.failed and all(r == "primary" for v in rb.table.values() for r in v)
+
+
+def test_routed_comm_lazy_classes_cpu():
+    run_gloo(_routed_lazy_cpu, 2)
 
 
 
