@@ -37,6 +37,22 @@ constexpr int LDS_BYTES = 4 * IMG;               // [A p0 | A p1 | B p0 | B p1]
 constexpr int NP = IMG / 1024 / 4;               // 1 KiB DMA pieces per wave per operand per K-tile: 8
 }  // namespace w4
 
+// M/N-major image (transposed operand [K][M]): two 128-column halves of 64 k-rows x 256 B, chunk ch of
+// k-row k stored at ch ^ mswz(k) (the conflict-free ds_read_b64_tr_b16 swizzle of gemm_k64.hip)
+__device__ __forceinline__ int w4_mswz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+
+__device__ __forceinline__ bf16x4 w4_tr4(const char* lds, int byte_off) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lds + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+// AT: A stored M-major [K][M] (weight gradients dy^T x); BT: B stored N-major [K][N] (input gradients dy W,
+// weight gradients); otherwise K-major.  C = alpha A B^T in every case.
+// KT: K is not a multiple of 128 (two K-tiles): the loop runs over ceil(K / 128) pairs and every DMA
+// lane whose 8 k-values lie at or past K gets an out-of-range buffer offset -- the buffer unit returns
+// zeros for it, so the tail contributes nothing (K a multiple of 8: chunks are whole).
+template <bool AT, bool BT, bool KT>
 __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -48,37 +64,79 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   const int grp = t / per_group, in_g = t - grp * per_group;
   const int gm0 = grp * kGroupM, gh = min(kGroupM, tiles_m - gm0);
   const int m0 = (gm0 + in_g % gh) * 256, n0 = (in_g / gh) * 256;
-  const int nk = g.K / BK;
+  const int nk = KT ? 2 * ((g.K + 2 * BK - 1) / (2 * BK)) : g.K / BK;
 
-  // ---- DMA: piece q (0..7) of this wave holds rows 32 q + 8 wave + (lane >> 3) of the tile, the lane's
-  // 16-byte chunk XOR-swizzled by the row (row & 7 == lane >> 3); rows past M / N clamped ----
+  // ---- DMA sources (byte offsets of this wave's 8 pieces of K-tile 0; a K-tile adds kstep) ----
+  // K-major: piece q holds rows 32 q + 8 wave + (lane >> 3), the lane's 16-byte chunk XOR-swizzled by
+  //   the row (row & 7 == lane >> 3); rows past M / N clamped to the last one.
+  // M/N-major: piece gp = 4 q + wave holds k-rows 4 (gp & 15) + (lane >> 4) of half gp >> 4, chunk
+  //   (lane & 15) ^ mswz(k); chunks past M / N clamped to the last full one.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.a), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.b), 0, 0x7fffffff, 0x00020000);
   unsigned voA[w4::NP], voB[w4::NP];
-  {
-    const int rl = 8 * wave + (lane >> 3), ch = (lane & 7) ^ (lane >> 3);
-#pragma unroll
-    for (int q = 0; q < w4::NP; ++q) {
-      const int ra = min(m0 + 32 * q + rl, g.M - 1), rb = min(n0 + 32 * q + rl, g.N - 1);
-      voA[q] = (unsigned)(((int64_t)ra * g.lda + 8 * ch) * 2);
-      voB[q] = (unsigned)(((int64_t)rb * g.ldb + 8 * ch) * 2);
+  auto src_off = [&](bool tr, int x0, int X, int64_t ld, int q) -> unsigned {
+    if (!tr) {
+      const int r = min(x0 + 32 * q + 8 * wave + (lane >> 3), X - 1);
+      return (unsigned)(((int64_t)r * ld + 8 * ((lane & 7) ^ (lane >> 3))) * 2);
     }
+    const int gp = 4 * q + wave, k = 4 * (gp & 15) + (lane >> 4);
+    const int col = min(x0 + 128 * (gp >> 4) + 8 * ((lane & 15) ^ w4_mswz(k)), X - 8);
+    return (unsigned)(((int64_t)k * ld + col) * 2);
+  };
+#pragma unroll
+  for (int q = 0; q < w4::NP; ++q) {
+    voA[q] = src_off(AT, m0, g.M, g.lda, q);
+    voB[q] = src_off(BT, n0, g.N, g.ldb, q);
   }
+  // the k (within a K-tile) of this lane's 8 values in piece q: K-major chunk 8 c, M/N-major k-row
+  auto lane_k = [&](bool tr, int q) {
+    return tr ? 4 * ((4 * q + wave) & 15) + (lane >> 4) : 8 * ((lane & 7) ^ (lane >> 3));
+  };
+  auto kt_off = [&](unsigned vo, bool tr, int q, int kt) -> unsigned {  // the K-tail's zero fill
+    if constexpr (!KT) return vo;
+    return kt * BK + lane_k(tr, q) < g.K ? vo : 0x80000000u;
+  };
+  const unsigned kstepA = AT ? (unsigned)(BK * g.lda * 2) : (unsigned)(BK * 2);
+  const unsigned kstepB = BT ? (unsigned)(BK * g.ldb * 2) : (unsigned)(BK * 2);
   const unsigned lds0 = lds_addr(lds);
   auto dma = [&](int kt, int par) {  // all 16 pieces of K-tile kt into image par (prologue form)
-    const unsigned so = (unsigned)kt * (BK * 2);
 #pragma unroll
     for (int q = 0; q < w4::NP; ++q) {
-      bglds16(rsA, voA[q], so, lds0 + par * w4::IMG + (4 * q + wave) * 1024);
-      bglds16(rsB, voB[q], so, lds0 + (2 + par) * w4::IMG + (4 * q + wave) * 1024);
+      bglds16(rsA, kt_off(voA[q], AT, q, kt), (unsigned)kt * kstepA, lds0 + par * w4::IMG + (4 * q + wave) * 1024);
+      bglds16(rsB, kt_off(voB[q], BT, q, kt), (unsigned)kt * kstepB,
+              lds0 + (2 + par) * w4::IMG + (4 * q + wave) * 1024);
     }
   };
 
-  // ---- fragment reads: (row 16 j + (lane & 15) of the wave's 128-row half, k 32 kk + 8 (lane >> 4)) ----
+  // ---- fragment reads: (index 16 j + (lane & 15) of the wave's 128-wide half, k 32 kk + 8 (lane >> 4)) ----
+  // K-major: one ds_read_b128 at a per-lane base (per kk) + 2048 j.  M/N-major: two ds_read_b64_tr_b16
+  // (k-rows 32 kk + 8 g + q and + 4, g = lane >> 4, q = (lane >> 2) & 3) at per-lane, per-j offsets: the
+  // chunk 2 j + (p >> 1) (p = lane & 3) XOR the row swizzle is (j ^ c) * 32 + ..., c = 2 q + (g & 1).
   const int rrow = lane & 15, x = (lane >> 4) ^ (lane & 7);
-  const int aoff[2] = {(wr * 128 + rrow) * 128 + 16 * x, (wr * 128 + rrow) * 128 + 16 * (x ^ 4)};
-  const int boff[2] = {2 * w4::IMG + (wc * 128 + rrow) * 128 + 16 * x, 2 * w4::IMG + (wc * 128 + rrow) * 128 + 16 * (x ^ 4)};
-  auto rd = [&](int off) { return *reinterpret_cast<const bf16x8*>(lds + off); };
+  int kofA[2], kofB[2];                 // K-major per-kk lane bases
+  int tlo[8], thi[8];                   // M/N-major per-j lane offsets inside a half image (lo / hi rows)
+  {
+    const int gg = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3, c = 2 * qq + (gg & 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      tlo[j] = (8 * gg + qq) * 256 + 32 * (j ^ c) + 16 * (pp >> 1) + 8 * (pp & 1);
+      thi[j] = (8 * gg + qq + 4) * 256 + 32 * (j ^ c) + 16 * ((pp >> 1) ^ 1) + 8 * (pp & 1);
+    }
+  }
+  kofA[0] = (wr * 128 + rrow) * 128 + 16 * x;
+  kofA[1] = (wr * 128 + rrow) * 128 + 16 * (x ^ 4);
+  kofB[0] = (wc * 128 + rrow) * 128 + 16 * x;
+  kofB[1] = (wc * 128 + rrow) * 128 + 16 * (x ^ 4);
+  const char* imgA = lds + (AT ? wr * (w4::IMG / 2) : 0);
+  const char* imgB = lds + 2 * w4::IMG + (BT ? wc * (w4::IMG / 2) : 0);
+  auto frag = [&](bool tr, const char* img, const int (&kof)[2], int par, int kk, int j) -> bf16x8 {
+    if (!tr) return *reinterpret_cast<const bf16x8*>(img + par * w4::IMG + kof[kk] + j * 2048);
+    const char* b = img + par * w4::IMG + kk * 8192;
+    const bf16x4 lo = w4_tr4(b, tlo[j]), hi = w4_tr4(b, thi[j]);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto rdA = [&](int par, int kk, int j) { return frag(AT, imgA, kofA, par, kk, j); };
+  auto rdB = [&](int par, int kk, int j) { return frag(BT, imgB, kofB, par, kk, j); };
   // The MFMA as inline asm with the accumulator pinned to AGPRs ("+a") and the fragments to VGPRs:
   // with the builtin the register allocator re-permuted the 256 accumulators and parked fragments in
   // AGPRs every iteration (~530 v_accvgpr moves per 256 MFMAs).  Hazards: a dependent MFMA chain on one
@@ -104,8 +162,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
     // half 0: 64 MFMAs on a0 / b0; between them the 16 reads of half 1 of this K-tile
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s < 8) b1[s] = rd(boff[1] + p * w4::IMG + s * 2048);
-      else a1[s - 8] = rd(aoff[1] + p * w4::IMG + (s - 8) * 2048);
+      if (s < 8) b1[s] = rdB(p, 1, s);
+      else a1[s - 8] = rdA(p, 1, s - 8);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = 4 * s + q, j = idx >> 3, i = idx & 7;
@@ -117,11 +175,12 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
     bar();    // B1: every wave's are -- image p may be refilled
     // half 1: 64 MFMAs on a1 / b1; the DMA of K-tile kt + 2 between the first 32, the reads of K-tile kt + 1's
     // half 0 between the last 32
-    const unsigned so = (unsigned)min(kt + 2, nk - 1) * (BK * 2);
+    const int kn = min(kt + 2, nk - 1);
+    const unsigned soA = (unsigned)kn * kstepA, soB = (unsigned)kn * kstepB;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s < 8) bglds16(rsA, voA[s], so, lds0 + p * w4::IMG + (4 * s + wave) * 1024);
-      else bglds16(rsB, voB[s - 8], so, lds0 + (2 + p) * w4::IMG + (4 * (s - 8) + wave) * 1024);
+      if (s < 8) bglds16(rsA, kt_off(voA[s], AT, s, kn), soA, lds0 + p * w4::IMG + (4 * s + wave) * 1024);
+      else bglds16(rsB, kt_off(voB[s - 8], BT, s - 8, kn), soB, lds0 + (2 + p) * w4::IMG + (4 * (s - 8) + wave) * 1024);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int idx = 2 * s + q, j = idx >> 3, i = idx & 7;
@@ -133,8 +192,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
     bar();                  // B2: every wave's pieces of K-tile kt + 1 landed
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s < 8) b0[s] = rd(boff[0] + (p ^ 1) * w4::IMG + s * 2048);
-      else a0[s - 8] = rd(aoff[0] + (p ^ 1) * w4::IMG + (s - 8) * 2048);
+      if (s < 8) b0[s] = rdB(p ^ 1, 0, s);
+      else a0[s - 8] = rdA(p ^ 1, 0, s - 8);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int idx = 32 + 2 * s + q, j = idx >> 3, i = idx & 7;
@@ -151,8 +210,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   bar();
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    b0[s] = rd(boff[0] + s * 2048);
-    a0[s] = rd(aoff[0] + s * 2048);
+    b0[s] = rdB(0, 0, s);
+    a0[s] = rdA(0, 0, s);
   }
   // nk even (K % 128 == 0, checked on the host): pairs of K-tiles, parities compile-time constants, one
   // loop body and no tail -- branchy tails made the register allocator shuffle all 256 accumulators
@@ -180,14 +239,26 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   }
 }
 
+template <bool AT, bool BT, bool KT>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(Args g) {
-  w4_body(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  w4_body<AT, BT, KT>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
 }  // namespace k64
 }  // namespace dta
 
-hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, hipStream_t st) {
-  hipLaunchKernelGGL(dta::k64::gemm_w4_kernel, dim3(g.tiles_m * g.tiles_n), dim3(256), 0, st, g);
+template <bool KT>
+static void w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t st) {
+  using namespace dta::k64;
+  const dim3 grid(g.tiles_m * g.tiles_n), block(256);
+  if (!a_t && !b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, false, KT>), grid, block, 0, st, g);
+  else if (!a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, true, KT>), grid, block, 0, st, g);
+  else if (a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<true, true, KT>), grid, block, 0, st, g);
+  else hipLaunchKernelGGL((gemm_w4_kernel<true, false, KT>), grid, block, 0, st, g);
+}
+
+hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t st) {
+  if (g.K % (2 * dta::k64::BK)) w4_launch<true>(g, a_t, b_t, st);
+  else w4_launch<false>(g, a_t, b_t, st);
   return hipGetLastError();
 }

@@ -297,7 +297,7 @@ K64 = 10
 # csrc/gemm_k64.hip tiles the dispatcher times: 5 / 6 / 8 = the 8-wave 256x256 / 256x128 / 128x256
 # tiles with the two-phase K loop (3-11 % faster than their four-phase forms 1 / 2 / 4 at every
 # GPT-2 and Llama shape: profiles/gemm_k64_vs_hipblaslt.txt), 3 / 7 = 128x128 in both forms
-K64_TILES = (5, 6, 3, 7, 8)
+K64_TILES = (9, 5, 6, 3, 7, 8)  # 9: csrc/gemm_w4.hip (4 waves, 256 x 256, intra-wave read / MFMA overlap)
 # a hand-written candidate wins a shape when it is at most this much slower than the library (1.0: the
 # faster one; a 2 % preference measured 0.25 ms/step slower on the GPT-2 DDP step, same-box A/B)
 _PREFER_DTA = 1.0

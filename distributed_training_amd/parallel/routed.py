@@ -88,6 +88,14 @@ class RoutedComm(Communicator):
         self.counts[r] += 1
         return self.fast if r == "fast" else self.primary
 
+    def route_of(self, op: str, dtype: torch.dtype, nbytes: int) -> str:
+        """``"primary"`` / ``"fast"`` for a message (no counting, no lazy class)."""
+        routes = self.table.get((op, dtype))
+        if routes is None:
+            return "primary"
+        k = next((i for i, s in enumerate(self.sizes) if nbytes <= s), len(self.sizes) - 1)
+        return routes[k]
+
     def _add_class(self, size: int) -> None:
         """A new size class (every op and dtype calibrated at ``size``), kept in ascending order."""
         new = self._calibrate([size], self.iters)

@@ -67,7 +67,7 @@ case "$task" in
       2> gpurun_out/gemm64_bench.err || { tail -20 gpurun_out/gemm64_bench.err; exit 1; }
     python scripts/gemm64_table.py gpurun_out/gemm64_bench.jsonl ;;
   w4)
-    timeout -k 10 600 python scripts/bench_w4.py ${1:-llama,gpt2} ${2:-5} ${3:-5,6,7,8,3} > gpurun_out/w4_bench.jsonl \
+    timeout -k 10 600 python scripts/bench_w4.py ${1:-llama,gpt2} ${2:-5} ${3:-5,6,7,8,3} ${4:-fwd,dgrad,wgrad} > gpurun_out/w4_bench.jsonl \
       2> gpurun_out/w4_bench.err || { tail -20 gpurun_out/w4_bench.err; exit 1; }
     cut -c1-240 gpurun_out/w4_bench.jsonl ;;
   *)

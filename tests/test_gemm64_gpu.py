@@ -155,22 +155,26 @@ def test_gemm64_busy_chip(a_t, b_t, tile):
         assert err < 8e-3, (tile, a_t, b_t, err)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (300, 520, 384), (1000, 200, 1280),
-                                   (8192, 50304 // 16, 768), (64, 1000, 128)])
-def test_gemm_w4_exact_and_edges(M, N, K):
-    """Tile 9 (csrc/gemm_w4.hip: 4 waves, 256 x 256, intra-wave interleave; NT only): exact on small
-    integers at full tiles and at EDGE tiles in both dimensions (rows past M / N clamped in the DMA,
-    stores predicated), K from the shortest pipeline (two K-tiles) up."""
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 256), (304, 520, 384), (1000, 200, 1280),
+                                   (8192, 50304 // 16, 768), (64, 1000, 128),
+                                   # K tails (not a multiple of two 64-deep K-tiles): zero-filled DMA lanes
+                                   (256, 512, 72), (304, 264, 520), (64, 64, 8), (512, 256, 1016)])
+def test_gemm_w4_exact_and_edges(a_t, b_t, M, N, K):
+    """Tile 9 (csrc/gemm_w4.hip: 4 waves, 256 x 256, intra-wave interleave) in every operand layout: exact
+    on small integers at full tiles and at EDGE tiles in both dimensions (K-major rows / M-N-major chunks
+    past M / N clamped in the DMA, stores predicated), and with K tails (any K multiple of 8: the DMA lanes
+    past K read zeros through out-of-range buffer offsets)."""
     from distributed_training_amd.ops import native
 
-    gen = torch.Generator().manual_seed(M * 7 + N + K)
-    a = torch.randint(-3, 4, (M, K), generator=gen).float()
-    b = torch.randint(-3, 4, (N, K), generator=gen).float()
-    want = a @ b.t()
+    gen = torch.Generator().manual_seed(M * 7 + N + K + 2 * a_t + b_t)
+    a = torch.randint(-3, 4, (K, M) if a_t else (M, K), generator=gen).float()
+    b = torch.randint(-3, 4, (K, N) if b_t else (N, K), generator=gen).float()
+    want = (a.t() if a_t else a) @ (b if b_t else b.t())
     out = torch.full((M, N), float("nan"), device="cuda")
-    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), False, False, out, out_f32=True, tile=9)
+    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, out_f32=True, tile=9)
     torch.cuda.synchronize()
-    assert torch.equal(got.cpu(), want), (M, N, K)
+    assert torch.equal(got.cpu(), want), (a_t, b_t, M, N, K)
 
 
 @pytest.mark.parametrize("epi", [0, 2, 32])

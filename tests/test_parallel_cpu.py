@@ -655,3 +655,26 @@ def test_hybrid_shard_strategy_from_config():
     assert st.sharding == "hybrid"
     with pytest.raises(ValueError):
         FSDPStrategy(False, sharding="hsdp2")
+
+
+def test_step_graph_off_when_buckets_route_to_rccl():
+    """at world size > 1 the whole-step hipGraph is not used when any DDP bucket's
+    all-reduce routes to RCCL (RCCL-in-graph replay unverified on a multi-GPU node); IPC-only routes keep it."""
+    from types import SimpleNamespace
+
+    from distributed_training_amd.engine.trainer import Trainer
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.routed import MiB, RoutedComm
+
+    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB, 16 * MiB), calibrate=False)
+    buckets = [SimpleNamespace(start=0, end=MiB // 8), SimpleNamespace(start=MiB // 8, end=3 * MiB)]
+    flat = SimpleNamespace(grad=torch.zeros(1, dtype=torch.bfloat16))
+    tr = Trainer.__new__(Trainer)
+    tr.env = SimpleNamespace(world_size=2)
+    tr.model = SimpleNamespace(comm=rc, flat=flat, buckets=buckets)
+    rc.table[("all_reduce", torch.bfloat16)] = ["fast", "fast"]
+    assert not tr._buckets_on_rccl()
+    rc.table[("all_reduce", torch.bfloat16)] = ["fast", "primary"]  # the 5.8 MB bucket goes to RCCL
+    assert tr._buckets_on_rccl()
+    tr.env = SimpleNamespace(world_size=1)
+    assert not tr._buckets_on_rccl()
