@@ -56,6 +56,34 @@ __device__ __forceinline__ void load_bias4(const Args& g, int n, float (&bv)[4])
   }
 }
 
+// The bf16 values of output `which` (0: c, 1: c2 of the GELU dual store) at row m, columns n .. n+3 -- the
+// fused epilogue of store4 below without the store (the LDS-staged epilogue of csrc/gemm_w4.hip stores them)
+__device__ __forceinline__ bf16x4 val4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4], int which) {
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
+  if (g.epi == EPI_GELU) {
+    if (g.c2) {
+      const bf16x4 h4 = pk4_bf16(v[0], v[1], v[2], v[3]);
+      if (which == 0) return h4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_fast(bf2f(h4[r]));
+      return pk4_bf16(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
+  } else if (g.epi == EPI_DGELU) {
+    const bf16x4 h4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_fast(bf2f(h4[r]));
+  } else if (g.epi == EPI_RES) {
+    const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(g.res + (int64_t)m * g.ldr + n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);
+  }
+  return pk4_bf16(v[0], v[1], v[2], v[3]);
+}
+
 __device__ __forceinline__ void store4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4]) {
   float v[4];
 #pragma unroll

@@ -526,6 +526,7 @@ constexpr int kTiles = 4;
 constexpr int kBufDma = 16;
 // the 4-wave 256 x 256 tile with intra-wave read / MFMA overlap (csrc/gemm_w4.hip), every layout
 constexpr int kW4 = 9;
+constexpr int kW4S = 10;  // the same with the LDS-staged epilogue (whole 256-B row pieces per store)
 constexpr int kFlatDma = 32;
 __host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
 __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
@@ -535,14 +536,14 @@ __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128
 
 using namespace dta;
 
-hipError_t dta_gemm_w4_launch(const k64::Args& g, bool a_t, bool b_t, hipStream_t st);  // csrc/gemm_w4.hip
+hipError_t dta_gemm_w4_launch(const k64::Args& g, bool a_t, bool b_t, bool staged, hipStream_t st);  // gemm_w4.hip
 
 // 0 if the tile does not cover the problem, else the tile id (1-4, or 5-8 for the same tiles with
 // the two-phase K loop).  tile = 0: the fewest rounds of resident workgroups weighted by the tile's
 // relative efficiency (bigger tiles reuse more per byte).
 int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   // W4: any M, N, K multiples of 8 (clamped DMA rows / chunks, predicated stores, zero-filled K tail)
-  if (tile == k64::kW4) return K % 8 == 0 && K > 0 && M % 8 == 0 && N % 8 == 0 ? tile : 0;
+  if (tile == k64::kW4 || tile == k64::kW4S) return K % 8 == 0 && K > 0 && M % 8 == 0 && N % 8 == 0 ? tile : 0;
   if (K % k64::BK || K < k64::BK) return 0;
   if (tile & (k64::kBufDma | k64::kFlatDma)) {  // the same tile, DMA form chosen explicitly
     const int bits = tile & (k64::kBufDma | k64::kFlatDma);
@@ -583,7 +584,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
                         const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st) {
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
-  if (tile == k64::kW4) {
+  if (tile == k64::kW4 || tile == k64::kW4S) {
     // buffer-descriptor DMA with 32-bit offsets: every operand byte within 2 GiB of its base; a transposed
     // operand's extent a multiple of 8 (its DMA chunks are clamped whole)
     const int64_t a_bytes = 2 * (a_t ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
@@ -611,7 +612,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
     g.epi = epi;
     g.tiles_m = (M + 255) / 256;
     g.tiles_n = (N + 255) / 256;
-    return dta_gemm_w4_launch(g, a_t, b_t, st);
+    return dta_gemm_w4_launch(g, a_t, b_t, tile == k64::kW4S, st);
   }
   bool buf = (tile & k64::kFlatDma) == 0;
   tile &= ~(k64::kBufDma | k64::kFlatDma);

@@ -52,7 +52,7 @@ __device__ __forceinline__ bf16x4 w4_tr4(const char* lds, int byte_off) {
 // KT: K is not a multiple of 128 (two K-tiles): the loop runs over ceil(K / 128) pairs and every DMA
 // lane whose 8 k-values lie at or past K gets an out-of-range buffer offset -- the buffer unit returns
 // zeros for it, so the tail contributes nothing (K a multiple of 8: chunks are whole).
-template <bool AT, bool BT, bool KT>
+template <bool AT, bool BT, bool KT, bool STG>
 __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -71,8 +71,16 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   //   the row (row & 7 == lane >> 3); rows past M / N clamped to the last one.
   // M/N-major: piece gp = 4 q + wave holds k-rows 4 (gp & 15) + (lane >> 4) of half gp >> 4, chunk
   //   (lane & 15) ^ mswz(k); chunks past M / N clamped to the last full one.
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.a), 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.b), 0, 0x7fffffff, 0x00020000);
+  // (the base pointers through readfirstlane: the descriptor must live in SGPRs for the asm, and a kernel
+  // grown by the staged epilogue lost the compiler's proof that g's fields are uniform)
+  auto uni = [](const bf16* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<bf16*>(((uint64_t)hi << 32) | lo);
+  };
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(uni(g.a), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(uni(g.b), 0, 0x7fffffff, 0x00020000);
   unsigned voA[w4::NP], voB[w4::NP];
   auto src_off = [&](bool tr, int x0, int X, int64_t ld, int q) -> unsigned {
     if (!tr) {
@@ -225,6 +233,42 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
 
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment; rows / columns past M / N
   // (clamped duplicates) are not stored ----
+  if constexpr (STG) {  // (the host takes this form only for one bf16 output: no c32, no GELU dual store)
+    {
+      // LDS-staged: the wave's 128 x 128 bf16 result goes through its own 32 KiB of the (now free) LDS and
+      // leaves as whole 256-B row pieces (one global_store_dwordx4 per lane: 4 rows per instruction)
+      // instead of 64 stores of 16 rows x 32 B each.  Staging image: row r at 256 r, its 16-B chunk c at
+      // c ^ (r & 15) (2-way conflicts at most on the 8-B writes, none on the row reads).
+      bar();  // every wave's reads and DMA are done: the LDS is free
+      char* st = lds + wave * (w4::IMG);
+      auto pass = [&](bf16* dst, int64_t ldd, int which) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int nl = 16 * i + 4 * (lane >> 4);
+          float bv[4];
+          load_bias4(g, min(n0 + wc * 128 + nl, g.N - 4), bv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ml = 16 * j + (lane & 15);
+            const bf16x4 v = val4(g, min(m0 + wr * 128 + ml, g.M - 1), min(n0 + wc * 128 + nl, g.N - 4), acc[i][j],
+                                  bv, which);
+            *reinterpret_cast<bf16x4*>(st + ml * 256 + 16 * ((nl >> 3) ^ (ml & 15)) + 8 * ((nl >> 2) & 1)) = v;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+          const int row = 4 * r + (lane >> 4), c = lane & 15;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + row * 256 + 16 * (c ^ (row & 15)));
+          const int m = m0 + wr * 128 + row, n = n0 + wc * 128 + 8 * c;
+          if (m < g.M && n < g.N) *reinterpret_cast<bf16x8*>(dst + (int64_t)m * ldd + n) = v;
+        }
+      };
+      // (one output only: the host takes the per-fragment form for the GELU dual store -- a conditional
+      // second pass here made the compiler place the K loop's DMA descriptors in VGPRs)
+      pass(g.c, g.ldc, 0);
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int n = n0 + wc * 128 + 16 * i + 4 * (lane >> 4);
@@ -239,26 +283,34 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   }
 }
 
-template <bool AT, bool BT, bool KT>
+template <bool AT, bool BT, bool KT, bool STG>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(Args g) {
-  w4_body<AT, BT, KT>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  w4_body<AT, BT, KT, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
 }  // namespace k64
 }  // namespace dta
 
-template <bool KT>
+template <bool KT, bool STG>
 static void w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t st) {
   using namespace dta::k64;
   const dim3 grid(g.tiles_m * g.tiles_n), block(256);
-  if (!a_t && !b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, false, KT>), grid, block, 0, st, g);
-  else if (!a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, true, KT>), grid, block, 0, st, g);
-  else if (a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<true, true, KT>), grid, block, 0, st, g);
-  else hipLaunchKernelGGL((gemm_w4_kernel<true, false, KT>), grid, block, 0, st, g);
+  if (!a_t && !b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, false, KT, STG>), grid, block, 0, st, g);
+  else if (!a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<false, true, KT, STG>), grid, block, 0, st, g);
+  else if (a_t && b_t) hipLaunchKernelGGL((gemm_w4_kernel<true, true, KT, STG>), grid, block, 0, st, g);
+  else hipLaunchKernelGGL((gemm_w4_kernel<true, false, KT, STG>), grid, block, 0, st, g);
 }
 
-hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t st) {
-  if (g.K % (2 * dta::k64::BK)) w4_launch<true>(g, a_t, b_t, st);
-  else w4_launch<false>(g, a_t, b_t, st);
+// staged: the LDS-staged epilogue (tile id 10) instead of per-fragment stores (tile id 9); one bf16 output only
+hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, bool staged, hipStream_t st) {
+  const bool kt = g.K % (2 * dta::k64::BK) != 0;
+  staged = staged && g.c32 == nullptr && !(g.epi == dta::k64::EPI_GELU && g.c2 != nullptr);
+  if (kt) {
+    if (staged) w4_launch<true, true>(g, a_t, b_t, st);
+    else w4_launch<true, false>(g, a_t, b_t, st);
+  } else {
+    if (staged) w4_launch<false, true>(g, a_t, b_t, st);
+    else w4_launch<false, false>(g, a_t, b_t, st);
+  }
   return hipGetLastError();
 }

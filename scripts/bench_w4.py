@@ -68,7 +68,7 @@ def main():
                 ref = At @ Bt
                 outs = {"torch": torch.empty_like(ref)}
                 fns = {"torch": lambda: torch.mm(At, Bt, out=outs["torch"])}
-                for t in tiles + [9]:
+                for t in tiles + [9, 10]:
                     if C.gemm64_tile(M, N, K, t):
                         outs[t] = torch.empty_like(ref)
                         fns[t] = (lambda t=t, a=a, b=b, a_t=a_t, b_t=b_t:

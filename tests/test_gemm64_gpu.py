@@ -177,8 +177,9 @@ def test_gemm_w4_exact_and_edges(a_t, b_t, M, N, K):
     assert torch.equal(got.cpu(), want), (a_t, b_t, M, N, K)
 
 
+@pytest.mark.parametrize("tile", [9, 10])
 @pytest.mark.parametrize("epi", [0, 2, 32])
-def test_gemm_w4_epilogues(epi):
+def test_gemm_w4_epilogues(epi, tile):
     """Tile 9 with bias / alpha and the fused epilogues (GELU dual store, + residual) vs fp32 torch."""
     from distributed_training_amd.ops import native
 
@@ -190,13 +191,33 @@ def test_gemm_w4_epilogues(epi):
     ref = a.float() @ b.float().t() + bias.float()
     if epi == 2:
         h, g = native().gemm64(a, b, False, False, torch.empty(M, N, device="cuda", dtype=torch.bfloat16),
-                               torch.empty(M, N, device="cuda", dtype=torch.bfloat16), False, 1.0, bias, 2, None, 9)
+                               torch.empty(M, N, device="cuda", dtype=torch.bfloat16), False, 1.0, bias, 2, None, tile)
         _close(h, ref, K)
         _close(g, F.gelu(h.float(), approximate="tanh"), K)
     elif epi == 32:
         res = torch.randn(M, N, generator=gen).bfloat16().cuda()
-        y, = native().gemm64(a, b, False, False, None, None, False, 1.0, bias, 32, res, 9)
+        y, = native().gemm64(a, b, False, False, None, None, False, 1.0, bias, 32, res, tile)
         _close(y, ref + res.float(), K)
     else:
-        y, = native().gemm64(a, b, False, False, None, None, False, 0.5, bias, 0, None, 9)
+        y, = native().gemm64(a, b, False, False, None, None, False, 0.5, bias, 0, None, tile)
         _close(y, 0.5 * (a.float() @ b.float().t()) + bias.float(), K)
+
+
+@pytest.mark.parametrize("a_t,b_t", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (304, 520, 384), (8192, 50304 // 16, 768), (256, 512, 72)])
+def test_gemm_w4_staged_epilogue_exact(a_t, b_t, M, N, K):
+    """Tile 10: the W4 kernel with the LDS-staged bf16 epilogue (whole 256-B row pieces per store), edges
+    predicated: exact against fp32 on small integers whose sums stay exactly representable in bf16."""
+    from distributed_training_amd.ops import native
+
+    gen = torch.Generator().manual_seed(M + 3 * N + K + 2 * a_t + b_t)
+    a = torch.randint(-1, 2, (K, M) if a_t else (M, K), generator=gen).float()
+    b = torch.randint(-1, 2, (K, N) if b_t else (N, K), generator=gen).float()
+    want = ((a.t() if a_t else a) @ (b if b_t else b.t())).clamp(-256, 256)
+    a = a * (torch.rand(a.shape, generator=gen) < 0.25)  # sparse: |sum| <= K / 4 ... clamp checks below
+    want = (a.t() if a_t else a) @ (b if b_t else b.t())
+    assert want.abs().max() <= 256
+    out = torch.full((M, N), float("nan"), device="cuda").bfloat16()
+    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=10)
+    torch.cuda.synchronize()
+    assert torch.equal(got.float().cpu(), want), (a_t, b_t, M, N, K)
