@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Any, Optional
+from typing import Any, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -52,10 +52,10 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(n))
         self.eps = eps
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         return lm.layer_norm(x, self.weight, self.bias, self.eps)
 
-    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Any:
+    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """``(x + res, LN(x + res))`` in one kernel; ``res=None`` -> ``(x, LN(x))``."""
         if res is None:
             return x, self(x)
@@ -69,7 +69,7 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = lm.Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = lm.Linear(cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, S, C = x.shape
         # q/k/v are read in place from the projection output; dq/dk/dv land in one packed buffer
         y = lm.attention_packed(self.c_attn(x), self.n_head, self.n_head, causal=True)
@@ -82,7 +82,7 @@ class MLP(nn.Module):
         self.c_fc = lm.Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = lm.Linear(4 * cfg.n_embd, cfg.n_embd)
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         # c_proj(gelu(c_fc(x))): the GELU in c_fc's GEMM epilogue (pre-activation and activation stored
         # in one pass), its backward folded into c_proj's input-gradient GEMM
         h, a = lm.linear_gelu(x, self.c_fc.weight, self.c_fc.bias)
@@ -97,7 +97,7 @@ class Block(nn.Module):
         self.ln_2 = LayerNorm(cfg.n_embd)
         self.mlp = MLP(cfg)
 
-    def forward(self, x: torch.Tensor, h: Optional[torch.Tensor] = None) -> Any:
+    def forward(self, x: torch.Tensor, h: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """``h``: the previous block's MLP output, not yet added to the
         residual stream -- the add is fused into this block's ln_1 (and this
         block's MLP output is handed on the same way), so no residual add runs
@@ -155,7 +155,7 @@ class GPT2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Logits ``[B, S, V]``; with ``targets``, the mean token cross-entropy
         (LM head and loss fused: the logits are never materialised twice)."""
         B, S = idx.shape

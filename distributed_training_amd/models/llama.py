@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Any, Optional
+from typing import Any, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -47,10 +47,10 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(n))
         self.eps = eps
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         return lm.rms_norm(x, self.weight, self.eps)
 
-    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Any:
+    def add_forward(self, x: torch.Tensor, res: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """``(x + res, RMSNorm(x + res))`` in one kernel; ``res=None`` -> ``(x, RMSNorm(x))``."""
         if res is None:
             return x, self(x)
@@ -65,7 +65,7 @@ class Attention(nn.Module):
         self.wqkv = lm.Linear(cfg.n_embd, (self.H + 2 * self.Hkv) * self.D, bias=False)
         self.wo = lm.Linear(self.H * self.D, cfg.n_embd, bias=False)
 
-    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         B, S, _ = x.shape
         # RoPE + GQA attention on the packed projection output (one packed dQKV in backward)
         y = lm.attention_packed(self.wqkv(x), self.H, self.Hkv, causal=True, rope=(cos, sin))
@@ -78,7 +78,7 @@ class FeedForward(nn.Module):
         self.w13 = lm.Linear(cfg.n_embd, 2 * cfg.ffn_hidden, bias=False)
         self.w2 = lm.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.w2(lm.swiglu(self.w13(x)))
 
 
@@ -90,7 +90,7 @@ class Block(nn.Module):
         self.ffn_norm = RMSNorm(cfg.n_embd, cfg.norm_eps)
         self.feed_forward = FeedForward(cfg)
 
-    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, h: Optional[torch.Tensor] = None) -> Any:
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, h: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Residual adds fused into the norms (see GPT-2 ``Block``); returns ``(x, h)``."""
         x, y = self.attention_norm.add_forward(x, h)
         x, y = self.ffn_norm.add_forward(x, self.attention(y, cos, sin))
@@ -138,7 +138,7 @@ class Llama(nn.Module):
     def enable_activation_checkpointing(self, on: bool = True) -> None:
         self.activation_checkpointing = on
 
-    def fsdp_extra_units(self) -> Any:
+    def fsdp_extra_units(self) -> List[nn.Module]:
         """Modules that are FSDP units of their own besides the blocks (parallel/fsdp.py
         ``lm_wrap_policy``): the embedding and the output head, 525 M parameters each at 8B --
         in the root unit they would be gathered synchronously before the forward and held
@@ -148,7 +148,7 @@ class Llama(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Logits; with ``targets``, the mean token cross-entropy (head + loss fused)."""
         x = self.tok_embeddings(idx)
         cos, sin = self.rope_cos, self.rope_sin

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Any, Callable, Dict, Optional, Tuple
+from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import torch
 import torch.nn.functional as F
@@ -54,14 +54,14 @@ def attention_reference(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causa
 
 class _FlashAttn(Function):
     @staticmethod
-    def forward(ctx: Any, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool, scale: float) -> Any:
+    def forward(ctx: Any, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool, scale: float) -> torch.Tensor:
         o, lse = native().attn_fwd(q, k, v, bool(causal), float(scale), -1)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale = causal, scale
         return o
 
     @staticmethod
-    def backward(ctx: Any, do: torch.Tensor) -> Any:
+    def backward(ctx: Any, do: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
         dq, dk, dv = native().attn_bwd(do, q, k, v, o, lse, bool(ctx.causal), float(ctx.scale), -1)
@@ -77,7 +77,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = 
     return attention_reference(q, k, v, causal, scale)
 
 
-def _split_qkv(qkv: torch.Tensor, H: int, Hkv: int) -> Any:
+def _split_qkv(qkv: torch.Tensor, H: int, Hkv: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     B, S, W = qkv.shape
     D = W // (H + 2 * Hkv)
     t = qkv.view(B, S, H + 2 * Hkv, D)
@@ -93,7 +93,7 @@ class _PackedAttn(Function):
 
     @staticmethod
     def forward(ctx: Any, qkv: torch.Tensor, H: int, Hkv: int, causal: bool, scale: float, cos: torch.Tensor,
-                sin: torch.Tensor) -> Any:
+                sin: torch.Tensor) -> torch.Tensor:
         B, S, W = qkv.shape
         D = W // (H + 2 * Hkv)
         if cos is not None:
@@ -106,7 +106,7 @@ class _PackedAttn(Function):
         return o
 
     @staticmethod
-    def backward(ctx: Any, do: torch.Tensor) -> Any:
+    def backward(ctx: Any, do: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         qkv, o, lse, cos, sin = ctx.saved_tensors
         H, Hkv, causal, scale, has_rope = ctx.cfg
         B, S, W = qkv.shape
@@ -141,7 +141,7 @@ def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: boo
 # ------------------------------------------------------------------ norms
 class _Norm(Function):
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool, eps: float) -> Any:
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool, eps: float) -> torch.Tensor:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, mean, rstd, _ = native().norm_fwd(x2, w.contiguous(), None if rms else b.contiguous(), rms, eps, -1)
@@ -151,7 +151,7 @@ class _Norm(Function):
         return y.view(shape)
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         x2, w, mean, rstd = ctx.saved_tensors
         pw, pb = ctx.params
         dx, dw, db = native().norm_bwd(dy.reshape(x2.shape).contiguous(), x2, w.contiguous(), mean, rstd, ctx.rms,
@@ -166,7 +166,7 @@ class _AddNorm(Function):
 
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool,
-                eps: float) -> Any:
+                eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, mean, rstd, xsum = native().norm_fwd(x2, w.contiguous(), None if rms else b.contiguous(), rms, eps, -1,
@@ -180,7 +180,7 @@ class _AddNorm(Function):
         return xsum.view(shape), y.view(shape)
 
     @staticmethod
-    def backward(ctx: Any, g_x: Optional[torch.Tensor], g_y: Optional[torch.Tensor]) -> Any:
+    def backward(ctx: Any, g_x: Optional[torch.Tensor], g_y: Optional[torch.Tensor]) -> Tuple[Optional[torch.Tensor], ...]:
         xsum, w, mean, rstd = ctx.saved_tensors
         if g_y is None:
             return g_x, g_x, None, None, None, None
@@ -193,7 +193,7 @@ class _AddNorm(Function):
         return dx, dx, dw, (None if ctx.rms else db), None, None
 
 
-def add_layer_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
+def add_layer_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
     """Returns ``(x + res, layer_norm(x + res))``."""
     if x.is_cuda:
         _need_bf16(x, res, w, b)
@@ -202,7 +202,7 @@ def add_layer_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch
     return xn, F.layer_norm(xn, (xn.shape[-1],), w, b, eps)
 
 
-def add_rms_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
+def add_rms_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
     """Returns ``(x + res, rms_norm(x + res))``."""
     if x.is_cuda:
         _need_bf16(x, res, w)
@@ -211,14 +211,14 @@ def add_rms_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float
     return xn, rms_norm(xn, w, eps)
 
 
-def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     if x.is_cuda:
         _need_bf16(x, w, b)
         return _Norm.apply(x, w, b, False, eps)
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
-def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     if x.is_cuda:
         _need_bf16(x, w)
         return _Norm.apply(x, w, None, True, eps)
@@ -348,7 +348,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
 
 
 def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
-              alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> Any:
+              alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     C = native()
     if impl >= K64:
         return C.gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
@@ -369,7 +369,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
 
-    def run_torch() -> Any:
+    def run_torch() -> torch.Tensor:
         A = a.t() if a_t else a
         B = b if b_t else b.t()
         if bias is not None and alpha == 1.0:
@@ -401,11 +401,11 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     N = w.shape[0]
     C = native()
 
-    def run_torch() -> Any:
+    def run_torch() -> Tuple[torch.Tensor, torch.Tensor]:
         h = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
         return h, C.gelu_fwd(h, -1)
 
-    def run_k64(t: int) -> Any:
+    def run_k64(t: int) -> Tuple[torch.Tensor, ...]:
         h = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
         return tuple(C.gemm64(x2, w, False, False, h, torch.empty_like(h), False, 1.0, b, 2, None, t))
 
@@ -587,7 +587,7 @@ def wgrad_flush() -> None:
 
 
 def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
-                 b: Optional[torch.Tensor] = None) -> Any:
+                 b: Optional[torch.Tensor] = None) -> Union[torch.Tensor, Tuple[torch.Tensor, Optional[torch.Tensor]]]:
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
     Small outputs with a long token reduction (GPT-2: 768 x 768 .. 3072 x 768
     over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip), which fills
@@ -637,7 +637,7 @@ class _Linear(Function):
     kernel or :func:`gemm` (see _weight_grad)."""
 
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> Any:
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)  # the Parameters themselves (their .grad decides a direct write)
@@ -647,7 +647,7 @@ class _Linear(Function):
         return gemm(x2, w, bias=b, kind="fwd").view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         x, w = ctx.saved_tensors
         pw, pb = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -675,12 +675,12 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and h2.is_contiguous()
           and h2.data_ptr() % 16 == 0 and N % 8 == 0)
 
-    def run(impl: Any) -> Any:
+    def run(impl: Any) -> torch.Tensor:
         if impl >= K64:
             return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
         return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, impl)
 
-    def run_torch() -> Any:
+    def run_torch() -> torch.Tensor:
         return C.gelu_bwd(torch.mm(dy2, w), h2, -1)
 
     impl = 0
@@ -702,7 +702,7 @@ class _GeluLinear(Function):
     :func:`_dgelu_dgrad` (the GELU backward folded into the input-gradient GEMM)."""
 
     @staticmethod
-    def forward(ctx: Any, h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, a: Optional[torch.Tensor] = None) -> Any:
+    def forward(ctx: Any, h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, a: Optional[torch.Tensor] = None) -> torch.Tensor:
         hc = h.contiguous()
         if a is None:
             a = native().gelu_fwd(hc, -1)
@@ -715,7 +715,7 @@ class _GeluLinear(Function):
         return gemm(a2, w, bias=b, kind="fwd").view(*h.shape[:-1], w.shape[0])
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         h, a, w = ctx.saved_tensors
         pw, pb = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -741,7 +741,7 @@ class _LinearGelu(Function):
     and backward is exactly :class:`_Linear`'s."""
 
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> Any:
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.params = (w, b)
@@ -758,13 +758,13 @@ class _LinearGelu(Function):
         return h, a
 
     @staticmethod
-    def backward(ctx: Any, dh: Optional[torch.Tensor], da: Optional[torch.Tensor]) -> Any:
+    def backward(ctx: Any, dh: Optional[torch.Tensor], da: Optional[torch.Tensor]) -> Tuple[Optional[torch.Tensor], ...]:
         if dh is None:  # (h unused downstream: nothing to propagate)
             return None, None, None
         return _Linear.backward(ctx, dh)
 
 
-def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> Any:
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``(h, gelu(h))`` for ``h = linear(x, w, b)``; feed both to :func:`gelu_linear` (``a=``)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
@@ -774,7 +774,7 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = No
 
 
 def gelu_linear(h: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
-                a: Optional[torch.Tensor] = None) -> Any:
+                a: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``linear(gelu(h), w, b)`` with the GELU backward fused into the input-gradient GEMM on GPU;
     ``a``: gelu(h) already computed (by :func:`linear_gelu`'s epilogue)."""
     if h.is_cuda and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
@@ -783,7 +783,7 @@ def gelu_linear(h: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = No
     return linear(gelu(h), w, b)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> Any:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
             and x.shape[-1] % 8 == 0 and w.shape[0] % 8 == 0:
         return _Linear.apply(x, w, b)
@@ -793,7 +793,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
 class Linear(torch.nn.Linear):
     """``nn.Linear`` (same parameters / state-dict keys) routed through :func:`linear`."""
 
-    def forward(self, x: torch.Tensor) -> Any:
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
         return linear(x, self.weight, self.bias)
 
 
@@ -805,7 +805,7 @@ class LMHead(torch.nn.Linear):
     last blocks, its gradient reduce-scattered as soon as the head's backward -- the first of
     the backward -- is done."""
 
-    def forward(self, y: torch.Tensor, targets: Optional[torch.Tensor] = None) -> Any:
+    def forward(self, y: torch.Tensor, targets: Optional[torch.Tensor] = None) -> torch.Tensor:
         if targets is not None:
             return linear_cross_entropy(y, self.weight, targets)
         return linear(y, self.weight, self.bias)
@@ -817,25 +817,25 @@ class Embedding(torch.nn.Embedding):
 
     fsdp_backward_needs_params = False
 
-    def forward(self, idx: torch.Tensor) -> Any:
+    def forward(self, idx: torch.Tensor) -> torch.Tensor:
         return embedding(idx, self.weight)
 
 
 # ------------------------------------------------------------------ activations
 class _Gelu(Function):
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor) -> Any:
+    def forward(ctx: Any, x: torch.Tensor) -> torch.Tensor:
         xc = x.contiguous()
         ctx.save_for_backward(xc)
         return native().gelu_fwd(xc, -1)
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> torch.Tensor:
         (x,) = ctx.saved_tensors
         return native().gelu_bwd(dy.contiguous(), x, -1)
 
 
-def gelu(x: torch.Tensor) -> Any:
+def gelu(x: torch.Tensor) -> torch.Tensor:
     if x.is_cuda:
         _need_bf16(x)
         return _Gelu.apply(x)
@@ -844,18 +844,18 @@ def gelu(x: torch.Tensor) -> Any:
 
 class _SwiGLU(Function):
     @staticmethod
-    def forward(ctx: Any, ab: torch.Tensor) -> Any:
+    def forward(ctx: Any, ab: torch.Tensor) -> torch.Tensor:
         abc = ab.contiguous()
         ctx.save_for_backward(abc)
         return native().swiglu_fwd(abc, -1)
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> torch.Tensor:
         (ab,) = ctx.saved_tensors
         return native().swiglu_bwd(dy.contiguous(), ab, -1)
 
 
-def swiglu(ab: torch.Tensor) -> Any:
+def swiglu(ab: torch.Tensor) -> torch.Tensor:
     """``silu(a) * b`` for ``ab = [a | b]`` along the last dim."""
     if ab.is_cuda:
         _need_bf16(ab)
@@ -874,7 +874,7 @@ def rope_tables(seq_len: int, head_dim: int, theta: float = 10000.0,
     return f.cos().float().to(device), f.sin().float().to(device)
 
 
-def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
+def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     S, D = x.shape[1], x.shape[-1]
     c = cos[:S].view(1, S, 1, D // 2).to(torch.float32)
     s = sin[:S].view(1, S, 1, D // 2).to(torch.float32)
@@ -884,21 +884,21 @@ def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any
 
 class _Rope(Function):
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
+    def forward(ctx: Any, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         y = x.contiguous().clone()
         native().rope_(y, cos, sin, False, -1)
         ctx.save_for_backward(cos, sin)
         return y
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         cos, sin = ctx.saved_tensors
         dx = dy.contiguous().clone()
         native().rope_(dx, cos, sin, True, -1)
         return dx, None, None
 
 
-def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> Any:
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     """Rotate-half RoPE on [B, S, heads, D]."""
     if x.is_cuda:
         _need_bf16(x)
@@ -942,13 +942,13 @@ class _Embedding(Function):
     bucket copy of the sum."""
 
     @staticmethod
-    def forward(ctx: Any, idx: torch.Tensor, w: torch.Tensor) -> Any:
+    def forward(ctx: Any, idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         ctx.save_for_backward(idx)
         ctx.wparam = w
         return F.embedding(idx, w)
 
     @staticmethod
-    def backward(ctx: Any, dy: torch.Tensor) -> Any:
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         (idx,) = ctx.saved_tensors
         w = ctx.wparam
         if not ctx.needs_input_grad[1]:
@@ -981,7 +981,7 @@ def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------ loss
 class _CrossEntropy(Function):
     @staticmethod
-    def forward(ctx: Any, logits: torch.Tensor, target: torch.Tensor, ignore_index: int) -> Any:
+    def forward(ctx: Any, logits: torch.Tensor, target: torch.Tensor, ignore_index: int) -> torch.Tensor:
         # no host sync: the valid-token count stays on the device
         count = (target != ignore_index).sum().clamp_min(1).float()
         dlogits = torch.empty_like(logits)
@@ -990,7 +990,7 @@ class _CrossEntropy(Function):
         return loss_rows.sum() / count
 
     @staticmethod
-    def backward(ctx: Any, g: torch.Tensor) -> Any:
+    def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         dlogits, count = ctx.saved_tensors
         return dlogits * (g / count).to(dlogits.dtype), None, None
 
@@ -1004,7 +1004,7 @@ class _LinearCrossEntropy(Function):
     pass over it."""
 
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int) -> Any:
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int) -> torch.Tensor:
         x2 = x.reshape(-1, x.shape[-1])
         logits = gemm(x2, w, kind="head_fwd")
         count = (target != ignore_index).sum().clamp_min(1).float()
@@ -1015,7 +1015,7 @@ class _LinearCrossEntropy(Function):
         return loss_rows.sum() / count
 
     @staticmethod
-    def backward(ctx: Any, g: torch.Tensor) -> Any:
+    def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         x2, w, dlogits, count = ctx.saved_tensors
         s = (g / count).to(dlogits.dtype)  # stays on the device (no host sync in backward)
         dx = dw = None
@@ -1028,7 +1028,7 @@ class _LinearCrossEntropy(Function):
         return dx, dw, None, None
 
 
-def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
+def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
     """Mean token cross-entropy of ``x @ w.T`` against ``target`` (the LM head + loss)."""
     if x.is_cuda:
         _need_bf16(x, w)
@@ -1037,7 +1037,7 @@ def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor,
     return F.cross_entropy(logits.float(), target.reshape(-1), ignore_index=ignore_index)
 
 
-def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
     """Mean token cross-entropy over ``logits [N, V]`` (fused fwd+bwd kernel on GPU)."""
     if logits.is_cuda:
         _need_bf16(logits)

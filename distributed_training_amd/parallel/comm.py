@@ -25,7 +25,7 @@ import os
 import sys
 import threading
 import time
-from typing import Any, Callable, Deque, List, Optional, Tuple
+from typing import Any, Callable, Deque, Iterator, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -35,7 +35,7 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
 
 
 @contextlib.contextmanager
-def _stdout_to_stderr() -> Any:
+def _stdout_to_stderr() -> Iterator[None]:
     """Redirect the C-level stdout (fd 1) to stderr for the duration."""
     sys.stdout.flush()
     saved = os.dup(1)
@@ -110,12 +110,12 @@ class TorchComm(Communicator):
         self.device = device or torch.device("cpu")
         self.backend = dist.get_backend(group) if dist.is_initialized() else "none"
 
-    def _w(self, work: Any, async_op: bool) -> Any:
+    def _w(self, work: Any, async_op: bool) -> Optional[CommWork]:
         if async_op:
             return CommWork(torch_work=work)
         return None
 
-    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Any:
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
         if self.world_size == 1:
             return CommWork() if async_op else None
         if op == "avg":
@@ -124,7 +124,7 @@ class TorchComm(Communicator):
         work = dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Any:
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Optional[CommWork]:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -132,7 +132,7 @@ class TorchComm(Communicator):
         work = dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         return self._w(work, async_op)
 
-    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Any:
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
         if self.world_size == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -149,7 +149,7 @@ class TorchComm(Communicator):
             post()
         return None
 
-    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Optional[CommWork]:
         if self.world_size == 1:
             return CommWork() if async_op else None
         if self.group is not None:  # ``src`` is a rank of this communicator's group, as for every backend here
@@ -373,7 +373,7 @@ class RcclComm(_StreamComm):
     def supports_avg(self) -> bool:
         return True
 
-    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Any:
+    def all_reduce(self, t: Any, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
         if self._p2p_ok(t, op):
             sc = 1.0 / self.world_size if op == "avg" else 1.0
             h, it = self._p2p._h, self._p2p.timeout_iters
@@ -381,7 +381,7 @@ class RcclComm(_StreamComm):
         return self._enqueue(lambda s: self._comm.all_reduce(t, op, s), async_op, [t],
                              f"all_reduce {t.numel()} x {t.dtype}")
 
-    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Any:
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False) -> Optional[CommWork]:
         if self.world_size == 1:  # single rank: a device copy on the current stream
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.view(-1))
@@ -389,11 +389,11 @@ class RcclComm(_StreamComm):
         return self._enqueue(lambda s: self._comm.all_gather(out, inp, s), async_op, [out, inp],
                              f"all_gather {inp.numel()} x {inp.dtype}")
 
-    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Any:
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", async_op: bool = False) -> Optional[CommWork]:
         return self._enqueue(lambda s: self._comm.reduce_scatter(out, inp, op, s), async_op, [out, inp],
                              f"reduce_scatter {out.numel()} x {out.dtype}")
 
-    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Any:
+    def broadcast(self, t: Any, src: int = 0, async_op: bool = False) -> Optional[CommWork]:
         return self._enqueue(lambda s: self._comm.broadcast(t, src, s), async_op, [t],
                              f"broadcast {t.numel()} x {t.dtype}")
 

@@ -41,7 +41,7 @@ from __future__ import annotations
 import contextlib
 import hashlib
 import logging
-from typing import Any, List, Optional
+from typing import Any, Callable, Iterator, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -142,7 +142,7 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._pending = [[] for _ in self.buckets]
 
-    def _make_hook(self, i: int) -> Any:
+    def _make_hook(self, i: int) -> Callable[[torch.Tensor], None]:
         def hook(p: torch.Tensor) -> None:
             if not self.require_sync:
                 return
@@ -256,7 +256,7 @@ class DistributedDataParallel(nn.Module):
         lm.FLUSH_LISTENERS.append(on_flush)
         return True
 
-    def _ov_range(self, b: int) -> Any:
+    def _ov_range(self, b: int) -> Tuple[int, int]:
         bk = self.buckets[b]
         end = self.flat.master.numel() if b == len(self.buckets) - 1 else bk.end
         return bk.start, end
@@ -337,7 +337,7 @@ class DistributedDataParallel(nn.Module):
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
-    def no_sync(self) -> Any:
+    def no_sync(self) -> Iterator[None]:
         old = self.require_sync
         self.require_sync = False
         try:
@@ -366,7 +366,7 @@ class DistributedDataParallel(nn.Module):
                     sd[key] = self.flat.master_view(i).detach()
         return sd
 
-    def load_state_dict(self, state_dict: Any, strict: bool = True) -> Any:
+    def load_state_dict(self, state_dict: Any, strict: bool = True) -> None:
         res = super().load_state_dict(state_dict, strict=strict)
         if self.flat.mixed:
             with torch.no_grad():

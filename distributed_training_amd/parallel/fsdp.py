@@ -42,7 +42,7 @@ from __future__ import annotations
 import functools
 import os
 import logging
-from typing import Any, Callable, Dict, List, Optional, Sequence, Set, Tuple, Type, Union
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Set, Tuple, Type, Union
 
 import torch
 import torch.nn as nn
@@ -101,13 +101,13 @@ class _SplitInto(torch.autograd.Function):
     the unit's gradient, plus a copy into the flat gradient after it)."""
 
     @staticmethod
-    def forward(ctx: Any, full: torch.Tensor, unit: Any) -> Any:
+    def forward(ctx: Any, full: torch.Tensor, unit: Any) -> Tuple[torch.Tensor, ...]:
         ctx.unit = unit
         ctx.set_materialize_grads(False)
         return tuple(full.split(unit._split_sizes))
 
     @staticmethod
-    def backward(ctx: Any, *grads: Any) -> Any:
+    def backward(ctx: Any, *grads: Any) -> Tuple[Optional[torch.Tensor], None]:
         u = ctx.unit
         dest = u.grad_buffer()
         pos = 0
@@ -510,7 +510,7 @@ class FullyShardedDataParallel(nn.Module):
             return self._fwd_order[k]
         return None
 
-    def _make_pre_forward(self, u: _Unit) -> Any:
+    def _make_pre_forward(self, u: _Unit) -> Callable[[nn.Module, Any], None]:
         def pre(mod: Any, args: Any) -> Any:
             if u.in_backward:  # checkpoint recomputation: already gathered
                 u.unshard(async_op=False)
@@ -528,7 +528,7 @@ class FullyShardedDataParallel(nn.Module):
 
         return pre
 
-    def _make_post_forward(self, u: _Unit) -> Any:
+    def _make_post_forward(self, u: _Unit) -> Callable[[nn.Module, Any, Any], Any]:
         def post(mod: Any, args: Any, output: Any) -> Any:
             if u.in_backward:
                 # activation-checkpoint recomputation inside this unit's backward:
@@ -550,7 +550,7 @@ class FullyShardedDataParallel(nn.Module):
             return
         u._bwd_ready = False
 
-        def hook(grad: torch.Tensor) -> Any:
+        def hook(grad: torch.Tensor) -> torch.Tensor:
             if not u._bwd_ready:
                 u._bwd_ready = True
                 u.in_backward = True
@@ -819,7 +819,7 @@ class FullyShardedDataParallel(nn.Module):
         return self.full_state_dict(rank0_only=True, offload_to_cpu=True)
 
     @torch.no_grad()
-    def load_state_dict(self, state_dict: Any, strict: bool = True) -> Any:
+    def load_state_dict(self, state_dict: Any, strict: bool = True) -> None:
         fg = self.shards
         missing = []
         for u in self.units:
@@ -915,7 +915,7 @@ class FullyShardedDataParallel(nn.Module):
                  "shard": u.shard_size, "root": int(u.is_root)} for u in self.units]
 
 
-def _iter_tensors(x: Any) -> Any:
+def _iter_tensors(x: Any) -> Iterator[torch.Tensor]:
     if isinstance(x, torch.Tensor):
         yield x
     elif isinstance(x, (list, tuple)):
