@@ -36,6 +36,9 @@ hipError_t dta_linear_step(const dta::LinStepArgs*, hipStream_t);
 int dta_gemm_bf16_tile(int, int, int, int);
 int dta_gemm_group_max();
 int dta_gemm_k64_group_max();
+hipError_t dta_gemm_w4_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
+                                   void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
+                                   hipStream_t);
 hipError_t dta_gemm_k64_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
                                     void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
                                     hipStream_t);
@@ -193,11 +196,13 @@ torch::Tensor gemm_bf16(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t, c1
 
 // Grouped weight (+ bias) gradients: dW_i = A_i^T B_i into c_i, db_i = column sums of A_i
 // (A_i = dy [K, M_i], B_i = x [K, N_i], c_i [M_i, N_i] bf16; db_i bf16 [M_i] or None).
-// k64 = true: csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; K multiples of 64), else
-// csrc/gemm_bf16.hip's (32-deep stages).
+// impl (``k64``): 1 = csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; K multiples of 64), 2 =
+// csrc/gemm_w4.hip's (4-wave intra-wave interleave; M, N, K multiples of 8), 0 = csrc/gemm_bf16.hip's
+// (32-deep stages).
 void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, std::vector<torch::Tensor> c,
-                      std::vector<c10::optional<torch::Tensor>> db, int64_t stream, bool k64) {
+                      std::vector<c10::optional<torch::Tensor>> db, int64_t stream, int64_t impl) {
   const int n = (int)a.size();
+  const bool k64 = impl != 0, w4 = impl == 2;
   const int gmax = k64 ? dta_gemm_k64_group_max() : dta_gemm_group_max();
   TORCH_CHECK(n >= 1 && n <= gmax && (int)b.size() == n && (int)c.size() == n && (int)db.size() == n,
               "gemm_wgrad_group: 1..", gmax, " problems, equal list lengths");
@@ -215,9 +220,15 @@ void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b
                   "gemm_wgrad_group: bf16 2-D GPU tensors, unit inner stride, 16-byte aligned rows");
     TORCH_CHECK(A.size(0) == B.size(0) && Cc.size(0) == A.size(1) && Cc.size(1) == B.size(1),
                 "gemm_wgrad_group: A [K, M], B [K, N], C [M, N]");
-    TORCH_CHECK(A.size(1) % 256 == 0 && B.size(1) % 256 == 0 && A.size(0) % (k64 ? 64 : 32) == 0 && A.size(0) > 0 &&
-                    A.size(0) < (1 << 30),
-                "gemm_wgrad_group: M, N multiples of 256, K a multiple of 32 (64 for k64)");
+    if (w4) {
+      TORCH_CHECK(A.size(1) % 8 == 0 && B.size(1) % 8 == 0 && A.size(0) % 8 == 0 && A.size(0) > 0 &&
+                      A.size(0) < (1 << 30),
+                  "gemm_wgrad_group (w4): M, N, K multiples of 8");
+    } else {
+      TORCH_CHECK(A.size(1) % 256 == 0 && B.size(1) % 256 == 0 && A.size(0) % (k64 ? 64 : 32) == 0 &&
+                      A.size(0) > 0 && A.size(0) < (1 << 30),
+                  "gemm_wgrad_group: M, N multiples of 256, K a multiple of 32 (64 for k64)");
+    }
     ap[i] = A.data_ptr();
     bp[i] = B.data_ptr();
     cp[i] = Cc.data_ptr();
@@ -235,7 +246,8 @@ void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b
       dp[i] = d.data_ptr();
     }
   }
-  ok((k64 ? dta_gemm_k64_wgrad_group : dta_gemm_wgrad_group)(n, ap.data(), lda.data(), bp.data(), ldb.data(), cp.data(),
+  ok((w4 ? dta_gemm_w4_wgrad_group : k64 ? dta_gemm_k64_wgrad_group : dta_gemm_wgrad_group)(
+         n, ap.data(), lda.data(), bp.data(), ldb.data(), cp.data(),
                                                              ldc.data(), M.data(), N.data(), K.data(), dp.data(),
                                                              stream_of(stream)),
      "gemm_wgrad_group");

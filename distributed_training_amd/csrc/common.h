@@ -190,6 +190,19 @@ __device__ __forceinline__ void bglds16(__amdgpu_buffer_rsrc_t rsrc, unsigned vo
       : "memory");
 }
 
+// bglds16 without the M0 save / restore, for kernels that own M0 (no other M0 use in the loop: the
+// compiler is told M0 is clobbered).  The restore right behind the load waited for the load to dispatch
+// (it reads M0 then): with one wave per SIMD that wait sat in the MFMA stream (csrc/gemm_w4.hip).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // M0 is "reserved": the kernels using this have no other M0 use
+__device__ __forceinline__ void bglds16_m0(__amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff, unsigned dst) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :
+               : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 // LDS byte address of a __shared__ object (wave-uniform)
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const __attribute__((address_space(3))) char*)p);

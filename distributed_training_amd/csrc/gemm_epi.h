@@ -115,6 +115,14 @@ __device__ __forceinline__ void store4(const Args& g, int m, int n, const f32x4&
   *reinterpret_cast<bf16x4*>(g.c + (int64_t)m * g.ldc + n) = pk4_bf16(v[0], v[1], v[2], v[3]);
 }
 
+// Grouped weight gradients: several problems' tiles in ONE launch (csrc/gemm_k64.hip, csrc/gemm_w4.hip)
+constexpr int kGroupMax = 16;
+struct GroupArgs {
+  int n;
+  int tile_start[kGroupMax + 1];
+  Args p[kGroupMax];
+};
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");

@@ -477,12 +477,6 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
 // two-phase loop): dW_i = A_i^T B_i for several problems in ONE launch of 256 x 256 tiles over the
 // full token reduction, the bias gradients from the same MFMA pipe (CS); the tiles of all problems
 // form one list, XCD-remapped so each XCD takes a contiguous run.
-constexpr int kGroupMax = 16;
-struct GroupArgs {
-  int n;
-  int tile_start[kGroupMax + 1];
-  Args p[kGroupMax];
-};
 
 template <bool BUF>
 __global__ void __launch_bounds__(512) gemm_k64_group_kernel(GroupArgs ga) {

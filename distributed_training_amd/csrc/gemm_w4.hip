@@ -52,9 +52,12 @@ __device__ __forceinline__ bf16x4 w4_tr4(const char* lds, int byte_off) {
 // KT: K is not a multiple of 128 (two K-tiles): the loop runs over ceil(K / 128) pairs and every DMA
 // lane whose 8 k-values lie at or past K gets an out-of-range buffer offset -- the buffer unit returns
 // zeros for it, so the tail contributes nothing (K a multiple of 8: chunks are whole).
-template <bool AT, bool BT, bool KT, bool STG>
-__device__ __forceinline__ void w4_body(const Args& g, const int t) {
-  __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
+// CS: the kernel may also sum the bias gradient db[m] = sum_k A(m, k) (weight gradients; done where the
+// uniform flag `cs` is set: tile column 0 of a problem with db): MFMAs of A's fragments against an all-ones
+// B fragment, the two waves sharing A rows taking four fragments each (+4 MFMAs per half-step per wave;
+// VGPR accumulators: the AGPR file is full)
+template <bool AT, bool BT, bool KT, bool STG, bool CS = false>
+__device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, const bool cs = false) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -110,8 +113,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   auto dma = [&](int kt, int par) {  // all 16 pieces of K-tile kt into image par (prologue form)
 #pragma unroll
     for (int q = 0; q < w4::NP; ++q) {
-      bglds16(rsA, kt_off(voA[q], AT, q, kt), (unsigned)kt * kstepA, lds0 + par * w4::IMG + (4 * q + wave) * 1024);
-      bglds16(rsB, kt_off(voB[q], BT, q, kt), (unsigned)kt * kstepB,
+      bglds16_m0(rsA, kt_off(voA[q], AT, q, kt), (unsigned)kt * kstepA, lds0 + par * w4::IMG + (4 * q + wave) * 1024);
+      bglds16_m0(rsB, kt_off(voB[q], BT, q, kt), (unsigned)kt * kstepB,
               lds0 + (2 + par) * w4::IMG + (4 * q + wave) * 1024);
     }
   };
@@ -160,6 +163,37 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a0[8], b0[8], a1[8], b1[8];  // half-step 0 / 1 fragments: A rows (j), B rows (i)
+  f32x4 accb[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                   f32x4{0.f, 0.f, 0.f, 0.f}};
+  // (the all-ones fragment and the zeroed accb are made opaque once, here: a constant the compiler
+  // re-materialises with a VALU write right before an asm MFMA that reads it is an unguarded VALU -> MFMA
+  // hazard; the fragment index 4 wc + jj goes through a uniform branch for the same reason -- a runtime
+  // register-array index becomes v_cndmask selects right before the MFMA)
+  bf16x8 ones;
+  {
+    const bf16 one = f2bf(1.f);
+    ones = bf16x8{one, one, one, one, one, one, one, one};
+  }
+  if constexpr (CS) {
+    asm volatile("" : "+v"(ones));
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(accb[jj]));
+  }
+  auto mma_cs = [&](const bf16x8 (&af)[8]) {
+    if constexpr (CS) {
+      if (!cs) return;
+      if (wc == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(accb[jj]) : "v"(ones), "v"(af[jj]));
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(accb[jj]) : "v"(ones), "v"(af[4 + jj]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 
   // one K-tile kt (P = its parity = image): MFMAs of both half-steps; between them the reads of half 1,
   // the DMA of K-tile kt + 2 into this image (past the last K-tile: the last one again, never read -- the
@@ -179,6 +213,7 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    mma_cs(a0);
     lgkm0();  // this wave's reads of K-tile kt are done
     bar();    // B1: every wave's are -- image p may be refilled
     // half 1: 64 MFMAs on a1 / b1; the DMA of K-tile kt + 2 between the first 32, the reads of K-tile kt + 1's
@@ -187,8 +222,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
     const unsigned soA = (unsigned)kn * kstepA, soB = (unsigned)kn * kstepB;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s < 8) bglds16(rsA, kt_off(voA[s], AT, s, kn), soA, lds0 + p * w4::IMG + (4 * s + wave) * 1024);
-      else bglds16(rsB, kt_off(voB[s - 8], BT, s - 8, kn), soB, lds0 + (2 + p) * w4::IMG + (4 * (s - 8) + wave) * 1024);
+      if (s < 8) bglds16_m0(rsA, kt_off(voA[s], AT, s, kn), soA, lds0 + p * w4::IMG + (4 * s + wave) * 1024);
+      else bglds16_m0(rsB, kt_off(voB[s - 8], BT, s - 8, kn), soB, lds0 + (2 + p) * w4::IMG + (4 * (s - 8) + wave) * 1024);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int idx = 2 * s + q, j = idx >> 3, i = idx & 7;
@@ -196,6 +231,7 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    mma_cs(a1);
     vm_wait<2 * w4::NP>();  // K-tile kt + 1 landed (this wave's pieces; kt + 2's stay in flight)
     bar();                  // B2: every wave's pieces of K-tile kt + 1 landed
 #pragma unroll
@@ -211,6 +247,13 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
     }
   };
 
+  // the zeroed accumulators pinned in AGPRs before the first MFMA (v_accvgpr_write -> MFMA SrcC needs
+  // wait states the compiler cannot know to insert for an asm MFMA; the prologue's DMA issue and waits
+  // below give far more)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
   // ---- prologue: K-tiles 0 and 1 in flight, K-tile 0's half-0 fragments in registers ----
   dma(0, 0);
   dma(1, 1);
@@ -226,11 +269,36 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
   for (int kt = 0; kt < nk; kt += 2) {
     ktile(kt, std::integral_constant<int, 0>{});
     ktile(kt + 1, std::integral_constant<int, 1>{});
+    // wait states behind the pair's last MFMAs: at the loop exit the register allocator may copy an
+    // accumulator (v_accvgpr_read / _mov) before any statement of ours runs, and it does not know the asm
+    // statements are MFMAs (24 cycles per 4096 MFMA cycles)
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
   }
   vm_wait<0>();  // the never-read reloads of the last iterations land before the LDS is released
-  // the last MFMAs' results (in flight in the matrix pipe) before any v_accvgpr_read of the epilogue
+  // The last MFMAs' results are still in the matrix pipe: wait states before any v_accvgpr_read.  The
+  // compiler does not know the asm statements are MFMAs, so every accumulator is then passed through an
+  // empty asm ("+a") AFTER the nops -- volatile asm keeps its order, and the epilogue's reads depend on
+  // those outputs.  (Without it hipcc read the last-written accumulators right behind their MFMA: wrong
+  // sums in rows 240-255 of every tile, tests/test_gemm64_gpu.py.)
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  if constexpr (CS) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(accb[jj]));
+  }
 
+  if constexpr (CS) {  // (the four values of a lane's accb are equal: every B "row" is all ones)
+    if (cs && (lane >> 4) == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int m = m0 + wr * 128 + 16 * (4 * wc + jj) + lane;
+        if (m < g.M) g.db[m] = f2bf(accb[jj][0]);
+      }
+    }
+  }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment; rows / columns past M / N
   // (clamped duplicates) are not stored ----
   if constexpr (STG) {  // (the host takes this form only for one bf16 output: no c32, no GELU dual store)
@@ -285,11 +353,75 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t) {
 
 template <bool AT, bool BT, bool KT, bool STG>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(Args g) {
-  w4_body<AT, BT, KT, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
+  w4_body<AT, BT, KT, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n), lds);
+}
+
+
+// Grouped weight gradients (the contract of gemm_k64.hip's gemm_k64_group_kernel on the W4 pipeline):
+// dW_i = A_i^T B_i (A_i = dy [K][M_i], B_i = x [K][N_i]) for up to kGroupMax problems in one launch, the
+// tiles of all problems one XCD-remapped list; tile column 0 of a problem with db_i also sums its bias
+// gradient (the CS instantiation, chosen per workgroup by a uniform branch).
+template <bool KT>
+__global__ void __launch_bounds__(256, 1) gemm_w4_group_kernel(GroupArgs ga) {
+  // the problem's Args read in place from the kernel-argument segment (GroupArgs is the only argument,
+  // at offset 0): indexing the by-value struct with the runtime q made the compiler copy all 16 Args
+  const GroupArgs* gp = (const GroupArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int t = xcd_remap(blockIdx.x, gp->tile_start[gp->n]);
+  int q = 0;
+  while (q + 1 < gp->n && t >= gp->tile_start[q + 1]) ++q;
+  q = __builtin_amdgcn_readfirstlane(q);
+  const Args& g = gp->p[q];
+  const int tt = t - gp->tile_start[q];
+  // tile column 0 <=> (in_g / gh) == 0 in w4_body's grouped order
+  const int per_group = kGroupM * g.tiles_n, grp = tt / per_group, in_g = tt - grp * per_group;
+  const int gh = min(kGroupM, g.tiles_m - grp * kGroupM);
+  const bool cs = __builtin_amdgcn_readfirstlane(g.db != nullptr && in_g / gh == 0 ? 1 : 0) != 0;
+  __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
+  w4_body<true, true, KT, false, true>(g, tt, lds, cs);
 }
 
 }  // namespace k64
 }  // namespace dta
+
+hipError_t dta_gemm_w4_wgrad_group(int n, const void* const* a, const int64_t* lda, const void* const* b,
+                                   const int64_t* ldb, void* const* c, const int64_t* ldc, const int* M, const int* N,
+                                   const int* K, void* const* db, hipStream_t st) {
+  using namespace dta;
+  using namespace dta::k64;
+  if (n < 1 || n > kGroupMax) return hipErrorInvalidValue;
+  GroupArgs ga{};
+  ga.n = n;
+  int total = 0;
+  bool kt = false;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] % 8 || N[i] % 8 || K[i] % 8 || K[i] < 8) return hipErrorInvalidValue;
+    if (2 * ((int64_t)(K[i] - 1) * lda[i] + M[i]) >= 0x7fffffffLL || 2 * ((int64_t)(K[i] - 1) * ldb[i] + N[i]) >= 0x7fffffffLL)
+      return hipErrorInvalidValue;
+    Args& g = ga.p[i];
+    g.a = static_cast<const bf16*>(a[i]);
+    g.b = static_cast<const bf16*>(b[i]);
+    g.c = static_cast<bf16*>(c[i]);
+    g.lda = lda[i];
+    g.ldb = ldb[i];
+    g.ldc = ldc[i];
+    g.M = M[i];
+    g.N = N[i];
+    g.K = K[i];
+    g.tiles_m = (M[i] + 255) / 256;
+    g.tiles_n = (N[i] + 255) / 256;
+    g.alpha = 1.f;
+    g.epi = EPI_NONE;
+    g.db = static_cast<bf16*>(db[i]);
+    ga.tile_start[i] = total;
+    total += g.tiles_m * g.tiles_n;
+    kt = kt || K[i] % (2 * BK) != 0;
+  }
+  ga.tile_start[n] = total;
+  if (kt) hipLaunchKernelGGL(gemm_w4_group_kernel<true>, dim3(total), dim3(256), 0, st, ga);
+  else hipLaunchKernelGGL(gemm_w4_group_kernel<false>, dim3(total), dim3(256), 0, st, ga);
+  return hipGetLastError();
+}
 
 template <bool KT, bool STG>
 static void w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t st) {
