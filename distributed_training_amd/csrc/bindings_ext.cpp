@@ -33,8 +33,6 @@ struct LinStepArgs {
 }  // namespace dta
 
 hipError_t dta_linear_step(const dta::LinStepArgs*, hipStream_t);
-int dta_gemm_bf16_tile(int, int, int, int);
-int dta_gemm_group_max();
 int dta_gemm_k64_group_max();
 hipError_t dta_gemm_w4_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
                                    void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
@@ -42,11 +40,6 @@ hipError_t dta_gemm_w4_wgrad_group(int, const void* const*, const int64_t*, cons
 hipError_t dta_gemm_k64_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
                                     void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
                                     hipStream_t);
-hipError_t dta_gemm_wgrad_group(int, const void* const*, const int64_t*, const void* const*, const int64_t*,
-                                void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
-                                hipStream_t);
-hipError_t dta_gemm_bf16(const void*, int64_t, bool, const void*, int64_t, bool, void*, float*, int64_t, int, int, int,
-                         float, const void*, int, const void*, int64_t, int, hipStream_t);
 int dta_gemm_k64_tile(int, int, int, int);
 hipError_t dta_gemm_k64(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, void*, int64_t, float*,
                         int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t);
@@ -138,72 +131,16 @@ void linear_step(torch::Tensor X, torch::Tensor T, torch::Tensor ring, torch::Te
 
 bool aligned16(const torch::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
 
-// C[M, N] = alpha * op(A) op(B)^T (+ bias, act, + residual).  a: [M, K] (a_t: [K, M]); b: [N, K] (b_t: [K, N]);
-// both bf16 with unit inner stride, row strides multiples of 8 elements.
-torch::Tensor gemm_bf16(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t, c10::optional<torch::Tensor> out,
-                        bool out_f32, double alpha, c10::optional<torch::Tensor> bias, int64_t act,
-                        c10::optional<torch::Tensor> residual, int64_t tile, int64_t stream) {
-  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm: GPU tensors");
-  TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm: bf16 operands");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, unit inner stride");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && aligned16(a) && aligned16(b),
-              "gemm: row strides multiples of 8 elements, 16-byte aligned bases");
-  const int64_t M = a_t ? a.size(1) : a.size(0), K = a_t ? a.size(0) : a.size(1);
-  const int64_t N = b_t ? b.size(1) : b.size(0), Kb = b_t ? b.size(0) : b.size(1);
-  TORCH_CHECK(K == Kb, "gemm: inner dimensions differ");
-  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm: dims too large");
-  TORCH_CHECK(dta_gemm_bf16_tile((int)M, (int)N, (int)K, (int)tile) != 0,
-              "gemm: shape not covered (M, N multiples of the tile, K a multiple of 32)");
-  // act 16: GELU backward epilogue, C = (alpha op(A) op(B)^T) * gelu_tanh'(residual) (the residual operand
-  // is the activation's input; nothing is added)
-  TORCH_CHECK(act == 0 || act == 2 || act == 16, "gemm: act 0 (none), 2 (gelu_tanh) or 16 (x gelu_tanh'(residual))");
-  TORCH_CHECK(act != 16 || (residual && residual->defined() && !(bias && bias->defined())),
-              "gemm: act 16 needs the residual operand (the GELU input) and no bias");
-  torch::Tensor c;
-  if (out && out->defined()) {
-    c = *out;
-    TORCH_CHECK(c.is_cuda() && c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 &&
-                    c.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0,
-                "gemm: out must be [M, N], unit inner stride, 16-byte aligned rows");
-    TORCH_CHECK(c.scalar_type() == (out_f32 ? torch::kFloat32 : torch::kBFloat16), "gemm: out dtype");
-  } else {
-    c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
-  }
-  const void* bp = nullptr;
-  if (bias && bias->defined()) {
-    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == torch::kBFloat16 && bias->is_contiguous() &&
-                    bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
-                "gemm: bias bf16 [N]");
-    bp = bias->data_ptr();
-  }
-  const void* rp = nullptr;
-  int64_t ldr = 0;
-  if (residual && residual->defined()) {
-    TORCH_CHECK(!out_f32, "gemm: residual with bf16 output only");
-    TORCH_CHECK(residual->is_cuda() && residual->scalar_type() == torch::kBFloat16 && residual->dim() == 2 &&
-                    residual->size(0) == M && residual->size(1) == N && residual->stride(1) == 1 &&
-                    residual->stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(residual->data_ptr()) % 8 == 0,
-                "gemm: residual bf16 [M, N]");
-    rp = residual->data_ptr();
-    ldr = residual->stride(0);
-  }
-  ok(dta_gemm_bf16(a.data_ptr(), a.stride(0), a_t, b.data_ptr(), b.stride(0), b_t, out_f32 ? nullptr : c.data_ptr(),
-                   out_f32 ? c.data_ptr<float>() : nullptr, c.stride(0), (int)M, (int)N, (int)K, (float)alpha, bp,
-                   (int)act, rp, ldr, (int)tile, stream_of(stream)),
-     "gemm_bf16");
-  return c;
-}
-
 // Grouped weight (+ bias) gradients: dW_i = A_i^T B_i into c_i, db_i = column sums of A_i
 // (A_i = dy [K, M_i], B_i = x [K, N_i], c_i [M_i, N_i] bf16; db_i bf16 [M_i] or None).
-// impl (``k64``): 1 = csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; K multiples of 64), 2 =
-// csrc/gemm_w4.hip's (4-wave intra-wave interleave; M, N, K multiples of 8), 0 = csrc/gemm_bf16.hip's
-// (32-deep stages).
+// impl: 1 = csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; M, N multiples of 256, K of 64),
+// 2 = csrc/gemm_w4.hip's (4-wave intra-wave interleave; M, N, K multiples of 8; no bias gradients).
 void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b, std::vector<torch::Tensor> c,
                       std::vector<c10::optional<torch::Tensor>> db, int64_t stream, int64_t impl) {
   const int n = (int)a.size();
-  const bool k64 = impl != 0, w4 = impl == 2;
-  const int gmax = k64 ? dta_gemm_k64_group_max() : dta_gemm_group_max();
+  TORCH_CHECK(impl == 1 || impl == 2, "gemm_wgrad_group: impl 1 (k64) or 2 (w4)");
+  const bool w4 = impl == 2;
+  const int gmax = dta_gemm_k64_group_max();
   TORCH_CHECK(n >= 1 && n <= gmax && (int)b.size() == n && (int)c.size() == n && (int)db.size() == n,
               "gemm_wgrad_group: 1..", gmax, " problems, equal list lengths");
   std::vector<const void*> ap(n), bp(n);
@@ -225,9 +162,9 @@ void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b
                       A.size(0) < (1 << 30),
                   "gemm_wgrad_group (w4): M, N, K multiples of 8");
     } else {
-      TORCH_CHECK(A.size(1) % 256 == 0 && B.size(1) % 256 == 0 && A.size(0) % (k64 ? 64 : 32) == 0 &&
-                      A.size(0) > 0 && A.size(0) < (1 << 30),
-                  "gemm_wgrad_group: M, N multiples of 256, K a multiple of 32 (64 for k64)");
+      TORCH_CHECK(A.size(1) % 256 == 0 && B.size(1) % 256 == 0 && A.size(0) % 64 == 0 && A.size(0) > 0 &&
+                      A.size(0) < (1 << 30),
+                  "gemm_wgrad_group (k64): M, N multiples of 256, K a multiple of 64");
     }
     ap[i] = A.data_ptr();
     bp[i] = B.data_ptr();
@@ -240,13 +177,14 @@ void gemm_wgrad_group(std::vector<torch::Tensor> a, std::vector<torch::Tensor> b
     K[i] = (int)A.size(0);
     dp[i] = nullptr;
     if (db[i] && db[i]->defined()) {
+      TORCH_CHECK(!w4, "gemm_wgrad_group (w4): no bias gradients (use the k64 group)");
       const auto& d = *db[i];
       TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kBFloat16 && d.is_contiguous() && d.numel() == M[i],
                   "gemm_wgrad_group: db bf16 [M]");
       dp[i] = d.data_ptr();
     }
   }
-  ok((w4 ? dta_gemm_w4_wgrad_group : k64 ? dta_gemm_k64_wgrad_group : dta_gemm_wgrad_group)(
+  ok((w4 ? dta_gemm_w4_wgrad_group : dta_gemm_k64_wgrad_group)(
          n, ap.data(), lda.data(), bp.data(), ldb.data(), cp.data(),
                                                              ldc.data(), M.data(), N.data(), K.data(), dp.data(),
                                                              stream_of(stream)),
@@ -329,20 +267,14 @@ void dta_register_ext(pybind11::module_& m) {
         py::arg("loss_ring"), py::arg("loss_cursor"), py::arg("nsteps"), py::arg("loss_kind"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("grad_scale"), py::arg("nesterov"),
         py::arg("maximize"), py::arg("stream") = -1);
-  m.def("gemm", &gemm_bf16, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
-        py::arg("out") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0, py::arg("bias") = py::none(),
-        py::arg("act") = 0, py::arg("residual") = py::none(), py::arg("tile") = 0, py::arg("stream") = -1);
   m.def("gemm_wgrad_group", &gemm_wgrad_group, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("db"),
-        py::arg("stream") = -1, py::arg("k64") = false);
+        py::arg("stream") = -1, py::arg("impl") = 1);
   m.def("gemm64_group_max", &dta_gemm_k64_group_max);
   m.def("gemm64", &gemm_k64, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
         py::arg("out") = py::none(), py::arg("out2") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("res") = py::none(), py::arg("tile") = 0,
         py::arg("stream") = -1);
   m.def("gemm64_tile", [](int M, int N, int K, int tile) { return dta_gemm_k64_tile(M, N, K, tile); },
-        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
-  m.def("gemm_group_max", &dta_gemm_group_max);
-  m.def("gemm_tile", [](int M, int N, int K, int tile) { return dta_gemm_bf16_tile(M, N, K, tile); },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
   m.def("linear_step_supported", [](int I, int C, int B, bool mom) { return dta_linear_step_supported(I, C, B, mom) != 0; });
 }

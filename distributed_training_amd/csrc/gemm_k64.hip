@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
   k64_body<BM, BN, WC, AT, BT, PH, BUF, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
-// Grouped weight gradients (csrc/gemm_bf16.hip gemm_group_kernel's contract on this kernel's 64-deep
+// Grouped weight gradients (on this kernel's 64-deep
 // two-phase loop): dW_i = A_i^T B_i for several problems in ONE launch of 256 x 256 tiles over the
 // full token reduction, the bias gradients from the same MFMA pipe (CS); the tiles of all problems
 // form one list, XCD-remapped so each XCD takes a contiguous run.

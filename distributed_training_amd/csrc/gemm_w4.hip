@@ -52,12 +52,8 @@ __device__ __forceinline__ bf16x4 w4_tr4(const char* lds, int byte_off) {
 // KT: K is not a multiple of 128 (two K-tiles): the loop runs over ceil(K / 128) pairs and every DMA
 // lane whose 8 k-values lie at or past K gets an out-of-range buffer offset -- the buffer unit returns
 // zeros for it, so the tail contributes nothing (K a multiple of 8: chunks are whole).
-// CS: the kernel may also sum the bias gradient db[m] = sum_k A(m, k) (weight gradients; done where the
-// uniform flag `cs` is set: tile column 0 of a problem with db): MFMAs of A's fragments against an all-ones
-// B fragment, the two waves sharing A rows taking four fragments each (+4 MFMAs per half-step per wave;
-// VGPR accumulators: the AGPR file is full)
-template <bool AT, bool BT, bool KT, bool STG, bool CS = false>
-__device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, const bool cs = false) {
+template <bool AT, bool BT, bool KT, bool STG>
+__device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -163,38 +159,6 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, c
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a0[8], b0[8], a1[8], b1[8];  // half-step 0 / 1 fragments: A rows (j), B rows (i)
-  f32x4 accb[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                   f32x4{0.f, 0.f, 0.f, 0.f}};
-  // (the all-ones fragment and the zeroed accb are made opaque once, here: a constant the compiler
-  // re-materialises with a VALU write right before an asm MFMA that reads it is an unguarded VALU -> MFMA
-  // hazard; the fragment index 4 wc + jj goes through a uniform branch for the same reason -- a runtime
-  // register-array index becomes v_cndmask selects right before the MFMA)
-  bf16x8 ones;
-  {
-    const bf16 one = f2bf(1.f);
-    ones = bf16x8{one, one, one, one, one, one, one, one};
-  }
-  if constexpr (CS) {
-    asm volatile("" : "+v"(ones));
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(accb[jj]));
-  }
-  auto mma_cs = [&](const bf16x8 (&af)[8]) {
-    if constexpr (CS) {
-      if (!cs) return;
-      if (wc == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(accb[jj]) : "v"(ones), "v"(af[jj]));
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(accb[jj]) : "v"(ones), "v"(af[4 + jj]));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
   // one K-tile kt (P = its parity = image): MFMAs of both half-steps; between them the reads of half 1,
   // the DMA of K-tile kt + 2 into this image (past the last K-tile: the last one again, never read -- the
   // wait counts stay static) and the reads of K-tile kt + 1's half 0 (after the last K-tile: that
@@ -213,7 +177,6 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, c
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    mma_cs(a0);
     lgkm0();  // this wave's reads of K-tile kt are done
     bar();    // B1: every wave's are -- image p may be refilled
     // half 1: 64 MFMAs on a1 / b1; the DMA of K-tile kt + 2 between the first 32, the reads of K-tile kt + 1's
@@ -231,7 +194,6 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, c
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    mma_cs(a1);
     vm_wait<2 * w4::NP>();  // K-tile kt + 1 landed (this wave's pieces; kt + 2's stay in flight)
     bar();                  // B2: every wave's pieces of K-tile kt + 1 landed
 #pragma unroll
@@ -285,20 +247,6 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds, c
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  if constexpr (CS) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) asm volatile("" : "+v"(accb[jj]));
-  }
-
-  if constexpr (CS) {  // (the four values of a lane's accb are equal: every B "row" is all ones)
-    if (cs && (lane >> 4) == 0) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int m = m0 + wr * 128 + 16 * (4 * wc + jj) + lane;
-        if (m < g.M) g.db[m] = f2bf(accb[jj][0]);
-      }
-    }
-  }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment; rows / columns past M / N
   // (clamped duplicates) are not stored ----
   if constexpr (STG) {  // (the host takes this form only for one bf16 output: no c32, no GELU dual store)
@@ -358,10 +306,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(Args g) {
 }
 
 
-// Grouped weight gradients (the contract of gemm_k64.hip's gemm_k64_group_kernel on the W4 pipeline):
-// dW_i = A_i^T B_i (A_i = dy [K][M_i], B_i = x [K][N_i]) for up to kGroupMax problems in one launch, the
-// tiles of all problems one XCD-remapped list; tile column 0 of a problem with db_i also sums its bias
-// gradient (the CS instantiation, chosen per workgroup by a uniform branch).
+// Grouped weight gradients (the contract of gemm_k64.hip's gemm_k64_group_kernel on the W4 pipeline, minus
+// the bias gradient): dW_i = A_i^T B_i (A_i = dy [K][M_i], B_i = x [K][N_i]) for up to kGroupMax problems in
+// one launch, the tiles of all problems one XCD-remapped list, LDS-staged stores.  Problems with a bias
+// gradient go to the k64 group (ops/lm.py): W4 is chosen for the big bias-free Llama projections, and the
+// extra db MFMAs pushed this kernel past the register file (the AGPRs hold the 256 accumulators).
 template <bool KT>
 __global__ void __launch_bounds__(256, 1) gemm_w4_group_kernel(GroupArgs ga) {
   // the problem's Args read in place from the kernel-argument segment (GroupArgs is the only argument,
@@ -371,14 +320,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_group_kernel(GroupArgs ga) {
   int q = 0;
   while (q + 1 < gp->n && t >= gp->tile_start[q + 1]) ++q;
   q = __builtin_amdgcn_readfirstlane(q);
-  const Args& g = gp->p[q];
-  const int tt = t - gp->tile_start[q];
-  // tile column 0 <=> (in_g / gh) == 0 in w4_body's grouped order
-  const int per_group = kGroupM * g.tiles_n, grp = tt / per_group, in_g = tt - grp * per_group;
-  const int gh = min(kGroupM, g.tiles_m - grp * kGroupM);
-  const bool cs = __builtin_amdgcn_readfirstlane(g.db != nullptr && in_g / gh == 0 ? 1 : 0) != 0;
   __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
-  w4_body<true, true, KT, false, true>(g, tt, lds, cs);
+  w4_body<true, true, KT, true>(gp->p[q], t - gp->tile_start[q], lds);
 }
 
 }  // namespace k64
@@ -395,7 +338,7 @@ hipError_t dta_gemm_w4_wgrad_group(int n, const void* const* a, const int64_t* l
   int total = 0;
   bool kt = false;
   for (int i = 0; i < n; ++i) {
-    if (M[i] % 8 || N[i] % 8 || K[i] % 8 || K[i] < 8) return hipErrorInvalidValue;
+    if (M[i] % 8 || N[i] % 8 || K[i] % 8 || K[i] < 8 || db[i] != nullptr) return hipErrorInvalidValue;
     if (2 * ((int64_t)(K[i] - 1) * lda[i] + M[i]) >= 0x7fffffffLL || 2 * ((int64_t)(K[i] - 1) * ldb[i] + N[i]) >= 0x7fffffffLL)
       return hipErrorInvalidValue;
     Args& g = ga.p[i];
@@ -412,7 +355,6 @@ hipError_t dta_gemm_w4_wgrad_group(int n, const void* const* a, const int64_t* l
     g.tiles_n = (N[i] + 255) / 256;
     g.alpha = 1.f;
     g.epi = EPI_NONE;
-    g.db = static_cast<bf16*>(db[i]);
     ga.tile_start[i] = total;
     total += g.tiles_m * g.tiles_n;
     kt = kt || K[i] % (2 * BK) != 0;

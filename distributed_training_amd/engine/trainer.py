@@ -254,6 +254,8 @@ class Trainer:
                 g = GraphedStep(self._run_batch_eager, [source.clone(), targets.clone()], warmup=1,
                                 engine=self.model)
                 self._graphed = g if g.ok else False
+                if g.ok:
+                    logger.info("step graph: the whole training step is replayed as one hipGraph")
                 return g.warmup_losses[-1]
             if all(s.shape == x.shape and s.dtype == x.dtype for s, x in zip(g.static, (source, targets))):
                 return g(source, targets)

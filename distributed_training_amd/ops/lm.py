@@ -7,10 +7,10 @@ tensors use the equivalent PyTorch math, which is also the numerics reference
 of the GPU tests.
 
 Projection GEMMs (forward x W^T + b, input gradient dy W, weight gradient
-dy^T x, the LM head) go through :func:`gemm`: the gfx950 GEMM of
-``csrc/gemm_bf16.hip`` (bias / scale fused in its epilogue) or hipBLASLt,
-whichever measured faster for that shape on this GPU (timed once per shape
-and process, ``DTA_GEMM=auto``; ``dta`` / ``torch`` force one).  Weight
+dy^T x, the LM head) go through :func:`gemm`: the gfx950 GEMMs of
+``csrc/gemm_k64.hip`` / ``csrc/gemm_w4.hip`` (bias / scale / GELU / residual fused
+in their epilogues) or hipBLASLt, whichever measured faster for that shape on this
+GPU (timed once per shape and process, ``DTA_GEMM=auto``; ``dta`` / ``torch`` force one).  Weight
 gradients with small outputs keep the split-K kernel of ``csrc/gemm.hip``.
 """
 from __future__ import annotations
@@ -291,8 +291,8 @@ def _save_cache() -> None:
         pass
 
 
-# implementation ids in _GEMM_CHOICE: 0 = hipBLASLt (torch), 1..3 = csrc/gemm_bf16.hip tile (round-2
-# kernel, 32-deep stages; kept for K % 64 != 0), 10 + t = csrc/gemm_k64.hip tile t (64-deep stages)
+# implementation ids in _GEMM_CHOICE: 0 = hipBLASLt (torch), 10 + t = csrc/gemm_k64.hip tile t (64-deep
+# stages; tiles 9 / 10 = csrc/gemm_w4.hip, which also covers K % 64 != 0 -- the round-2 kernel that did is gone)
 K64 = 10
 # csrc/gemm_k64.hip tiles the dispatcher times: 5 / 6 / 8 = the 8-wave 256x256 / 256x128 / 128x256
 # tiles with the two-phase K loop (3-11 % faster than their four-phase forms 1 / 2 / 4 at every
@@ -303,18 +303,10 @@ K64_TILES = (9, 5, 6, 3, 7, 8)  # 9: csrc/gemm_w4.hip (4 waves, 256 x 256, intra
 _PREFER_DTA = 1.0
 
 
-def _k64_on() -> bool:
-    """``DTA_GEMM_K64=0``: leave csrc/gemm_k64.hip out of the candidates (A/B against round 2)."""
-    return os.environ.get("DTA_GEMM_K64", "1") != "0"
-
-
 def gemm_candidates(M: int, N: int, K: int) -> list:
     """Hand-written GEMM implementations that cover an M x N x K problem (ids as in _GEMM_CHOICE)."""
     C = native()
-    k64 = [K64 + t for t in K64_TILES if _k64_on() and C.gemm64_tile(M, N, K, t)]
-    if k64:
-        return k64
-    return [t for t in (1, 2, 3) if C.gemm_tile(M, N, K, t)]
+    return [K64 + t for t in K64_TILES if C.gemm64_tile(M, N, K, t)]
 
 
 def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]]) -> int:
@@ -333,7 +325,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
     if mode == "torch" or not dta:
         c = 0
     elif mode == "dta" or torch.cuda.is_current_stream_capturing():
-        c = max(dta)  # (k64 ids sort after the round-2 tiles; the k64 auto tile is listed first below)
+        c = dta[0]
         auto = native().gemm64_tile(M, N, K, 0)
         if K64 + auto in dta:
             c = K64 + auto
@@ -349,10 +341,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
 
 def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
               alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    C = native()
-    if impl >= K64:
-        return C.gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
-    return C.gemm(a, b, a_t, b_t, out, False, alpha, bias, 0, None, impl)
+    return native().gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
 
 
 def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -544,7 +533,7 @@ def _queue_end_join() -> None:
 # are queued, and once the queue holds >= DTA_WGRAD_GROUP 256 x 256 output tiles (default
 # 200: two GPT-2 layers = 216 tiles) ONE grouped launch computes all of them over the full
 # token reduction -- no split, no slabs, bias gradients from the same MFMA pipe
-# (csrc/gemm_bf16.hip gemm_group_kernel).  The queue is flushed before every DDP bucket
+# (csrc/gemm_k64.hip gemm_k64_group_kernel).  The queue is flushed before every DDP bucket
 # launch and at the end of the backward (same stream: no further synchronisation); under the
 # FSDP engine (unit pieces, ``_dta_defer_ok``) a unit's reduce-scatter waits for the flush that
 # writes its pieces (parallel/fsdp.py ``_launch_waiting``).
@@ -566,21 +555,21 @@ def _group_threshold() -> int:
 
 
 def wgrad_flush() -> None:
-    """Launch the queued weight gradients (grouped, at most gemm_group_max() per launch)."""
+    """Launch the queued weight gradients (grouped, at most gemm64_group_max() per launch)."""
     if not _DEFER:
         return
     items = list(_DEFER)
     _DEFER.clear()
     _DEFER_TILES[0] = 0
     C = native()
-    # csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop) when every reduction is a multiple of
-    # 64 tokens (DTA_WGRAD_GROUP_K64=0: the round-2 kernel), else csrc/gemm_bf16.hip's
-    k64 = os.environ.get("DTA_WGRAD_GROUP_K64", "1") != "0" and all(it[0].shape[0] % 64 == 0 for it in items)
-    gmax = C.gemm64_group_max() if k64 else C.gemm_group_max()
+    # csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; every queued reduction is a multiple of
+    # 64 tokens, _weight_grad).  csrc/gemm_w4.hip's grouped kernel (impl 2) measured slower on every
+    # weight-gradient shape (profiles/gemm_w4_vs_k64_hipblaslt.txt) and has no bias gradients.
+    gmax = C.gemm64_group_max()
     for i in range(0, len(items), gmax):
         part = items[i:i + gmax]
         C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
-                           [it[3] for it in part], -1, k64)
+                           [it[3] for it in part], -1, 1)
     GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
     for fn in list(FLUSH_LISTENERS):
         fn()
@@ -606,7 +595,7 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
         thr = _group_threshold()
         if thr and cw is not None and (cb is not None or not with_bias) \
                 and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
-                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and K % 32 == 0 and cw.stride(0) % 8 == 0 \
+                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and cw.stride(0) % 8 == 0 \
                 and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
             # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
             # holds ALIASES of the slices, never the tensors returned to autograd: a second
@@ -618,7 +607,7 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             _DEFER_TILES[0] += (M // 256) * (N // 256)
             GEMM_STATS["deferred_wgrad"] += 1
             _queue_end_join()
-            if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm_group_max():
+            if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm64_group_max():
                 wgrad_flush()
             return (cw, cb) if with_bias else cw
         if with_bias:
@@ -675,10 +664,8 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and h2.is_contiguous()
           and h2.data_ptr() % 16 == 0 and N % 8 == 0)
 
-    def run(impl: Any) -> torch.Tensor:
-        if impl >= K64:
-            return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
-        return C.gemm(dy2, w, False, True, None, False, 1.0, None, 16, h2, impl)
+    def run(impl: int) -> torch.Tensor:
+        return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
 
     def run_torch() -> torch.Tensor:
         return C.gelu_bwd(torch.mm(dy2, w), h2, -1)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""csrc/gemm_k64.hip (64-deep stages, phase-interleaved half-tile DMA) vs the round-2
-kernel (csrc/gemm_bf16.hip) vs torch (hipBLASLt) on the GPT-2 small / Llama-3 8B
+"""csrc/gemm_k64.hip (64-deep stages, phase-interleaved half-tile DMA; tiles 9 / 10 = csrc/gemm_w4.hip)
+vs torch (hipBLASLt) on the GPT-2 small / Llama-3 8B
 projection shapes -- forward (x W^T), input gradient (dy W), weight gradient
 (dy^T x) -- plus the FUSED costs the dispatcher compares: c_fc forward with the
 GELU dual store vs hipBLASLt + gelu_fwd, and the GELU-backward dgrad vs hipBLASLt +
@@ -62,23 +62,15 @@ def main():
             bias = (torch.randn(nout, device="cuda") * 0.1).bfloat16()
             fl = 2.0 * T * nout * nin
             cases = {
-                "fwd": ((T, nout, nin), lambda: F.linear(x, w),
-                        lambda t: C.gemm(x, w, tile=t), lambda t: C.gemm64(x, w, tile=t)[0], False, False),
-                "dgrad": ((T, nin, nout), lambda: torch.mm(dy, w),
-                          lambda t: C.gemm(dy, w, False, True, tile=t),
-                          lambda t: C.gemm64(dy, w, False, True, tile=t)[0], False, True),
-                "wgrad": ((nout, nin, T), lambda: torch.mm(dy.t(), x),
-                          lambda t: C.gemm(dy, x, True, True, tile=t),
-                          lambda t: C.gemm64(dy, x, True, True, tile=t)[0], True, True),
+                "fwd": ((T, nout, nin), lambda: F.linear(x, w), lambda t: C.gemm64(x, w, tile=t)[0]),
+                "dgrad": ((T, nin, nout), lambda: torch.mm(dy, w), lambda t: C.gemm64(dy, w, False, True, tile=t)[0]),
+                "wgrad": ((nout, nin, T), lambda: torch.mm(dy.t(), x), lambda t: C.gemm64(dy, x, True, True, tile=t)[0]),
             }
-            for kind, ((M, N, K), tfn, old, new, _, _) in cases.items():
+            for kind, ((M, N, K), tfn, new) in cases.items():
                 ref = tfn()
                 fns = {"torch": tfn}
-                old_t = C.gemm_tile(M, N, K, 0)
-                if old_t:
-                    fns[f"r2_t{old_t}"] = (lambda t=old_t: old(t))
                 errs = {}
-                for t in range(1, 9):  # 5-8: tiles 1-4 with the two-phase K loop
+                for t in range(1, 11):  # 5-8: tiles 1-4 with the two-phase K loop; 9 / 10: csrc/gemm_w4.hip
                     if C.gemm64_tile(M, N, K, t):
                         fns[f"k64_t{t}"] = (lambda t=t: new(t))
                         errs[f"k64_t{t}"] = float(f"{relerr(new(t), ref):.2e}")
@@ -110,8 +102,7 @@ def main():
                                   "us": {k: round(v, 1) for k, v in times.items()}}), flush=True)
                 w2 = (torch.randn(nin, nout, device="cuda") * 0.02).bfloat16()  # c_proj weight [768, 3072]
                 dy2 = torch.randn(T, nin, device="cuda").bfloat16()
-                fns = {"torch+gelu_bwd": lambda: C.gelu_bwd(torch.mm(dy2, w2), h, -1),
-                       "r2_dgelu": lambda: C.gemm(dy2, w2, False, True, None, False, 1.0, None, 16, h, 0)}
+                fns = {"torch+gelu_bwd": lambda: C.gelu_bwd(torch.mm(dy2, w2), h, -1)}
                 for t in range(1, 9):
                     if C.gemm64_tile(T, nout, nin, t):
                         fns[f"k64_t{t}_dgelu"] = (lambda t=t: C.gemm64(dy2, w2, False, True, epi=16, res=h, tile=t))

@@ -3,7 +3,7 @@
 
     python scripts/gemm_one.py M N K [layout] [impls]
 layout: nt (forward x W^T), nn (dgrad dy W), tn (wgrad dy^T x); impls: comma list of
-torch, r2 (csrc/gemm_bf16.hip, auto tile), k64 (csrc/gemm_k64.hip auto tile) or k64tN."""
+torch, k64 (csrc/gemm_k64.hip auto tile) or k64tN (tiles 9 / 10: csrc/gemm_w4.hip)."""
 import sys
 from pathlib import Path
 
@@ -24,8 +24,6 @@ C = native()
 def run(impl):
     if impl == "torch":
         return (a.t() if a_t else a) @ (b if b_t else b.t())
-    if impl == "r2":
-        return C.gemm(a, b, a_t, b_t)
     tile = int(impl[4:]) if impl.startswith("k64t") else 0
     return C.gemm64(a, b, a_t, b_t, tile=tile)[0]
 

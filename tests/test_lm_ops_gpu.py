@@ -522,18 +522,18 @@ def test_ddp_deferred_after_raised_backward(monkeypatch):
             assert _rel(p.grad, rp[name].grad) < 2e-2, (it, name)
 
 
-@pytest.mark.parametrize("k64", [0, 1, 2])
-def test_gemm_wgrad_group_vs_fp32(k64):
-    """The grouped weight-gradient launch (256 x 256 tiles, full token reduction, bias gradient
-    on the MFMA pipe) on problems of different shapes and K, strided operands, vs fp32 torch --
-    the round-2 kernel (32-deep stages, K multiples of 32) and csrc/gemm_k64.hip's (64-deep
-    two-phase loop; the bias columns split over the waves sharing A rows)."""
+@pytest.mark.parametrize("impl", [1, 2])
+def test_gemm_wgrad_group_vs_fp32(impl):
+    """The grouped weight-gradient launch (full token reduction, several problems' tiles in one
+    launch) on problems of different shapes and K, strided operands, vs fp32 torch: csrc/gemm_k64.hip's
+    (impl 1: 256 x 256 tiles, bias gradients on the MFMA pipe split over the waves sharing A rows) and
+    csrc/gemm_w4.hip's (impl 2: edge tiles and K tails, no bias gradients -- refused)."""
     from distributed_training_amd.ops import native
 
     torch.manual_seed(12)
-    shapes = [(1024, 512, 256), (2048, 256, 768), (512, 768, 512), (96 if not k64 else 192, 256, 256),
+    shapes = [(1024, 512, 256), (2048, 256, 768), (512, 768, 512), (192, 256, 256),
               (8192, 768, 768)]  # (K, M, N)
-    if k64 == 2:  # W4: edge tiles and K tails too
+    if impl == 2:  # W4: edge tiles and K tails too
         shapes += [(520, 264, 776), (136, 1000, 200)]
     A, B, Cs, D = [], [], [], []
     for K, M, N in shapes:
@@ -543,7 +543,11 @@ def test_gemm_wgrad_group_vs_fp32(k64):
         Cs.append(torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
         D.append(torch.empty(M, device=DEV, dtype=torch.bfloat16))
     D[1] = None  # a problem without bias
-    native().gemm_wgrad_group(A, B, Cs, D, -1, k64)
+    if impl == 2:  # W4: no bias gradients (refused), the products alone
+        with pytest.raises(RuntimeError, match="no bias gradients"):
+            native().gemm_wgrad_group(A, B, Cs, D, -1, impl)
+        D = [None] * len(shapes)
+    native().gemm_wgrad_group(A, B, Cs, D, -1, impl)
     for i in range(len(shapes)):
         assert _rel(Cs[i], A[i].float().t() @ B[i].float()) < 1e-2, i
         if D[i] is not None:
