@@ -971,10 +971,6 @@ static dta::MlpPArgs make_mlp_pargs(torch::Tensor Xp, torch::Tensor T, torch::Te
   a.weight_decay = (float)wd;
   a.nesterov = nesterov;
   a.maximize = maximize;
-  {
-    const char* e = std::getenv("DTA_MLP_SETPRIO");
-    a.prio_young = e ? std::atoi(e) : 0;
-  }
   // xinfo (DDP exchange, empty for one rank): world, rank, slot_elems, local_ll, xerr, xepoch,
   // timeout_iters, xmode, LL elements per rank buffer, peer_ll[0..world)
   a.world = 1;

@@ -450,8 +450,7 @@ int dta_linear_step_supported(int I, int C, int B, int momentum) {
 hipError_t dta_linear_step(const LinStepArgs* a, hipStream_t st) {
   if (!dta_linear_step_supported(a->I, a->C, a->B, a->M != nullptr) || a->nsteps < 0 || a->R < 1)
     return hipErrorInvalidValue;
-  static const bool wave_off = getenv("DTA_LINEAR_WAVE") && getenv("DTA_LINEAR_WAVE")[0] == '0';
-  if (!wave_off && a->I <= kWI && a->I % 4 == 0 && a->C <= kWC && a->B <= 64 &&
+  if (a->I <= kWI && a->I % 4 == 0 && a->C <= kWC && a->B <= 64 &&
       reinterpret_cast<uintptr_t>(a->X) % 16 == 0) {  // the reference's own shapes
     hipLaunchKernelGGL(linear_step_wave_kernel, dim3(1), dim3(64), 0, st, *a);
     return hipGetLastError();

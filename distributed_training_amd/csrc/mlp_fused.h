@@ -58,7 +58,6 @@ struct MlpPArgs {
   int nesterov, maximize;
   unsigned long long* dbg;  // diagnostic s_memtime stamps [waves][8] of one step (nullptr = off)
   int dbg_step;
-  int prio_young;           // 1: waves 4-7 (the younger half, losers of VALU arbitration) run at s_setprio 1
   // DDP across ranks (world > 1): per-step gradient exchange through the LL
   // slots of a dedicated p2p buffer set (csrc/p2p_allreduce.hip)
   int rank, world;

@@ -84,18 +84,6 @@ __device__ __forceinline__ void lds_barrier() {
     }                                                                                       \
   } while (0)
 
-// per-step phase stamps: only in a build with -DDTA_MP_PHASES (scripts/headline_clock.py
-// phases); the default build keeps their compares and branches out of the step loop
-#ifdef DTA_MP_PHASES
-#define MP_STAMP(k)                                                                             \
-  do {                                                                                          \
-    if (a.dbg && s == a.dbg_step && lane == 0) a.dbg[wave * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define MP_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
 
 // Activation image [32 samples][IMG]: 8-byte granules XOR-swizzled by row so
 // the per-lane column writes (32 lanes = 32 rows of one granule column) spread
@@ -583,9 +571,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   }
   const float lscale = (a.loss_type == LOSS_MSE) ? 1.f / (float)(B * OUT) : 1.f / (float)B;
 
-  // static priority for the younger half of the workgroup (MI355X_MICROARCH "Two waves per
-  // SIMD" item 4): one s_setprio before the loop, wave-uniform guard, no per-phase flips
-  if (a.prio_young && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   float dy_keep[OUT], loss_keep = 0.f;  // one rank: wave 0's dY / loss, finished after its backward
   float mb2[OUT];                       // one rank: the output bias' momenta (wave 0, lane 0)
 #pragma unroll
@@ -595,7 +580,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
   for (int s = 0; s < a.nsteps; ++s) {
     const int cb = s & 1;
     const bf16* Xb = Xs + cb * 32 * kMpXs;
-    MP_STAMP(0);
     // prefetch: features of step s+1, index of step s+2
     if (gthr && s + 1 < a.nsteps) {
       load_rows(idx_next);
@@ -638,9 +622,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
       yp[o] += __shfl_xor(yp[o], 32, kWave);
       if (hh == 0) Ypart[(wave * OUT + o) * 32 + r32] = yp[o];
     }
-    MP_STAMP(1);
     lds_barrier();  // ---------------- barrier 1
-    MP_STAMP(2);
     // ================= loss, dY, b2 (wave 0); next batch tile (staging threads) =================
     if (wave == 0) {
       const int r = r32;
@@ -718,9 +700,7 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
       }
     }
     if (gthr && s + 1 < a.nsteps) store_rows(cb ^ 1);
-    MP_STAMP(3);
     lds_barrier();  // ---------------- barrier 2
-    MP_STAMP(4);
     // ================= backward + SGD (own tiles) =================
     SgdH hs = hbase;
     hs.first = first;
@@ -789,7 +769,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) =
               pk4_bf16(dh[4 * g], dh[4 * g + 1], dh[4 * g + 2], dh[4 * g + 3]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tt == 0) MP_STAMP(6);
         gacc = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), zf0, gacc);
         gacc = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), zf1, gacc);
         if (upd) {
@@ -823,7 +802,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
                   make_float4(preg[tt][4 * g], preg[tt][4 * g + 1], preg[tt][4 * g + 2], preg[tt][4 * g + 3]);
           }
         }
-        if (tt == 0) MP_STAMP(7);
       }
     }
     } else {
@@ -867,7 +845,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
           *reinterpret_cast<bf16x4*>(Img + img_off(r32, h0 + 8 * g + 4 * hh, IMG)) =
               pk4_bf16(dh[4 * g], dh[4 * g + 1], dh[4 * g + 2], dh[4 * g + 3]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tt == 0) MP_STAMP(6);
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 0, h0, lane), xf0, c1);
         c1 = mfma32x32x16(img_trfrag(Img, IMG, 1, h0, lane), xf1, c1);
         if (multi && (upd || XM == 3)) {
@@ -891,7 +868,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
               xpush(a, ep, pbase + (h0 + mfma32_row(i, lane)) * pstride, (dycol ? c2[i] : c1[i]));
           }
         }
-        if (tt == 0) MP_STAMP(7);
       }
     }
     }
@@ -995,7 +971,6 @@ __global__ void __launch_bounds__(kMpThreads) mlp_persistent_kernel(MlpPArgs a) 
         }
       }
     }
-    MP_STAMP(5);
     first = 0;
     // one rank: no barrier here -- the next forward reads only this wave's own
     // rows of W1 / b1 / W2 (updated above by this wave) and b2 / the next batch

@@ -640,8 +640,6 @@ class FullyShardedDataParallel(nn.Module):
         self._ov_stream = torch.cuda.Stream(self.device)
         self._ov_first = True
         self._ov_done = set()
-        # grid cap of the in-backward updates (DTA_OV_OPT_BLOCKS; 0 = the full grid)
-        self._ov_blocks = int(os.environ.get("DTA_OV_OPT_BLOCKS", "0"))
         return True
 
     def _ov_step(self, u: "_Unit", work: Any = None) -> None:
@@ -654,7 +652,7 @@ class FullyShardedDataParallel(nn.Module):
             if work is not None:
                 work.wait(s)
             with prof.range_(f"fsdp.unit{u.index}.optimizer"):
-                self._ov.step_range(fg, lo, lo + fg.numels[i], self._ov_first, self._ov_blocks)
+                self._ov.step_range(fg, lo, lo + fg.numels[i], self._ov_first, 0)
         self._ov_first = False
         self._ov_done.add(u.index)
 
