@@ -20,21 +20,22 @@ namespace k64 {
 //    half kk = 0 run, the 16 ds_read_b128 of half kk = 1 are issued between them (one per 4 MFMAs);
 //    while half 1's MFMAs run, the 16 LDS-DMA pieces of K-tile t + 2 and then the 16 reads of K-tile
 //    t + 1's half 0 are issued between them -- no lgkmcnt(0) between a read and unrelated MFMAs;
-//  * two LDS images (64 KiB each, K-tile t in image t & 1), filled by buffer_load ... lds two K-tiles
-//    ahead; TWO barriers per K-tile: B1 after the wave's last read of K-tile t (the image may be
-//    refilled), B2 mid-way through half 1 after the counted vmcnt that retires K-tile t + 1's pieces
+//  * two LDS images (66 KiB each, K-tile t in image t & 1), filled by buffer_load ... lds two K-tiles
+//    ahead, the pieces spread over the MFMAs (below); barriers after the wave's last read of a
+//    (half) image (it may be refilled) and after the counted vmcnt that retires K-tile t + 1's pieces
 //    (its reads may start): the vmcnt is never 0 in the loop;
 //  * rows of A / B past M / N are CLAMPED in the DMA source (the duplicated rows' accumulators are
 //    never stored): 256-wide tiles cover N = 50304 (the GPT-2 head) with a predicated epilogue;
-//  * the same XOR-swizzled K-major images and conflict-free ds_read_b128 fragment reads as above,
+//  * padded-piece K-major images (conflict-free ds_read_b128 fragment reads, in-order DMA sources),
 //    mfma(B, A) so a lane's four accumulators are four consecutive output columns.
 // The structure is the one the library's best gfx950 kernel for these shapes uses (4 waves,
 // 128 x 128 per wave, MI16x16, direct-to-LDS, prefetch depth 2 -- its kernel name and disassembly);
 // the code is this file's own.
 namespace w4 {
-constexpr int IMG = 256 * BK * 2;                // one operand's K-tile image: 32 KiB
+constexpr int PIECE = 1056;                      // K-major 1 KiB DMA piece + 32 B of padding (see w4_body)
+constexpr int IMG = 32 * PIECE;                  // one operand's K-tile image: 32 pieces (33 KiB)
 constexpr int LDS_BYTES = 4 * IMG;               // [A p0 | A p1 | B p0 | B p1]
-constexpr int NP = IMG / 1024 / 4;               // 1 KiB DMA pieces per wave per operand per K-tile: 8
+constexpr int NP = 8;                            // 1 KiB DMA pieces per wave per operand per K-tile
 }  // namespace w4
 
 // M/N-major image (transposed operand [K][M]): two 128-column halves of 64 k-rows x 256 B, chunk ch of
@@ -52,6 +53,19 @@ __device__ __forceinline__ bf16x4 w4_tr4(const char* lds, int byte_off) {
 // KT: K is not a multiple of 128 (two K-tiles): the loop runs over ceil(K / 128) pairs and every DMA
 // lane whose 8 k-values lie at or past K gets an out-of-range buffer offset -- the buffer unit returns
 // zeros for it, so the tail contributes nothing (K a multiple of 8: chunks are whole).
+// STG: LDS-staged epilogue (one bf16 output).
+//
+// K-major images (no per-lane swizzle: a DMA piece's lanes read whole 128-B row segments in order): piece p
+// (0..31) holds rows p + 32 s (s = lane >> 3), lane & 7 = the 16-B chunk, at PIECE p -- row R at
+// PIECE (R % 32) + 128 (R / 32).  The 32 B of padding per piece put the 16 rows an MFMA fragment read touches
+// at 16-B units 2 (R % 8) + const: with the ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS every group
+// hits 16 distinct units -- conflict-free (checked by enumeration).  A fragment's reads at other j are
+// immediate offsets.
+//
+// The K loop issues a wave's 16 DMA pieces of K-tile t + 2 among its 128 MFMAs of K-tile t after B1: A's 8
+// between the first 32 MFMAs of half 1, B's 8 between the last 32 (one per 4 MFMAs; packed one per 2 MFMAs
+// they cost ~55 issue cycles each -- profiles/gemm_w4_diagnostics.txt, with the schedules and the persistent
+// form that were measured and dropped).
 template <bool AT, bool BT, bool KT, bool STG>
 __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -65,11 +79,11 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
   const int m0 = (gm0 + in_g % gh) * 256, n0 = (in_g / gh) * 256;
   const int nk = KT ? 2 * ((g.K + 2 * BK - 1) / (2 * BK)) : g.K / BK;
 
-  // ---- DMA sources (byte offsets of this wave's 8 pieces of K-tile 0; a K-tile adds kstep) ----
-  // K-major: piece q holds rows 32 q + 8 wave + (lane >> 3), the lane's 16-byte chunk XOR-swizzled by
-  //   the row (row & 7 == lane >> 3); rows past M / N clamped to the last one.
-  // M/N-major: piece gp = 4 q + wave holds k-rows 4 (gp & 15) + (lane >> 4) of half gp >> 4, chunk
-  //   (lane & 15) ^ mswz(k); chunks past M / N clamped to the last full one.
+  // ---- DMA: this wave's 8 pieces per operand and K-tile, q = 0..7 ----
+  // K-major: piece 4 q + wave.
+  // M/N-major: piece gp = 4 q + wave holds k-rows 4 (gp & 15) + (lane >> 4) of column half gp >> 4, chunk
+  //   (lane & 15) ^ mswz(k) (chunks past M / N clamped to the last full one); its half kk = (gp & 15) >= 8.
+  // Rows past M / N are clamped to the last one (their accumulators are never stored).
   // (the base pointers through readfirstlane: the descriptor must live in SGPRs for the asm, and a kernel
   // grown by the staged epilogue lost the compiler's proof that g's fields are uniform)
   auto uni = [](const bf16* p) {
@@ -83,8 +97,8 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
   unsigned voA[w4::NP], voB[w4::NP];
   auto src_off = [&](bool tr, int x0, int X, int64_t ld, int q) -> unsigned {
     if (!tr) {
-      const int r = min(x0 + 32 * q + 8 * wave + (lane >> 3), X - 1);
-      return (unsigned)(((int64_t)r * ld + 8 * ((lane & 7) ^ (lane >> 3))) * 2);
+      const int r = min(x0 + 4 * q + wave + 32 * (lane >> 3), X - 1);
+      return (unsigned)(((int64_t)r * ld + 8 * (lane & 7)) * 2);
     }
     const int gp = 4 * q + wave, k = 4 * (gp & 15) + (lane >> 4);
     const int col = min(x0 + 128 * (gp >> 4) + 8 * ((lane & 15) ^ w4_mswz(k)), X - 8);
@@ -95,9 +109,10 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
     voA[q] = src_off(AT, m0, g.M, g.lda, q);
     voB[q] = src_off(BT, n0, g.N, g.ldb, q);
   }
-  // the k (within a K-tile) of this lane's 8 values in piece q: K-major chunk 8 c, M/N-major k-row
+  // the k (within a K-tile) of this lane's 8 values in piece q
   auto lane_k = [&](bool tr, int q) {
-    return tr ? 4 * ((4 * q + wave) & 15) + (lane >> 4) : 8 * ((lane & 7) ^ (lane >> 3));
+    if (tr) return 4 * ((4 * q + wave) & 15) + (lane >> 4);
+    return 8 * (lane & 7);
   };
   auto kt_off = [&](unsigned vo, bool tr, int q, int kt) -> unsigned {  // the K-tail's zero fill
     if constexpr (!KT) return vo;
@@ -106,20 +121,27 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
   const unsigned kstepA = AT ? (unsigned)(BK * g.lda * 2) : (unsigned)(BK * 2);
   const unsigned kstepB = BT ? (unsigned)(BK * g.ldb * 2) : (unsigned)(BK * 2);
   const unsigned lds0 = lds_addr(lds);
+  // byte offset of this wave's piece q inside an operand image
+  auto pdst = [&](bool tr, int q) -> unsigned {
+    return (4 * q + wave) * (tr ? 1024 : w4::PIECE);
+  };
+  auto piece = [&](int op, int q, int kt, int par) {  // piece q of operand op (0 A, 1 B) of K-tile kt -> image par
+    if (op == 0) bglds16_m0(rsA, kt_off(voA[q], AT, q, kt), (unsigned)kt * kstepA, lds0 + par * w4::IMG + pdst(AT, q));
+    else bglds16_m0(rsB, kt_off(voB[q], BT, q, kt), (unsigned)kt * kstepB, lds0 + (2 + par) * w4::IMG + pdst(BT, q));
+  };
   auto dma = [&](int kt, int par) {  // all 16 pieces of K-tile kt into image par (prologue form)
 #pragma unroll
     for (int q = 0; q < w4::NP; ++q) {
-      bglds16_m0(rsA, kt_off(voA[q], AT, q, kt), (unsigned)kt * kstepA, lds0 + par * w4::IMG + (4 * q + wave) * 1024);
-      bglds16_m0(rsB, kt_off(voB[q], BT, q, kt), (unsigned)kt * kstepB,
-              lds0 + (2 + par) * w4::IMG + (4 * q + wave) * 1024);
+      piece(0, q, kt, par);
+      piece(1, q, kt, par);
     }
   };
 
   // ---- fragment reads: (index 16 j + (lane & 15) of the wave's 128-wide half, k 32 kk + 8 (lane >> 4)) ----
-  // K-major: one ds_read_b128 at a per-lane base (per kk) + 2048 j.  M/N-major: two ds_read_b64_tr_b16
-  // (k-rows 32 kk + 8 g + q and + 4, g = lane >> 4, q = (lane >> 2) & 3) at per-lane, per-j offsets: the
-  // chunk 2 j + (p >> 1) (p = lane & 3) XOR the row swizzle is (j ^ c) * 32 + ..., c = 2 q + (g & 1).
-  const int rrow = lane & 15, x = (lane >> 4) ^ (lane & 7);
+  // K-major: one ds_read_b128 at a per-lane base (per kk) + an immediate per j.  M/N-major: two
+  // ds_read_b64_tr_b16 (k-rows 32 kk + 8 g + q and + 4, g = lane >> 4, q = (lane >> 2) & 3) at per-lane, per-j
+  // offsets: the chunk 2 j + (p >> 1) (p = lane & 3) XOR the row swizzle is (j ^ c) * 32 + ..., c = 2 q + (g & 1).
+  const int rrow = lane & 15;
   int kofA[2], kofB[2];                 // K-major per-kk lane bases
   int tlo[8], thi[8];                   // M/N-major per-j lane offsets inside a half image (lo / hi rows)
   {
@@ -130,14 +152,20 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
       thi[j] = (8 * gg + qq + 4) * 256 + 32 * (j ^ c) + 16 * ((pp >> 1) ^ 1) + 8 * (pp & 1);
     }
   }
-  kofA[0] = (wr * 128 + rrow) * 128 + 16 * x;
-  kofA[1] = (wr * 128 + rrow) * 128 + 16 * (x ^ 4);
-  kofB[0] = (wc * 128 + rrow) * 128 + 16 * x;
-  kofB[1] = (wc * 128 + rrow) * 128 + 16 * (x ^ 4);
-  const char* imgA = lds + (AT ? wr * (w4::IMG / 2) : 0);
-  const char* imgB = lds + 2 * w4::IMG + (BT ? wc * (w4::IMG / 2) : 0);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    // R = 128 w + 16 j + rrow: PIECE (rrow + 16 (j & 1)) + 128 (4 w + (j >> 1)) + 16 (4 kk + (lane >> 4))
+    const int base = w4::PIECE * rrow + 16 * (4 * kk + (lane >> 4));
+    kofA[kk] = base + 512 * wr;
+    kofB[kk] = base + 512 * wc;
+  }
+  const char* imgA = lds + (AT ? wr * 16384 : 0);  // M/N-major: two 16 KiB halves (pieces 0-15, 16-31)
+  const char* imgB = lds + 2 * w4::IMG + (BT ? wc * 16384 : 0);
   auto frag = [&](bool tr, const char* img, const int (&kof)[2], int par, int kk, int j) -> bf16x8 {
-    if (!tr) return *reinterpret_cast<const bf16x8*>(img + par * w4::IMG + kof[kk] + j * 2048);
+    if (!tr) {
+      const int jo = 16 * w4::PIECE * (j & 1) + 128 * (j >> 1);
+      return *reinterpret_cast<const bf16x8*>(img + par * w4::IMG + kof[kk] + jo);
+    }
     const char* b = img + par * w4::IMG + kk * 8192;
     const bf16x4 lo = w4_tr4(b, tlo[j]), hi = w4_tr4(b, thi[j]);
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -159,12 +187,12 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a0[8], b0[8], a1[8], b1[8];  // half-step 0 / 1 fragments: A rows (j), B rows (i)
-  // one K-tile kt (P = its parity = image): MFMAs of both half-steps; between them the reads of half 1,
-  // the DMA of K-tile kt + 2 into this image (past the last K-tile: the last one again, never read -- the
-  // wait counts stay static) and the reads of K-tile kt + 1's half 0 (after the last K-tile: that
-  // never-read reload, equally harmless)
+  // one K-tile kt (P = its parity = image): MFMAs of both half-steps; between them the reads of half 1, the
+  // DMA of K-tile kt + 2 into this image (past the last K-tile: the last one again, never read -- the wait
+  // counts stay static) and the reads of K-tile kt + 1's half 0 (after the last K-tile: that never-read reload)
   auto ktile = [&](const int kt, auto P) {
     constexpr int p = decltype(P)::value;
+    const int kn = min(kt + 2, nk - 1);
     // half 0: 64 MFMAs on a0 / b0; between them the 16 reads of half 1 of this K-tile
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -179,14 +207,11 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
     }
     lgkm0();  // this wave's reads of K-tile kt are done
     bar();    // B1: every wave's are -- image p may be refilled
-    // half 1: 64 MFMAs on a1 / b1; the DMA of K-tile kt + 2 between the first 32, the reads of K-tile kt + 1's
-    // half 0 between the last 32
-    const int kn = min(kt + 2, nk - 1);
-    const unsigned soA = (unsigned)kn * kstepA, soB = (unsigned)kn * kstepB;
+    // half 1: 64 MFMAs on a1 / b1; A's 8 pieces of K-tile kt + 2 between the first 32, the reads of K-tile
+    // kt + 1's half 0 and B's 8 pieces between the last 32
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s < 8) bglds16_m0(rsA, kt_off(voA[s], AT, s, kn), soA, lds0 + p * w4::IMG + (4 * s + wave) * 1024);
-      else bglds16_m0(rsB, kt_off(voB[s - 8], BT, s - 8, kn), soB, lds0 + (2 + p) * w4::IMG + (4 * (s - 8) + wave) * 1024);
+      if (s % 2 == 0) piece(0, s / 2, kn, p);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int idx = 2 * s + q, j = idx >> 3, i = idx & 7;
@@ -194,12 +219,13 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    vm_wait<2 * w4::NP>();  // K-tile kt + 1 landed (this wave's pieces; kt + 2's stay in flight)
-    bar();                  // B2: every wave's pieces of K-tile kt + 1 landed
+    vm_wait<w4::NP>();  // B2: K-tile kt + 1 landed in every wave (K-tile kt + 2's 8 pieces of A stay in flight)
+    bar();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if (s < 8) b0[s] = rdB(p ^ 1, 0, s);
       else a0[s - 8] = rdA(p ^ 1, 0, s - 8);
+      if (s % 2 == 0) piece(1, s / 2, kn, p);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int idx = 32 + 2 * s + q, j = idx >> 3, i = idx & 7;
@@ -226,7 +252,19 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
     b0[s] = rdB(0, 0, s);
     a0[s] = rdA(0, 0, s);
   }
-  // nk even (K % 128 == 0, checked on the host): pairs of K-tiles, parities compile-time constants, one
+  // The last MFMAs' results are still in the matrix pipe when the loop ends: wait states before any
+  // v_accvgpr_read.  The compiler does not know the asm statements are MFMAs, so every accumulator is then
+  // passed through an empty asm ("+a") AFTER the nops -- volatile asm keeps its order, and the epilogue's
+  // reads depend on those outputs.  (Without it hipcc read the last-written accumulators right behind their
+  // MFMA: wrong sums in rows 240-255 of every tile, tests/test_gemm64_gpu.py.)
+  auto drain = [&]() {
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  };
+  // nk even (K % 128 == 0, or the K tail rounded up): pairs of K-tiles, parities compile-time constants, one
   // loop body and no tail -- branchy tails made the register allocator shuffle all 256 accumulators
   for (int kt = 0; kt < nk; kt += 2) {
     ktile(kt, std::integral_constant<int, 0>{});
@@ -237,53 +275,36 @@ __device__ __forceinline__ void w4_body(const Args& g, const int t, char* lds) {
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
   }
   vm_wait<0>();  // the never-read reloads of the last iterations land before the LDS is released
-  // The last MFMAs' results are still in the matrix pipe: wait states before any v_accvgpr_read.  The
-  // compiler does not know the asm statements are MFMAs, so every accumulator is then passed through an
-  // empty asm ("+a") AFTER the nops -- volatile asm keeps its order, and the epilogue's reads depend on
-  // those outputs.  (Without it hipcc read the last-written accumulators right behind their MFMA: wrong
-  // sums in rows 240-255 of every tile, tests/test_gemm64_gpu.py.)
-  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  drain();
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment; rows / columns past M / N
   // (clamped duplicates) are not stored ----
   if constexpr (STG) {  // (the host takes this form only for one bf16 output: no c32, no GELU dual store)
-    {
-      // LDS-staged: the wave's 128 x 128 bf16 result goes through its own 32 KiB of the (now free) LDS and
-      // leaves as whole 256-B row pieces (one global_store_dwordx4 per lane: 4 rows per instruction)
-      // instead of 64 stores of 16 rows x 32 B each.  Staging image: row r at 256 r, its 16-B chunk c at
-      // c ^ (r & 15) (2-way conflicts at most on the 8-B writes, none on the row reads).
-      bar();  // every wave's reads and DMA are done: the LDS is free
-      char* st = lds + wave * (w4::IMG);
-      auto pass = [&](bf16* dst, int64_t ldd, int which) {
+    // LDS-staged: the wave's 128 x 128 bf16 result goes through its own 32 KiB of the (now free) LDS and
+    // leaves as whole 256-B row pieces (one global_store_dwordx4 per lane: 4 rows per instruction)
+    // instead of 64 stores of 16 rows x 32 B each.  Staging image: row r at 256 r, its 16-B chunk c at
+    // c ^ (r & 15) (2-way conflicts at most on the 8-B writes, none on the row reads).
+    bar();  // every wave's reads and DMA are done: the LDS is free
+    char* st = lds + wave * (w4::IMG);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int nl = 16 * i + 4 * (lane >> 4);
-          float bv[4];
-          load_bias4(g, min(n0 + wc * 128 + nl, g.N - 4), bv);
+    for (int i = 0; i < 8; ++i) {
+      const int nl = 16 * i + 4 * (lane >> 4);
+      float bv[4];
+      load_bias4(g, min(n0 + wc * 128 + nl, g.N - 4), bv);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int ml = 16 * j + (lane & 15);
-            const bf16x4 v = val4(g, min(m0 + wr * 128 + ml, g.M - 1), min(n0 + wc * 128 + nl, g.N - 4), acc[i][j],
-                                  bv, which);
-            *reinterpret_cast<bf16x4*>(st + ml * 256 + 16 * ((nl >> 3) ^ (ml & 15)) + 8 * ((nl >> 2) & 1)) = v;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-          const int row = 4 * r + (lane >> 4), c = lane & 15;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + row * 256 + 16 * (c ^ (row & 15)));
-          const int m = m0 + wr * 128 + row, n = n0 + wc * 128 + 8 * c;
-          if (m < g.M && n < g.N) *reinterpret_cast<bf16x8*>(dst + (int64_t)m * ldd + n) = v;
-        }
-      };
-      // (one output only: the host takes the per-fragment form for the GELU dual store -- a conditional
-      // second pass here made the compiler place the K loop's DMA descriptors in VGPRs)
-      pass(g.c, g.ldc, 0);
-      return;
+      for (int j = 0; j < 8; ++j) {
+        const int ml = 16 * j + (lane & 15);
+        const bf16x4 v = val4(g, min(m0 + wr * 128 + ml, g.M - 1), min(n0 + wc * 128 + nl, g.N - 4), acc[i][j], bv, 0);
+        *reinterpret_cast<bf16x4*>(st + ml * 256 + 16 * ((nl >> 3) ^ (ml & 15)) + 8 * ((nl >> 2) & 1)) = v;
+      }
     }
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+      const int row = 4 * r + (lane >> 4), c = lane & 15;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(st + row * 256 + 16 * (c ^ (row & 15)));
+      const int m = m0 + wr * 128 + row, n = n0 + wc * 128 + 8 * c;
+      if (m < g.M && n < g.N) *reinterpret_cast<bf16x8*>(g.c + (int64_t)m * g.ldc + n) = v;
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -304,7 +325,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(Args g) {
   __shared__ __attribute__((aligned(1024))) char lds[w4::LDS_BYTES];
   w4_body<AT, BT, KT, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n), lds);
 }
-
 
 // Grouped weight gradients (the contract of gemm_k64.hip's gemm_k64_group_kernel on the W4 pipeline, minus
 // the bias gradient): dW_i = A_i^T B_i (A_i = dy [K][M_i], B_i = x [K][N_i]) for up to kGroupMax problems in
@@ -376,9 +396,12 @@ static void w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, hipStream_t s
 }
 
 // staged: the LDS-staged epilogue (tile id 10) instead of per-fragment stores (tile id 9); one bf16 output only
-hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, bool staged, hipStream_t st) {
-  const bool kt = g.K % (2 * dta::k64::BK) != 0;
-  staged = staged && g.c32 == nullptr && !(g.epi == dta::k64::EPI_GELU && g.c2 != nullptr);
+// (no fp32 output, no GELU dual store: those take the per-fragment form)
+hipError_t dta_gemm_w4_launch(const dta::k64::Args& g, bool a_t, bool b_t, bool staged_in, hipStream_t st) {
+  using namespace dta::k64;
+  const bool kt = g.K % (2 * BK) != 0;
+  const bool one_out = g.c32 == nullptr && !(g.epi == EPI_GELU && g.c2 != nullptr);
+  const bool staged = staged_in && one_out;
   if (kt) {
     if (staged) w4_launch<true, true>(g, a_t, b_t, st);
     else w4_launch<true, false>(g, a_t, b_t, st);

@@ -402,7 +402,7 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     if _gemm_ok(x2, w, b) and N % 8 == 0:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
         for t in K64_TILES:
-            if _k64_on() and C.gemm64_tile(M, N, K, t):
+            if C.gemm64_tile(M, N, K, t):
                 cands[K64 + t] = (lambda t=t: run_k64(t))
         impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands)
     if impl:

@@ -3,6 +3,7 @@
 at the GPT-2 small and Llama-3 8B shapes.  Causal FLOPs counted as the
 unmasked half (fwd 2*B*H*S^2*D, bwd 2.5x that)."""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -47,6 +48,14 @@ def main():
         o, lse = C.attn_fwd(q, k, v, True, sc, -1)
         t_fwd = timeit(lambda: C.attn_fwd(q, k, v, True, sc, -1))
         t_bwd = timeit(lambda: C.attn_bwd(do, q, k, v, o, lse, True, sc, -1))
+        # the forward's workgroup forms (csrc/attention.hip fwd_waves: 4 / 8 waves, "pp" the ping-pong kernel)
+        fwd_var, fwd_var_err = {}, {}
+        for wv in ("4", "8", "pp"):
+            os.environ["DTA_ATTN_FWD_WAVES"] = wv
+            fwd_var[wv] = round(timeit(lambda: C.attn_fwd(q, k, v, True, sc, -1)) * 1e6, 1)
+            ov, lv = C.attn_fwd(q, k, v, True, sc, -1)
+            fwd_var_err[wv] = [(ov.float() - o.float()).abs().max().item(), (lv - lse).abs().max().item()]
+        os.environ.pop("DTA_ATTN_FWD_WAVES", None)
         fl = 2.0 * B * H * S * S * D  # causal fwd (4*S^2*D/2)
         # torch SDPA reference (expects [B, H, S, D]; GQA expanded)
         rep = H // Hkv
@@ -73,7 +82,8 @@ def main():
                           "fwd_tflops": round(fl / t_fwd / 1e12, 1), "bwd_tflops": round(2.5 * fl / t_bwd / 1e12, 1),
                           "sdpa_fwd_us": round(t_tf * 1e6, 1), "sdpa_bwd_us": round(t_tb * 1e6, 1),
                           "packed_rope_fwd_us": round(t_pf * 1e6, 1), "packed_rope_bwd_us": round(t_pb * 1e6, 1),
-                          "max_abs_err_vs_sdpa": err}), flush=True)
+                          "max_abs_err_vs_sdpa": err, "fwd_variants_us": fwd_var,
+                          "fwd_variants_maxdiff_o_lse": fwd_var_err}), flush=True)
 
 
 if __name__ == "__main__":

@@ -42,9 +42,14 @@ def _losses(log):
     return vals
 
 
+# the GPU attention kernels take head dims 64 / 128: the CPU tests' 64-wide models widened to 256 (4 heads)
+GPU_WIDTH = ["model.n_embd=256"]
+
+
 @pytest.mark.parametrize("name,args", [
-    ("llama_fsdp", TINY_LLAMA + ["train=llama3_8b_fsdp", "+train.step_graph=true", "train.dataset_size=64"]),
-    ("gpt2_ddp", TINY_GPT2 + ["train=gpt2_ddp", "train.dataset_size=128"]),
+    ("llama_fsdp", TINY_LLAMA + GPU_WIDTH + ["model.ffn_hidden=512", "train=llama3_8b_fsdp", "+train.step_graph=true",
+                                             "train.dataset_size=64"]),
+    ("gpt2_ddp", TINY_GPT2 + GPU_WIDTH + ["train=gpt2_ddp", "train.dataset_size=128"]),
 ])
 def test_lm_step_graph_through_entrypoint_gpu(tmp_path, name, args):
     snap, log = _run(tmp_path, "run", args, epochs=4)

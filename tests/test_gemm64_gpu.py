@@ -203,11 +203,14 @@ def test_gemm_w4_epilogues(epi, tile):
         _close(y, 0.5 * (a.float() @ b.float().t()) + bias.float(), K)
 
 
+@pytest.mark.parametrize("tile", [10])
 @pytest.mark.parametrize("a_t,b_t", LAYOUTS)
-@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (304, 520, 384), (8192, 50304 // 16, 768), (256, 512, 72)])
-def test_gemm_w4_staged_epilogue_exact(a_t, b_t, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (304, 520, 384), (8192, 50304 // 16, 768), (256, 512, 72),
+                                   (8192, 8448, 192), (6400, 9000, 384)])
+def test_gemm_w4_staged_epilogue_exact(a_t, b_t, M, N, K, tile):
     """Tile 10: the W4 kernel with the LDS-staged bf16 epilogue (whole 256-B row pieces per store), edges
-    predicated: exact against fp32 on small integers whose sums stay exactly representable in bf16."""
+    predicated (the big shapes: many rounds of tiles, edge tiles and K tails): exact against fp32 on small
+    integers whose sums stay exactly representable in bf16."""
     from distributed_training_amd.ops import native
 
     gen = torch.Generator().manual_seed(M + 3 * N + K + 2 * a_t + b_t)
@@ -218,6 +221,6 @@ def test_gemm_w4_staged_epilogue_exact(a_t, b_t, M, N, K):
     want = (a.t() if a_t else a) @ (b if b_t else b.t())
     assert want.abs().max() <= 256
     out = torch.full((M, N), float("nan"), device="cuda").bfloat16()
-    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=10)
+    got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=tile)
     torch.cuda.synchronize()
     assert torch.equal(got.float().cpu(), want), (a_t, b_t, M, N, K)
