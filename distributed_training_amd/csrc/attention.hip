@@ -458,233 +458,6 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   }
 }
 
-// ------------------------------------------------------------------ forward, ping-pong form
-// 8 waves in two groups of 4 (one wave of each group per SIMD) that run ONE PHASE APART, so on every SIMD one
-// wave's MFMAs (S_j = K_j.Q^T, then O += V_{j-1}^T.P_{j-1}) run while its partner does its online softmax
-// (VALU) -- the two waves of the plain kernel above do the same step at the same time, so each waits for the
-// other's kind of work (MI355X_MICROARCH.md "Two waves per SIMD": one wave in a matrix segment, its partner in
-// a VALU / load segment).  Per 64-key block j, with a workgroup barrier after every phase:
-//   phase 2j:     group 0: S_j, PV_{j-1}          group 1: softmax_{j-1}; stores K_{j+1}, V_j; loads K_{j+2}, V_{j+1}
-//   phase 2j + 1: group 0: softmax_j             group 1: S_j, PV_{j-1}
-// K_j lives in Ks[j & 1] for phases 2j .. 2j+1 (stored in phase 2j-2), V_j in Vs[j & 1] for phases 2j+2 ..
-// 2j+3 (stored in phase 2j): every store lands in a buffer whose last reader finished a barrier earlier.
-// The groups' queries interleave (wave w: rows 32 (2 (w & 3) + group)) so causal skipping costs both the same.
-// The math (mask, rescale threshold, exp2 with the folded scale, LSE) is the plain kernel's.
-template <int D, bool CAUSAL>
-__global__ void __launch_bounds__(512, 2) attn_fwd_pp_kernel(AttnArgs a) {
-  constexpr int QB = 256;        // queries per workgroup
-  constexpr int BN = 64;         // keys per block
-  constexpr int NKS = D / 16;    // MFMA k-steps over D
-  constexpr int NDT = D / 32;    // 32-wide output tiles over D
-  __shared__ __attribute__((aligned(16))) bf16 Ks[2][BN * D];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[2][BN * D];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;
-  const int r32 = lane & 31, hh = lane >> 5;
-  int qb, bh;
-  fwd_block(blockIdx.x, a.B * a.H, (a.S + QB - 1) / QB, CAUSAL, qb, bh);
-  const int b = bh / a.H, h = bh % a.H;
-  const int hk = h / (a.H / a.Hkv);
-  const int q0w = qb * QB + 32 * (2 * (wave & 3) + grp);
-  const int qrow = q0w + r32;
-  const bf16* qbase = static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)h * D;
-  const bf16* kbase = static_cast<const bf16*>(a.k) + (int64_t)b * a.k_sb + (int64_t)hk * D;
-  const bf16* vbase = static_cast<const bf16*>(a.v) + (int64_t)b * a.v_sb + (int64_t)hk * D;
-
-  bf16x8 qf[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    if (qrow < a.S)
-      qf[ks] = *reinterpret_cast<const bf16x8*>(qbase + (int64_t)qrow * a.q_ss + ks * 16 + hh * 8);
-    else
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = f2bf(0.f);
-  }
-  f32x16 oacc[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = splat16(0.f);
-  float m = kNegBig, l = 0.f;
-  const float c = a.scale * kLog2e;
-  const int kv_end = CAUSAL ? min(qb * QB + QB, a.S) : a.S;
-  const int nblk = (kv_end + BN - 1) / BN;
-  auto active = [&](int j) __attribute__((always_inline)) { return !(CAUSAL && j * BN > q0w + 31); };  // some key of block j <= a query
-
-  f32x16 st[2];
-  bf16x8 pb[2][2];
-  // the MFMA phase as one software-pipelined stream (the plain kernel's attend()): NS ops of S_j (t, ks), then
-  // NP ops of PV_{j-1} (t, sh, dt); each op's LDS fragment read PF ops ahead into a register ring, sched_barriers
-  // pin the order (left to itself hipcc hoisted every read and spilled)
-  auto mfma_phase_c = [&](int j, auto DS, auto DP) __attribute__((always_inline)) {
-    constexpr bool do_s = decltype(DS)::value, do_pv = decltype(DP)::value;
-    constexpr int NS = 2 * NKS, NP = 4 * NDT, TOT = NS + NP, PF = 2, RING = PF + 1;
-    const bf16* Kb = Ks[j & 1];
-    const bf16* Vb = Vs[(j - 1) & 1];
-    bf16x8 ring[RING];
-    auto issue = [&](auto oc) __attribute__((always_inline)) {
-      constexpr int o = decltype(oc)::value;
-      if constexpr (o < NS) {
-        if constexpr (do_s) ring[o % RING] = row_frag<D>(Kb, (o / NKS) * 32 + r32, o % NKS, hh);
-      } else {
-        constexpr int cc = o - NS, t = cc / (2 * NDT), sh = (cc / NDT) % 2, dt = cc % NDT;
-        if constexpr (do_pv) ring[o % RING] = tr_frag<D>(Vb, t * 32, dt * 32, sh, lane);
-      }
-    };
-    auto compute = [&](auto oc) __attribute__((always_inline)) {
-      constexpr int o = decltype(oc)::value;
-      if constexpr (o < NS) {
-        constexpr int t = o / NKS, ks = o % NKS;
-        if constexpr (do_s) {
-          if constexpr (ks == 0) st[t] = splat16(0.f);
-          st[t] = mfma32x32x16(ring[o % RING], qf[ks], st[t]);
-        }
-      } else {
-        constexpr int cc = o - NS, t = cc / (2 * NDT), sh = (cc / NDT) % 2, dt = cc % NDT;
-        if constexpr (do_pv) oacc[dt] = mfma32x32x16(ring[o % RING], pb[t][sh], oacc[dt]);
-      }
-    };
-    static_for<PF>([&](auto oc) __attribute__((always_inline)) { issue(oc); });
-    static_for<TOT>([&](auto oc) __attribute__((always_inline)) {
-      constexpr int o = decltype(oc)::value;
-      if constexpr (o + PF < TOT) issue(std::integral_constant<int, o + PF>{});
-      __builtin_amdgcn_sched_barrier(0);
-      compute(oc);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-  };
-  auto mfma_phase = [&](int j, bool do_s, bool do_pv) __attribute__((always_inline)) {
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    if (do_s && do_pv) mfma_phase_c(j, T_{}, T_{});
-    else if (do_s) mfma_phase_c(j, T_{}, F_{});
-    else if (do_pv) mfma_phase_c(j, F_{}, T_{});
-  };
-  auto softmax = [&](int j) __attribute__((always_inline)) {
-    const int k0 = j * BN;
-    const bool need_mask = (CAUSAL && k0 + BN - 1 > q0w) || k0 + BN > a.S;
-    if (need_mask) {
-      const int lim = min(a.S - 1, CAUSAL ? qrow : a.S) - k0 - 4 * hh;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (t * 32 + mfma32_row(i, 0) > lim) st[t][i] = kNegBig;
-    }
-    float mblk = st[0][0];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t][i]);
-    mblk = xor32_max(mblk);
-    if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
-      const float mnew = fmaxf(m, mblk * c);
-      const float alpha = fexp2(m - mnew);
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-      m = mnew;
-    }
-    float lsum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = fexp2(__builtin_fmaf(st[t][i], c, -m));
-        st[t][i] = p;
-        lsum += p;
-      }
-    l += xor32_sum(lsum);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int sh = 0; sh < 2; ++sh)
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) pb[t][sh][jj] = f2bf(st[t][8 * sh + jj]);
-  };
-  auto phase_end = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-  // Tiles arrive by LDS-DMA (buffer_load ... lds: no staging registers, no LDS store instructions): a 64-row
-  // tile image is D / 8 pieces of 1 KiB, piece pc = rows 8 (pc / (D / 64)) .. + 7 x column subtiles 2 (pc %
-  // (D / 64)) + {0, 1}; lane i of a piece fills image bytes 1024 pc + 16 i, i.e. subtile row (i & 31) >> 2, slot
-  // i & 3, which holds chunk slot ^ ((row >> 2) & 3) of the row (the swizzle of lo<D>, applied to the SOURCE
-  // address).  Rows past S read zeros (buffer range = the sequence).  Group 1 issues K_{j+1} and V_j at the
-  // start of phase 2j and waits for them (vmcnt 0) before the barrier that ends phase 2j + 1.
-  constexpr int NPC = D / 8;                      // pieces per tile
-  const unsigned nrec_k = (unsigned)(((int64_t)(a.S - 1) * a.k_ss + D) * 2);
-  const unsigned nrec_v = (unsigned)(((int64_t)(a.S - 1) * a.v_ss + D) * 2);
-  const __amdgpu_buffer_rsrc_t rsK = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(kbase), 0, nrec_k, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(vbase), 0, nrec_v, 0x00020000);
-  auto piece_off = [&](int pc, int64_t ss) -> unsigned {  // lane's byte offset of piece pc within a tile
-    const int r = (lane & 31) >> 2, slot = lane & 3, st2 = lane >> 5;
-    const int row = 8 * (pc / (D / 64)) + r;
-    const int col = 32 * (2 * (pc % (D / 64)) + st2) + 8 * (slot ^ ((row >> 2) & 3));
-    return (unsigned)(((int64_t)row * ss + col) * 2);
-  };
-  const unsigned ldsK0 = lds_addr(&Ks[0][0]), ldsV0 = lds_addr(&Vs[0][0]);
-  constexpr int TB = BN * D * 2;                  // tile image bytes
-  constexpr int GP = NPC / 4;                     // group 1's pieces per wave per tile
-  unsigned offK[GP], offV[GP];
-#pragma unroll
-  for (int k = 0; k < GP; ++k) {
-    offK[k] = piece_off((wave & 3) + 4 * k, a.k_ss);
-    offV[k] = piece_off((wave & 3) + 4 * k, a.v_ss);
-  }
-  auto stage = [&](int j) __attribute__((always_inline)) {  // group 1: K_{j+1} and V_j into their buffers
-    if (j + 1 < nblk) {
-      const unsigned soff = (unsigned)((int64_t)(j + 1) * BN * a.k_ss * 2);
-#pragma unroll
-      for (int k = 0; k < GP; ++k)
-        bglds16(rsK, offK[k], soff, ldsK0 + ((j + 1) & 1) * TB + 1024 * ((wave & 3) + 4 * k));
-    }
-    if (j < nblk) {
-      const unsigned soff = (unsigned)((int64_t)j * BN * a.v_ss * 2);
-#pragma unroll
-      for (int k = 0; k < GP; ++k)
-        bglds16(rsV, offV[k], soff, ldsV0 + (j & 1) * TB + 1024 * ((wave & 3) + 4 * k));
-    }
-  };
-  // prologue: K_0 by all 8 waves
-#pragma unroll
-  for (int k = 0; k < NPC / 8; ++k) bglds16(rsK, piece_off(wave + 8 * k, a.k_ss), 0, ldsK0 + 1024 * (wave + 8 * k));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  phase_end();
-  for (int j = 0; j <= nblk; ++j) {
-    // ---- phase 2j ----
-    if (grp == 0) {
-      mfma_phase(j, j < nblk && active(j), j >= 1 && active(j - 1));
-    } else {
-      stage(j);
-      if (j >= 1 && active(j - 1)) softmax(j - 1);
-    }
-    phase_end();
-    // ---- phase 2j + 1 ----
-    if (grp == 0) {
-      if (j < nblk && active(j)) softmax(j);
-    } else {
-      mfma_phase(j, j < nblk && active(j), j >= 1 && active(j - 1));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of K_{j+1}, V_j landed
-    }
-    phase_end();
-  }
-  // ---- epilogue: O = O^T^T / l ; LSE ----
-  if (qrow < a.S) {
-    const float inv = 1.f / l;
-    bf16* orow = static_cast<bf16*>(a.o) + (int64_t)b * a.o_sb + (int64_t)qrow * a.o_ss + (int64_t)h * D;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const bf16x4 ov = {f2bf(oacc[dt][4 * g4] * inv), f2bf(oacc[dt][4 * g4 + 1] * inv),
-                           f2bf(oacc[dt][4 * g4 + 2] * inv), f2bf(oacc[dt][4 * g4 + 3] * inv)};
-        *reinterpret_cast<bf16x4*>(orow + dt * 32 + 8 * g4 + 4 * hh) = ov;
-      }
-    if (hh == 0) a.lse[((int64_t)b * a.H + h) * a.S + qrow] = (m + log2f(l)) / kLog2e;
-  }
-}
-
 // ------------------------------------------------------------------ backward
 
 // Query rows per slice of the dK/dV kernel: 64 (two 32-row MFMA tiles) halves
@@ -1081,8 +854,8 @@ static void fwd_launch(const AttnArgs& a, bool causal, hipStream_t st) {
 // whenever the grid still holds >= 256 (D = 64; GPT-2: 43.6 -> 37.4 us) or
 // >= 1024 (D = 128) such workgroups.
 static int fwd_waves(const AttnArgs& a, int D) {
-  const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4", "8" or "pp" (the ping-pong form)
-  if (force) return force[0] == 'p' ? 16 : atoi(force) == 8 ? 8 : 4;
+  const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
+  if (force) return atoi(force) == 8 ? 8 : 4;
   const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
   return wg8 >= (D == 128 ? 1024 : 256) ? 8 : 4;
 }
@@ -1097,16 +870,8 @@ static int dq_waves(const AttnArgs& a, int D) {
 
 template <int D>
 static hipError_t fwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
-  const int w = fwd_waves(a, D);
-  if (w == 16) {  // ping-pong: 8 waves, 256 queries per workgroup
-    dim3 grid((unsigned)(((a.S + 255) / 256) * a.B * a.H));
-    if (causal) hipLaunchKernelGGL((attn_fwd_pp_kernel<D, true>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_pp_kernel<D, false>), grid, dim3(512), 0, st, a);
-  } else if (w == 8) {
-    fwd_launch<D, 8>(a, causal, st);
-  } else {
-    fwd_launch<D, 4>(a, causal, st);
-  }
+  if (fwd_waves(a, D) == 8) fwd_launch<D, 8>(a, causal, st);
+  else fwd_launch<D, 4>(a, causal, st);
   return hipGetLastError();
 }
 

@@ -48,9 +48,9 @@ def main():
         o, lse = C.attn_fwd(q, k, v, True, sc, -1)
         t_fwd = timeit(lambda: C.attn_fwd(q, k, v, True, sc, -1))
         t_bwd = timeit(lambda: C.attn_bwd(do, q, k, v, o, lse, True, sc, -1))
-        # the forward's workgroup forms (csrc/attention.hip fwd_waves: 4 / 8 waves, "pp" the ping-pong kernel)
+        # the forward's workgroup forms (csrc/attention.hip fwd_waves: 4 / 8 waves)
         fwd_var, fwd_var_err = {}, {}
-        for wv in ("4", "8", "pp"):
+        for wv in ("4", "8"):
             os.environ["DTA_ATTN_FWD_WAVES"] = wv
             fwd_var[wv] = round(timeit(lambda: C.attn_fwd(q, k, v, True, sc, -1)) * 1e6, 1)
             ov, lv = C.attn_fwd(q, k, v, True, sc, -1)
