@@ -143,9 +143,14 @@ struct Cfg {
   static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
 };
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS>
+// STG (256 x 256 tiles, one bf16 output): the epilogue goes through the LDS as a whole 256 x 256 bf16 tile
+// image (the 128 KiB the K loop used) and leaves as whole 512-B rows -- instead of one 8-B store per lane per
+// fragment (16 rows x 32 B per instruction).  csrc/gemm_w4.hip's staged epilogue measured 10-15 % faster
+// than its per-fragment form.
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false>
 __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
+  static_assert(!STG || (BM == 256 && BN == 256), "staged epilogue: 256 x 256 tiles (the tile image fills the LDS)");
   using C = Cfg<BM, BN, WC, AT, BT>;
   constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
   constexpr bool STAG = WC == 4;  // two waves per SIMD: stagger the halves
@@ -452,6 +457,33 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     }
   }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment ----
+  if constexpr (STG) {
+    // tile image: row r at 512 r, its 16-B chunk c at c ^ (r & 31)
+    bar();  // every wave's last fragment reads and DMA are done: the LDS is free
+#pragma unroll
+    for (int i = 0; i < 2 * NTH; ++i) {
+      const int nh = i / NTH, ii = i % NTH;
+      const int nl = nh * HB + wc * (HB / WC) + 16 * ii + 4 * (lane >> 4);
+      float bv[4];
+      load_bias4(g, n0 + nl, bv);
+#pragma unroll
+      for (int j = 0; j < 2 * MTH; ++j) {
+        const int mh = j / MTH, jj = j % MTH;
+        const int ml = mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
+        const bf16x4 v = val4(g, m0 + ml, n0 + nl, acc[i][j], bv, 0);
+        *reinterpret_cast<bf16x4*>(lds + ml * 512 + 16 * ((nl >> 3) ^ (ml & 31)) + 8 * ((nl >> 2) & 1)) = v;
+      }
+    }
+    lgkm0();
+    bar();
+#pragma unroll
+    for (int r = 0; r < 256 / (2 * NW); ++r) {
+      const int row = wave * (256 / NW) + 2 * r + (lane >> 5), c = lane & 31;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * 512 + 16 * (c ^ (row & 31)));
+      *reinterpret_cast<bf16x8*>(g.c + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2 * NTH; ++i) {
     const int nh = i / NTH, ii = i % NTH;
@@ -468,9 +500,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 }
 
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF>
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false>
 __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
-  k64_body<BM, BN, WC, AT, BT, PH, BUF, false>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
 // Grouped weight gradients (on this kernel's 64-deep
@@ -483,11 +515,19 @@ __global__ void __launch_bounds__(512) gemm_k64_group_kernel(GroupArgs ga) {
   const int t = xcd_remap(blockIdx.x, ga.tile_start[ga.n]);
   int q = 0;
   while (q + 1 < ga.n && t >= ga.tile_start[q + 1]) ++q;
-  k64_body<256, 256, 4, true, true, 2, BUF, true>(ga.p[q], t - ga.tile_start[q]);
+  k64_body<256, 256, 4, true, true, 2, BUF, true, true>(ga.p[q], t - ga.tile_start[q]);
 }
 
+// stg: the staged epilogue (256 x 256, two-phase, buffer DMA, one bf16 output)
 template <int BM, int BN, int WC, bool AT, bool BT, bool BUF>
-static hipError_t launch(const Args& g, int ph, hipStream_t st) {
+static hipError_t launch(const Args& g, int ph, bool stg, hipStream_t st) {
+  if constexpr (BM == 256 && BN == 256 && BUF) {
+    if (ph == 2 && stg) {
+      hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF, true>), dim3(g.tiles_m * g.tiles_n),
+                         dim3(128 * WC), 0, st, g);
+      return hipGetLastError();
+    }
+  }
   if (ph == 2)
     hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF>), dim3(g.tiles_m * g.tiles_n), dim3(128 * WC), 0, st,
                        g);
@@ -498,16 +538,16 @@ static hipError_t launch(const Args& g, int ph, hipStream_t st) {
 }
 
 template <int BM, int BN, int WC, bool BUF>
-static hipError_t launch_l(const Args& g, bool at, bool bt, int ph, hipStream_t st) {
-  if (!at && !bt) return launch<BM, BN, WC, false, false, BUF>(g, ph, st);
-  if (!at && bt) return launch<BM, BN, WC, false, true, BUF>(g, ph, st);
-  if (at && bt) return launch<BM, BN, WC, true, true, BUF>(g, ph, st);
-  return launch<BM, BN, WC, true, false, BUF>(g, ph, st);
+static hipError_t launch_l(const Args& g, bool at, bool bt, int ph, bool stg, hipStream_t st) {
+  if (!at && !bt) return launch<BM, BN, WC, false, false, BUF>(g, ph, stg, st);
+  if (!at && bt) return launch<BM, BN, WC, false, true, BUF>(g, ph, stg, st);
+  if (at && bt) return launch<BM, BN, WC, true, true, BUF>(g, ph, stg, st);
+  return launch<BM, BN, WC, true, false, BUF>(g, ph, stg, st);
 }
 
 template <int BM, int BN, int WC>
-static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, bool buf, hipStream_t st) {
-  return buf ? launch_l<BM, BN, WC, true>(g, at, bt, ph, st) : launch_l<BM, BN, WC, false>(g, at, bt, ph, st);
+static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, bool buf, bool stg, hipStream_t st) {
+  return buf ? launch_l<BM, BN, WC, true>(g, at, bt, ph, stg, st) : launch_l<BM, BN, WC, false>(g, at, bt, ph, stg, st);
 }
 
 // tile ids: 1 = 256x256 (8 waves), 2 = 256x128 (8 waves), 3 = 128x128 (4 waves), 4 = 128x256 (8 waves);
@@ -522,6 +562,7 @@ constexpr int kBufDma = 16;
 constexpr int kW4 = 9;
 constexpr int kW4S = 10;  // the same with the LDS-staged epilogue (whole 256-B row pieces per store)
 constexpr int kFlatDma = 32;
+constexpr int kNoStg = 128;  // tile-id bit: the per-fragment epilogue even where the staged one applies (A/B)
 __host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
 __host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
 
@@ -539,8 +580,8 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   // W4: any M, N, K multiples of 8 (clamped DMA rows / chunks, predicated stores, zero-filled K tail)
   if (tile == k64::kW4 || tile == k64::kW4S) return K % 8 == 0 && K > 0 && M % 8 == 0 && N % 8 == 0 ? tile : 0;
   if (K % k64::BK || K < k64::BK) return 0;
-  if (tile & (k64::kBufDma | k64::kFlatDma)) {  // the same tile, DMA form chosen explicitly
-    const int bits = tile & (k64::kBufDma | k64::kFlatDma);
+  if (tile & (k64::kBufDma | k64::kFlatDma | k64::kNoStg)) {  // the same tile, DMA / epilogue form chosen explicitly
+    const int bits = tile & (k64::kBufDma | k64::kFlatDma | k64::kNoStg);
     const int t = dta_gemm_k64_tile(M, N, K, tile & ~bits);
     return t ? (t | bits) : 0;
   }
@@ -609,7 +650,8 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
     return dta_gemm_w4_launch(g, a_t, b_t, tile == k64::kW4S, st);
   }
   bool buf = (tile & k64::kFlatDma) == 0;
-  tile &= ~(k64::kBufDma | k64::kFlatDma);
+  const bool stg = (tile & k64::kNoStg) == 0 && c32 == nullptr && !(epi == k64::EPI_GELU && c2 != nullptr);
+  tile &= ~(k64::kBufDma | k64::kFlatDma | k64::kNoStg);
   if (buf) {  // 32-bit offsets: every byte of A and B within 2 GiB of its base (descriptor range)
     const int64_t a_bytes = 2 * (a_t ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
     const int64_t b_bytes = 2 * (b_t ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);
@@ -643,10 +685,10 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   g.tiles_m = M / k64::tile_bm(tile);
   g.tiles_n = N / k64::tile_bn(tile);
   switch (tile) {
-    case 1: return k64::launch_t<256, 256, 4>(g, a_t, b_t, ph, buf, st);
-    case 2: return k64::launch_t<256, 128, 4>(g, a_t, b_t, ph, buf, st);
-    case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, ph, buf, st);
-    default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, ph, buf, st);
+    case 1: return k64::launch_t<256, 256, 4>(g, a_t, b_t, ph, buf, stg, st);
+    case 2: return k64::launch_t<256, 128, 4>(g, a_t, b_t, ph, buf, stg, st);
+    case 3: return k64::launch_t<128, 128, 2>(g, a_t, b_t, ph, buf, stg, st);
+    default: return k64::launch_t<128, 256, 4>(g, a_t, b_t, ph, buf, stg, st);
   }
 }
 
