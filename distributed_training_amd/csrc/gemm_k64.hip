@@ -143,14 +143,15 @@ struct Cfg {
   static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
 };
 
-// STG (256 x 256 tiles, one bf16 output): the epilogue goes through the LDS as a whole 256 x 256 bf16 tile
-// image (the 128 KiB the K loop used) and leaves as whole 512-B rows -- instead of one 8-B store per lane per
-// fragment (16 rows x 32 B per instruction).  csrc/gemm_w4.hip's staged epilogue measured 10-15 % faster
-// than its per-fragment form.
+// STG (one bf16 output): the epilogue goes through the LDS as a whole BM x BN bf16 tile image (in the LDS
+// the K loop used: the image is at most its size) and leaves as whole 2 BN-byte rows -- instead of one 8-B
+// store per lane per fragment (16 rows x 32 B per instruction).  Measured (scripts/bench_w4.py, 256 x 256):
+// Llama o-proj forward 204.6 -> 188.6 us, LM head forward 6110 -> 5806 us (hipBLASLt 5830), GPT-2 qkv forward
+// 59.2 -> 44.8 us.
 template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false>
 __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
-  static_assert(!STG || (BM == 256 && BN == 256), "staged epilogue: 256 x 256 tiles (the tile image fills the LDS)");
+  static_assert(!STG || BM * BN * 2 <= 2 * Cfg<BM, BN, WC, AT, BT>::BUF, "staged epilogue: the tile image fits the LDS");
   using C = Cfg<BM, BN, WC, AT, BT>;
   constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
   constexpr bool STAG = WC == 4;  // two waves per SIMD: stagger the halves
@@ -458,7 +459,8 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment ----
   if constexpr (STG) {
-    // tile image: row r at 512 r, its 16-B chunk c at c ^ (r & 31)
+    // tile image: row r at 2 BN r, its 16-B chunk c (CPR per row) at c ^ (r % CPR)
+    constexpr int RB = 2 * BN, CPR = BN / 8, RPI = 64 / CPR;  // row bytes, chunks per row, rows per store
     bar();  // every wave's last fragment reads and DMA are done: the LDS is free
 #pragma unroll
     for (int i = 0; i < 2 * NTH; ++i) {
@@ -471,15 +473,15 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
         const int mh = j / MTH, jj = j % MTH;
         const int ml = mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
         const bf16x4 v = val4(g, m0 + ml, n0 + nl, acc[i][j], bv, 0);
-        *reinterpret_cast<bf16x4*>(lds + ml * 512 + 16 * ((nl >> 3) ^ (ml & 31)) + 8 * ((nl >> 2) & 1)) = v;
+        *reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ (ml % CPR)) + 8 * ((nl >> 2) & 1)) = v;
       }
     }
     lgkm0();
     bar();
 #pragma unroll
-    for (int r = 0; r < 256 / (2 * NW); ++r) {
-      const int row = wave * (256 / NW) + 2 * r + (lane >> 5), c = lane & 31;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * 512 + 16 * (c ^ (row & 31)));
+    for (int r = 0; r < BM / (RPI * NW); ++r) {
+      const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
       *reinterpret_cast<bf16x8*>(g.c + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) = v;
     }
     return;
@@ -518,13 +520,17 @@ __global__ void __launch_bounds__(512) gemm_k64_group_kernel(GroupArgs ga) {
   k64_body<256, 256, 4, true, true, 2, BUF, true, true>(ga.p[q], t - ga.tile_start[q]);
 }
 
-// stg: the staged epilogue (256 x 256, two-phase, buffer DMA, one bf16 output)
+// stg: the staged epilogue (buffer DMA, one bf16 output)
 template <int BM, int BN, int WC, bool AT, bool BT, bool BUF>
 static hipError_t launch(const Args& g, int ph, bool stg, hipStream_t st) {
-  if constexpr (BM == 256 && BN == 256 && BUF) {
-    if (ph == 2 && stg) {
-      hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF, true>), dim3(g.tiles_m * g.tiles_n),
-                         dim3(128 * WC), 0, st, g);
+  if constexpr (BUF) {
+    if (stg) {
+      if (ph == 2)
+        hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF, true>), dim3(g.tiles_m * g.tiles_n),
+                           dim3(128 * WC), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 4, BUF, true>), dim3(g.tiles_m * g.tiles_n),
+                           dim3(128 * WC), 0, st, g);
       return hipGetLastError();
     }
   }

@@ -226,22 +226,23 @@ def test_gemm_w4_staged_epilogue_exact(a_t, b_t, M, N, K, tile):
     assert torch.equal(got.float().cpu(), want), (a_t, b_t, M, N, K)
 
 
+@pytest.mark.parametrize("tile", [1, 3, 5, 6, 7, 8])
 @pytest.mark.parametrize("a_t,b_t", LAYOUTS)
-def test_gemm64_staged_epilogue_exact(a_t, b_t):
-    """Tile 5 (256 x 256, two-phase) with one bf16 output takes the LDS-staged epilogue (the whole tile
-    image through the LDS, whole 512-B row stores); tile 5 | 128 forces the per-fragment form: both exact
-    against fp32 on small integers whose sums stay exactly representable in bf16, on a grid of many tiles."""
+def test_gemm64_staged_epilogue_exact(a_t, b_t, tile):
+    """Every k64 tile with one bf16 output takes the LDS-staged epilogue (the whole tile image through the
+    LDS, whole-row stores); tile | 128 forces the per-fragment form: both exact against fp32 on small
+    integers whose sums stay exactly representable in bf16, on a grid of many tiles."""
     from distributed_training_amd.ops import native
 
     M, N, K = 1024, 1536, 512
-    gen = torch.Generator().manual_seed(77 + 2 * a_t + b_t)
+    gen = torch.Generator().manual_seed(77 + 4 * tile + 2 * a_t + b_t)
     a = torch.randint(-1, 2, (K, M) if a_t else (M, K), generator=gen).float()
     b = torch.randint(-1, 2, (K, N) if b_t else (N, K), generator=gen).float()
     a = a * (torch.rand(a.shape, generator=gen) < 0.25)
     want = (a.t() if a_t else a) @ (b if b_t else b.t())
     assert want.abs().max() <= 256
-    for tile in (5, 5 | 128):
+    for t in (tile, tile | 128):
         out = torch.full((M, N), float("nan"), device="cuda").bfloat16()
-        got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=tile)
+        got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=t)
         torch.cuda.synchronize()
-        assert torch.equal(got.float().cpu(), want), (tile, a_t, b_t)
+        assert torch.equal(got.float().cpu(), want), (t, a_t, b_t)
