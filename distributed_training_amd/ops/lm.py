@@ -231,7 +231,7 @@ _GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 
 GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "deferred_wgrad": 0, "group_launches": 0}
 
 
-def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 3, reps: int = 4) -> Dict[int, float]:
+def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 5, reps: int = 4) -> Dict[int, float]:
     """Median per-call time of each candidate, rounds interleaved (clock / cache state
     shared fairly; the first call of each -- code object load, library heuristics -- untimed)."""
     for fn in fns.values():
@@ -297,7 +297,7 @@ K64 = 10
 # csrc/gemm_k64.hip tiles the dispatcher times: 5 / 6 / 8 = the 8-wave 256x256 / 256x128 / 128x256
 # tiles with the two-phase K loop (3-11 % faster than their four-phase forms 1 / 2 / 4 at every
 # GPT-2 and Llama shape: profiles/gemm_k64_vs_hipblaslt.txt), 3 / 7 = 128x128 in both forms
-K64_TILES = (9, 5, 6, 3, 7, 8)  # 9: csrc/gemm_w4.hip (4 waves, 256 x 256, intra-wave read / MFMA overlap)
+K64_TILES = (10, 5, 6, 3, 7, 8)  # 10: csrc/gemm_w4.hip (4 waves, 256 x 256; staged epilogue where one bf16 output)
 # a hand-written candidate wins a shape when it is at most this much slower than the library (1.0: the
 # faster one; a 2 % preference measured 0.25 ms/step slower on the GPT-2 DDP step, same-box A/B)
 _PREFER_DTA = 1.0
