@@ -37,15 +37,20 @@ import os
 import sys
 import time
 from pathlib import Path
-from typing import Any
+from typing import TYPE_CHECKING, Any, Callable, Optional, Tuple
+
+if TYPE_CHECKING:  # annotations only: torch is imported inside the functions (fast --help)
+    import torch
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "samples/sec (whole node) + DDP scaling efficiency, toy MLP at 1/2/4/8 MI355X"
+# (step_fn(n): run n steps, finish(): last loss, the communicator or None)
+Runner = Tuple[Callable[[int], None], Callable[[], float], Optional[object]]
 
 
-def parse() -> Any:
+def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2048)
@@ -65,7 +70,7 @@ def parse() -> Any:
     return ap.parse_args()
 
 
-def setup_dist(args: Any) -> Any:
+def setup_dist(args: argparse.Namespace) -> Tuple[int, int, "torch.device"]:
     import torch
     import torch.distributed as dist
 
@@ -87,7 +92,7 @@ def setup_dist(args: Any) -> Any:
     return rank, ws, dev
 
 
-def build(args: Any, dev: Any, ws: Any) -> Any:
+def build(args: argparse.Namespace, dev: "torch.device", ws: int) -> Tuple[Any, "torch.nn.Module", Any]:
     import torch
 
     from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
@@ -102,7 +107,7 @@ def build(args: Any, dev: Any, ws: Any) -> Any:
     return ds, model, loader
 
 
-def run_fused(args: Any, dev: Any, ws: Any) -> Any:
+def run_fused(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runner":
     import torch
 
     from distributed_training_amd.engine.fused_mlp import FusedMLPProgram, fused_eligible
@@ -120,10 +125,10 @@ def run_fused(args: Any, dev: Any, ws: Any) -> Any:
     prog = FusedMLPProgram(model, opt, loader, comm, loss="mse", graph_steps=args.graph_steps,
                            own_tiles=args.own_tiles or None, allreduce_world1=bool(args.allreduce_world1))
 
-    def step_fn(n: Any) -> None:
+    def step_fn(n: int) -> None:
         prog.run_steps(n)
 
-    def finish() -> Any:
+    def finish() -> float:
         prog.store_to_module()
         return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
 
@@ -135,7 +140,7 @@ def run_fused(args: Any, dev: Any, ws: Any) -> Any:
     return step_fn, finish, comm
 
 
-def run_fused_linear(args: Any, dev: Any, ws: Any) -> Any:
+def run_fused_linear(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runner":
     """The reference's default workload (src/distributed_trainer.py:160-165, 199-200):
     nn.Linear(20, 1), F.cross_entropy on float targets, fp32, SGD, DDP -- on the fused
     Linear step program (csrc/linear_step.hip)."""
@@ -161,10 +166,10 @@ def run_fused_linear(args: Any, dev: Any, ws: Any) -> Any:
         raise SystemExit(f"fused Linear path not applicable: {why}")
     prog = FusedLinearProgram(model, opt, loader, comm, loss="cross_entropy")
 
-    def step_fn(n: Any) -> None:
+    def step_fn(n: int) -> None:
         prog.run_steps(n)
 
-    def finish() -> Any:
+    def finish() -> float:
         prog.store_to_module()
         return float(prog.last_losses(1)[0].item()) if prog.launched else float("nan")
 
@@ -172,7 +177,7 @@ def run_fused_linear(args: Any, dev: Any, ws: Any) -> Any:
     return step_fn, finish, comm
 
 
-def run_generic(args: Any, dev: Any, ws: Any) -> Any:
+def run_generic(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runner":
     import torch
     import torch.nn.functional as F
 
@@ -186,7 +191,7 @@ def run_generic(args: Any, dev: Any, ws: Any) -> Any:
     opt = FusedSGD(ddp.parameters(), lr=args.lr)
     state = {"it": None, "epoch": 0, "loss": None}
 
-    def next_batch() -> Any:
+    def next_batch() -> Tuple["torch.Tensor", "torch.Tensor"]:
         while True:
             if state["it"] is None:
                 loader.sampler.set_epoch(state["epoch"])
@@ -197,7 +202,7 @@ def run_generic(args: Any, dev: Any, ws: Any) -> Any:
                 state["it"] = None
                 state["epoch"] += 1
 
-    def step_fn(n: Any) -> None:
+    def step_fn(n: int) -> None:
         for _ in range(n):
             x, y = next_batch()
             opt.zero_grad()
@@ -208,13 +213,13 @@ def run_generic(args: Any, dev: Any, ws: Any) -> Any:
             opt.step()
             state["loss"] = loss
 
-    def finish() -> Any:
+    def finish() -> float:
         return float(state["loss"].item()) if state["loss"] is not None else float("nan")
 
     return step_fn, finish, comm
 
 
-def run_torch(args: Any, dev: Any, ws: Any) -> Any:
+def run_torch(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runner":
     """Stock PyTorch-ROCm with the reference's loop (src/distributed_trainer.py:160-183)."""
     import torch
     import torch.nn.functional as F
@@ -235,7 +240,7 @@ def run_torch(args: Any, dev: Any, ws: Any) -> Any:
     loader = DataLoader(ds, batch_size=args.batch, pin_memory=True, shuffle=False, sampler=sampler)
     state = {"it": None, "epoch": 0, "loss": None}
 
-    def next_batch() -> Any:
+    def next_batch() -> Tuple["torch.Tensor", "torch.Tensor"]:
         while True:
             if state["it"] is None:
                 sampler.set_epoch(state["epoch"])
@@ -246,7 +251,7 @@ def run_torch(args: Any, dev: Any, ws: Any) -> Any:
                 state["it"] = None
                 state["epoch"] += 1
 
-    def step_fn(n: Any) -> None:
+    def step_fn(n: int) -> None:
         for _ in range(n):
             x, y = next_batch()
             x = x.to(dev)
@@ -262,7 +267,7 @@ def run_torch(args: Any, dev: Any, ws: Any) -> Any:
             opt.step()
             state["loss"] = loss
 
-    def finish() -> Any:
+    def finish() -> float:
         return float(state["loss"].item()) if state["loss"] is not None else float("nan")
 
     return step_fn, finish, None

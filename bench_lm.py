@@ -20,10 +20,13 @@ import os
 import sys
 import time
 from pathlib import Path
-from typing import TYPE_CHECKING, Any, Optional
+from typing import TYPE_CHECKING, Any, Optional, Tuple, Union
 
 if TYPE_CHECKING:
     import torch
+
+    from distributed_training_amd.models.gpt2 import GPT2Config
+    from distributed_training_amd.models.llama import LlamaConfig
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -31,7 +34,7 @@ sys.path.insert(0, str(ROOT))
 PEAK_BF16 = 2.5e15  # dense bf16 MFMA peak per MI355X
 
 
-def parse() -> Any:
+def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--model", default="gpt2", choices=["gpt2", "llama3_8b", "llama_1b", "llama_tiny"])
@@ -56,7 +59,7 @@ def parse() -> Any:
     return ap.parse_args()
 
 
-def model_cfg(name: str, layers: Any) -> Any:
+def model_cfg(name: str, layers: int) -> Union["GPT2Config", "LlamaConfig"]:
     from distributed_training_amd.models.gpt2 import GPT2Config
     from distributed_training_amd.models.llama import LlamaConfig
 
@@ -134,7 +137,7 @@ def main() -> None:
         opt = FusedAdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1)
         overlap_opt = args.overlap_opt and wrapped.overlap_optimizer(opt)
 
-        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> Any:
+        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
             return lm.cross_entropy(logits.reshape(-1, logits.shape[-1]), y.reshape(-1))
     else:
         import torch.nn.functional as F
@@ -157,7 +160,7 @@ def main() -> None:
                             mixed_precision=MixedPrecision(param_dtype=torch.bfloat16, reduce_dtype=torch.bfloat16))
         opt = torch.optim.AdamW(wrapped.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1, fused=True)
 
-        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> Any:
+        def loss_fn(logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
             return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), y.reshape(-1))
 
     nb = data.shape[0] // args.batch
@@ -196,7 +199,7 @@ def main() -> None:
         # its construction runs 3 eager warm-up steps and the capture (untimed, before the warm-up below)
         from distributed_training_amd.engine.step_graph import GraphedStep
 
-        def gstep(xb: Any) -> Any:
+        def gstep(xb: torch.Tensor) -> torch.Tensor:
             opt.zero_grad(set_to_none=True)
             loss = wrapped(xb[:, :-1], xb[:, 1:])
             loss.backward()
@@ -302,28 +305,31 @@ def _patch_torch_ops() -> None:
 
     from distributed_training_amd.ops import lm
 
-    def attention(q: torch.Tensor, k: torch.Tensor, v: Any, causal: bool = True, scale: Optional[float] = None) -> Any:
+    def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
+                  scale: Optional[float] = None) -> torch.Tensor:
         H, Hkv = q.shape[2], k.shape[2]
         qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
         return F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale,
                                               enable_gqa=H != Hkv).transpose(1, 2)
 
-    def attention_packed(qkv: torch.Tensor, n_head: Any, n_kv_head: Any, causal: bool = True,
-                         scale: Optional[float] = None, rope: Any = None) -> Any:
+    def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: bool = True,
+                         scale: Optional[float] = None,
+                         rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
         q, k, v = lm._split_qkv(qkv, n_head, n_kv_head)
         if rope is not None:
             q, k = lm.rope_reference(q, *rope), lm.rope_reference(k, *rope)
         return attention(q, k, v, causal, scale)
 
-    def add_ln(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Any:
+    def add_ln(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+               eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
         xn = x + res
         return xn, F.layer_norm(xn, (xn.shape[-1],), w, b, eps)
 
-    def add_rms(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Any:
+    def add_rms(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
         xn = x + res
         return xn, F.rms_norm(xn, (xn.shape[-1],), w, eps)
 
-    def linear_ce(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> Any:
+    def linear_ce(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
         logits = F.linear(x, w)
         return F.cross_entropy(logits.reshape(-1, logits.shape[-1]).float(), target.reshape(-1),
                                ignore_index=ignore_index)
