@@ -1,7 +1,8 @@
 // W4: the 4-wave 256 x 256 bf16 GEMM tile with INTRA-wave read / MFMA overlap, NT layout
 // (C[M, N] = alpha * A[M, K] B[N, K]^T (+ bias, epilogue)): the forward projections x W^T of the
 // transformer blocks and the LM head -- SURVEY.md N07, nn.Linear at src/distributed_trainer.py:162,199
-// scaled to the GPT-2 / Llama configs.  Dispatched as tile id 9 of csrc/gemm_k64.hip's entry point.
+// scaled to the GPT-2 / Llama configs.  Dispatched as tile ids 9 (per-fragment epilogue) / 10 (LDS-staged)
+// of csrc/gemm_k64.hip's entry point; ops/lm.py times tile 10 against the k64 tiles and hipBLASLt per shape.
 #include "gemm_epi.h"
 
 #include <type_traits>
@@ -18,12 +19,12 @@ namespace k64 {
 // own LDS reads and DMA issue between its own MFMAs:
 //  * fragments double-buffered in registers at the 32-deep half-step (kk): while the 64 MFMAs of
 //    half kk = 0 run, the 16 ds_read_b128 of half kk = 1 are issued between them (one per 4 MFMAs);
-//    while half 1's MFMAs run, the 16 LDS-DMA pieces of K-tile t + 2 and then the 16 reads of K-tile
+//    while half 1's MFMAs run, the 16 LDS-DMA pieces of K-tile t + 2 and the 16 reads of K-tile
 //    t + 1's half 0 are issued between them -- no lgkmcnt(0) between a read and unrelated MFMAs;
 //  * two LDS images (66 KiB each, K-tile t in image t & 1), filled by buffer_load ... lds two K-tiles
-//    ahead, the pieces spread over the MFMAs (below); barriers after the wave's last read of a
-//    (half) image (it may be refilled) and after the counted vmcnt that retires K-tile t + 1's pieces
-//    (its reads may start): the vmcnt is never 0 in the loop;
+//    ahead, the pieces spread over the MFMAs (below); two barriers per K-tile: after the wave's last read
+//    of an image (it may be refilled) and after the counted vmcnt that retires K-tile t + 1's pieces (its
+//    reads may start): the vmcnt is never 0 in the loop;
 //  * rows of A / B past M / N are CLAMPED in the DMA source (the duplicated rows' accumulators are
 //    never stored): 256-wide tiles cover N = 50304 (the GPT-2 head) with a predicated epilogue;
 //  * padded-piece K-major images (conflict-free ds_read_b128 fragment reads, in-order DMA sources),
