@@ -508,9 +508,35 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     tile_store(kt, KVs[0], tid);
     tile_store(vt, KVs[1], tid);
   }
+  // D = 128 (one wave per SIMD): dK^T / dV^T accumulate in AGPRs through inline-asm MFMAs (this file's
+  // MFMAs are otherwise in the VGPR
+  // form): 128 (D = 128) fewer arch VGPRs, which is what lets the wave keep its 32 keys' K and V fragments
+  // in registers below instead of re-reading them from LDS for every 32-query tile (a third of the
+  // slice's LDS reads).  The compiler does not know the asm statements are MFMAs: the accumulators are
+  // pinned through empty asm after wait states where they are written by VALU (the zeros) and before
+  // they are read (the epilogue), as in csrc/gemm_w4.hip.
   f32x16 dvacc[NDT], dkacc[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) dvacc[dt] = dkacc[dt] = splat16(0.f);
+  constexpr bool KREG = D == 128;  // (D = 64 runs two waves per SIMD: its register budget keeps the LDS form)
+  if constexpr (KREG) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+a"(dvacc[dt]), "+a"(dkacc[dt]));
+  }
+  auto mma_acc = [](f32x16& acc, const bf16x8& x, const bf16x8& y) {
+    if constexpr (KREG) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(x), "v"(y));
+    else acc = mfma32x32x16(x, y, acc);
+  };
+  bf16x8 kf[KREG ? NKS : 1], vf[KREG ? NKS : 1];  // this wave's 32 keys: B operands of S = Q.K^T, dP = dO.V^T
+  if constexpr (KREG) {
+    __syncthreads();  // the K / V tile images are complete
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      kf[ks] = row_frag<D>(KVs[0], wave * 32 + r32, ks, hh);
+      vf[ks] = row_frag<D>(KVs[1], wave * 32 + r32, ks, hh);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  }
 
   const int qstart = CAUSAL ? kblk0 : 0;
   const int nslice = (a.S - qstart + BM - 1) / BM;
@@ -581,7 +607,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       }
       if constexpr (k < NA) {
         f[0] = row_frag<D>((k & 1) ? Db : Qb, qt * 32 + r32, k >> 1, hh);
-        f[1] = row_frag<D>(KVs[k & 1], wave * 32 + r32, k >> 1, hh);
+        if constexpr (!KREG) f[1] = row_frag<D>(KVs[k & 1], wave * 32 + r32, k >> 1, hh);
       } else {
         constexpr int cc = k - NA, st = (cc >> 1) / NDT, dt = (cc >> 1) % NDT;
         f[0] = tr_frag<D>((cc & 1) ? Qb : Db, qt * 32, dt * 32, st, lane);
@@ -591,8 +617,13 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       constexpr int o = decltype(oc)::value, qt = o / NOP, k = o % NOP;
       const bf16x8(&f)[2] = ring[o % RING];
       if constexpr (k < NA) {
-        if (k & 1) dp = mfma32x32x16(f[0], f[1], dp);
-        else s = mfma32x32x16(f[0], f[1], s);
+        if constexpr (KREG) {
+          if (k & 1) dp = mfma32x32x16(f[0], vf[k >> 1], dp);
+          else s = mfma32x32x16(f[0], kf[k >> 1], s);
+        } else {
+          if (k & 1) dp = mfma32x32x16(f[0], f[1], dp);
+          else s = mfma32x32x16(f[0], f[1], s);
+        }
         if constexpr (k == NA - 1) {
           const int q0 = q0s + qt * 32;
           // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate
@@ -616,11 +647,13 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
               pb[st][j] = f2bf(s[8 * st + j]);
               db[st][j] = f2bf(dp[8 * st + j]);
             }
+          // pb / db are VALU results read by the asm MFMAs below: wait states the compiler cannot know to add
+          if constexpr (KREG) asm volatile("s_nop 4" ::: "memory");
         }
       } else {
         constexpr int cc = k - NA, st = (cc >> 1) / NDT, dt = (cc >> 1) % NDT;
-        if constexpr (cc & 1) dkacc[dt] = mfma32x32x16(f[0], db[st], dkacc[dt]);
-        else dvacc[dt] = mfma32x32x16(f[0], pb[st], dvacc[dt]);
+        if constexpr (cc & 1) mma_acc(dkacc[dt], f[0], db[st]);
+        else mma_acc(dvacc[dt], f[0], pb[st]);
       }
     };
     static_for<PF>([&](auto oc) { issue(oc); });
@@ -639,6 +672,13 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     }
   } else {
     for (int it = 0; it < total; ++it) slice_it(it, sA);
+  }
+  // the last MFMAs' results are still in the matrix pipe: wait states, then every accumulator through an
+  // empty asm (the epilogue's reads depend on those outputs)
+  if constexpr (KREG) {
+    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) asm volatile("" : "+a"(dvacc[dt]), "+a"(dkacc[dt]));
   }
   // ---- epilogue: dK = (dK^T)^T * scale, dV = (dV^T)^T ----
   if (key < a.S) {
