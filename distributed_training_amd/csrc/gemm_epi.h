@@ -84,6 +84,22 @@ __device__ __forceinline__ bf16x4 val4(const Args& g, int m, int n, const f32x4&
   return pk4_bf16(v[0], v[1], v[2], v[3]);
 }
 
+// val4 of the EPI_DGELU / EPI_RES epilogues with the four res values given (read by the caller: the
+// LDS-staged epilogue of csrc/gemm_k64.hip stages the res tile with whole-row loads first)
+__device__ __forceinline__ bf16x4 val4_res(const Args& g, const f32x4& acc, const float (&bv)[4], const bf16x4 r4) {
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
+  if (g.epi == EPI_DGELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_fast(bf2f(r4[r]));
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = bf2f(f2bf(v[r])) + bf2f(r4[r]);
+  }
+  return pk4_bf16(v[0], v[1], v[2], v[3]);
+}
+
 __device__ __forceinline__ void store4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4]) {
   float v[4];
 #pragma unroll

@@ -246,3 +246,37 @@ def test_gemm64_staged_epilogue_exact(a_t, b_t, tile):
         got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out, tile=t)
         torch.cuda.synchronize()
         assert torch.equal(got.float().cpu(), want), (t, a_t, b_t)
+
+
+@pytest.mark.parametrize("tile", [1, 3, 5, 6, 7, 8])
+def test_gemm64_staged_fused_epilogues_bitwise(tile):
+    """The staged epilogue of the fused forms -- GELU dual store (two passes through the LDS image),
+    x gelu'(res) and + res (the res tile staged with whole-row loads, replaced in place) -- bit-identical
+    to the per-fragment epilogue (tile | 128), with bias and alpha; a res whose row stride is not a
+    multiple of 8 takes the per-fragment path and still agrees."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    gen = torch.Generator().manual_seed(31 + tile)
+    M, N, K = 1024, 1536, 384
+    x = torch.randn(M, K, generator=gen).bfloat16().cuda()
+    w = (torch.randn(N, K, generator=gen) * 0.1).bfloat16().cuda()
+    wn = (torch.randn(K, N, generator=gen) * 0.1).bfloat16().cuda()
+    bias = torch.randn(N, generator=gen).bfloat16().cuda()
+    res = torch.randn(M, N, generator=gen).bfloat16().cuda()
+    res_odd = torch.randn(M, N + 4, generator=gen).bfloat16().cuda()[:, :N]  # row stride N + 4
+
+    def both(fn):
+        a, b = fn(tile), fn(tile | 128)
+        torch.cuda.synchronize()
+        for u, v in zip(a, b):
+            assert torch.equal(u, v), tile
+        return a
+
+    h, act = both(lambda t: C.gemm64(x, w, bias=bias, epi=2, out2=torch.empty(M, N, dtype=torch.bfloat16, device="cuda"),
+                                     tile=t))
+    torch.testing.assert_close(act.float(), F.gelu(h.float(), approximate="tanh"), rtol=1.6e-2, atol=1e-2)
+    both(lambda t: C.gemm64(x, w, alpha=0.5, bias=bias, epi=32, res=res, tile=t))
+    both(lambda t: C.gemm64(x, w, epi=32, res=res_odd, tile=t))
+    both(lambda t: C.gemm64(x, wn, False, True, epi=16, res=res, tile=t))
+    both(lambda t: C.gemm64(x, wn, False, True, bias=bias, epi=16, res=res_odd, tile=t))
