@@ -450,8 +450,12 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
     check_bf16_2d(*dres, "dres");
     TORCH_CHECK(dres->numel() == x.numel(), "norm_bwd: residual grad shape mismatch");
   }
-  // ~512 workgroups (fills 256 CUs twice), a multiple of 4 rows each (one per wave)
-  const int rpb = (int)std::min<int64_t>(1024, std::max<int64_t>(4, ((N + 511) / 512 + 3) / 4 * 4));
+  // ~512 workgroups (fills 256 CUs twice), a multiple of 4 rows each (one per wave); wide rows
+  // (C % 2048 == 0: a workgroup per row, csrc/lm_ops.hip norm_bwd_wide_kernel) ~768 workgroups (three
+  // resident per CU at C = 4096)
+  const int rpb = C % 2048 == 0 && C <= 8192
+                      ? (int)std::min<int64_t>(1024, std::max<int64_t>(1, (N + 767) / 768))
+                      : (int)std::min<int64_t>(1024, std::max<int64_t>(4, ((N + 511) / 512 + 3) / 4 * 4));
   const int64_t nblk = (N + rpb - 1) / rpb;
   auto f32 = x.options().dtype(torch::kFloat32);
   auto dwp = torch::empty({nblk, C}, f32);

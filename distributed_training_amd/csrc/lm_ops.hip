@@ -184,6 +184,104 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// Wide rows (C a multiple of 2048: Llama's 4096): one 256-thread workgroup per row, NVL = C / 2048
+// 16-byte vectors per lane -- the one-wave-per-row form above needs C / 64 fp32 values of x-hat and
+// g per lane plus the prefetched row (512 registers and scratch spills at C = 4096, one wave per
+// SIMD).  The block walks its rows with the next row's loads in flight; the two per-row sums cross
+// the four waves through a double-buffered LDS slot (one barrier per row); each thread owns its
+// columns' dgamma / dbeta partials (no cross-wave reduction).
+template <int NVL, bool RMS>
+__global__ void __launch_bounds__(256) norm_bwd_wide_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ w, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, bf16* __restrict__ dx,
+                                                            float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                            int64_t N, int C, int rows_per_block,
+                                                            const bf16* __restrict__ dres) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float red[2][4][2];
+  float dwacc[NVL][8], dbacc[NVL][8];
+  bf16x8 wb[NVL];  // (kept packed)
+#pragma unroll
+  for (int i = 0; i < NVL; ++i) {
+    wb[i] = *reinterpret_cast<const bf16x8*>(w + (i * 256 + tid) * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[i][j] = dbacc[i][j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rend = min(r0 + rows_per_block, N);
+  bf16x8 xn[NVL], dn[NVL], rn[NVL];
+  float mun = 0.f, rsn = 0.f;
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) {
+      const int64_t o = row * C + (i * 256 + tid) * 8;
+      xn[i] = *reinterpret_cast<const bf16x8*>(x + o);
+      dn[i] = *reinterpret_cast<const bf16x8*>(dy + o);
+      if (dres) rn[i] = *reinterpret_cast<const bf16x8*>(dres + o);
+    }
+    mun = RMS ? 0.f : mean[row];
+    rsn = rstd[row];
+  };
+  if (r0 < rend) fetch(r0);
+  int par = 0;
+  for (int64_t row = r0; row < rend; ++row, par ^= 1) {
+    const float mu = mun, rs = rsn;
+    bf16x8 xc[NVL], dc[NVL], rc[NVL];
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) {
+      xc[i] = xn[i];
+      dc[i] = dn[i];
+      if (dres) rc[i] = rn[i];
+    }
+    if (row + 1 < rend) fetch(row + 1);
+    float xh[NVL][8], g[NVL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = bf2f(xc[i][j]), dv = bf2f(dc[i][j]);
+        xh[i][j] = (xv - mu) * rs;
+        g[i][j] = dv * bf2f(wb[i][j]);
+        s1 += g[i][j];
+        s2 += g[i][j] * xh[i][j];
+        dwacc[i][j] += dv * xh[i][j];
+        dbacc[i][j] += dv;
+      }
+    if (!RMS) s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      red[par][wave][0] = s1;
+      red[par][wave][1] = s2;
+    }
+    __syncthreads();
+    const float m1 = RMS ? 0.f : (red[par][0][0] + red[par][1][0] + red[par][2][0] + red[par][3][0]) / C;
+    const float m2 = (red[par][0][1] + red[par][1][1] + red[par][2][1] + red[par][3][1]) / C;
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rs * (g[i][j] - m1 - xh[i][j] * m2);
+      if (dres) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += bf2f(rc[i][j]);
+      }
+      store8(dx + row * C + (i * 256 + tid) * 8, o);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NVL; ++i) {
+    float* pw = dw_part + (int64_t)blockIdx.x * C + (i * 256 + tid) * 8;
+    *reinterpret_cast<float4*>(pw) = make_float4(dwacc[i][0], dwacc[i][1], dwacc[i][2], dwacc[i][3]);
+    *reinterpret_cast<float4*>(pw + 4) = make_float4(dwacc[i][4], dwacc[i][5], dwacc[i][6], dwacc[i][7]);
+    if (!RMS) {
+      float* pb = db_part + (int64_t)blockIdx.x * C + (i * 256 + tid) * 8;
+      *reinterpret_cast<float4*>(pb) = make_float4(dbacc[i][0], dbacc[i][1], dbacc[i][2], dbacc[i][3]);
+      *reinterpret_cast<float4*>(pb + 4) = make_float4(dbacc[i][4], dbacc[i][5], dbacc[i][6], dbacc[i][7]);
+    }
+  }
+}
+
 // Column sums of one or two [nrows, C] partial sets (colsum_block): blocks
 // [0, ceil(C/32)) finish set 0, the rest set 1 (e.g. a norm's dw and db in one launch).
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part0, const float* __restrict__ part1,
@@ -577,6 +675,18 @@ static hipError_t norm_bwd_nv(int nv, const bf16* dy, const bf16* x, const bf16*
                               const float* rstd, bf16* dx, float* dwp, float* dbp, int64_t N, int C, int rpb,
                               const bf16* dres, hipStream_t st) {
   dim3 grid((unsigned)((N + rpb - 1) / rpb)), blk(256);
+  if (C % 2048 == 0 && C <= 8192) {  // wide rows: a workgroup per row (norm_bwd_wide_kernel)
+#define NW_(V) \
+  hipLaunchKernelGGL((norm_bwd_wide_kernel<V, RMS>), grid, blk, 0, st, dy, x, w, mean, rstd, dx, dwp, dbp, N, C, rpb, dres)
+    switch (C / 2048) {
+      case 1: NW_(1); break;
+      case 2: NW_(2); break;
+      case 3: NW_(3); break;
+      default: NW_(4); break;
+    }
+#undef NW_
+    return hipGetLastError();
+  }
 #define NB(V) \
   hipLaunchKernelGGL((norm_bwd_kernel<V, RMS>), grid, blk, 0, st, dy, x, w, mean, rstd, dx, dwp, dbp, N, C, rpb, dres)
   switch (nv) {

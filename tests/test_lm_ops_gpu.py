@@ -49,14 +49,17 @@ def test_attention_strided_qkv_views():
     assert _rel(o, ref) < 1e-2
 
 
-@pytest.mark.parametrize("C", [768, 4096, 200 * 8])
+@pytest.mark.parametrize("C,N", [(768, 37), (4096, 37), (200 * 8, 37), (2048, 1537), (4096, 1537), (6144, 300),
+                                 (8192, 769)])
 @pytest.mark.parametrize("rms", [False, True])
-def test_norms(C, rms):
+def test_norms(C, N, rms):
+    """LayerNorm / RMSNorm forward + backward vs fp32 autograd; C a multiple of 2048 takes the
+    workgroup-per-row backward (several rows per workgroup once N > 768)."""
     torch.manual_seed(2)
-    x = (torch.randn(37, C, device=DEV) * 3 + 1).bfloat16().requires_grad_()
+    x = (torch.randn(N, C, device=DEV) * 3 + 1).bfloat16().requires_grad_()
     w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
     b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
-    dy = torch.randn(37, C, device=DEV).bfloat16()
+    dy = torch.randn(N, C, device=DEV).bfloat16()
     y = lm.rms_norm(x, w) if rms else lm.layer_norm(x, w, b)
     y.backward(dy)
     xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
@@ -241,10 +244,10 @@ def test_packed_attention_with_rope(H, Hkv, D, rope):
     assert _rel(qkv.grad, ref_in.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N,C", [(300, 768), (1000, 4096)])
 @pytest.mark.parametrize("rms", [False, True])
-def test_add_norm_fused_residual(rms):
+def test_add_norm_fused_residual(rms, N, C):
     torch.manual_seed(4)
-    N, C = 300, 768
     x = torch.randn(N, C, device=DEV).bfloat16().requires_grad_()
     r = torch.randn(N, C, device=DEV).bfloat16().requires_grad_()
     w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
