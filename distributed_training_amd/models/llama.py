@@ -68,7 +68,7 @@ class Attention(nn.Module):
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         B, S, _ = x.shape
         # RoPE + GQA attention on the packed projection output (one packed dQKV in backward)
-        y = lm.attention_packed(self.wqkv(x), self.H, self.Hkv, causal=True, rope=(cos, sin))
+        y = lm.attention_packed(self.wqkv(x), self.H, self.Hkv, causal=True, rope=(cos, sin), rope_inplace=True)
         return self.wo(y.reshape(B, S, self.H * self.D))
 
 

@@ -87,17 +87,21 @@ def _split_qkv(qkv: torch.Tensor, H: int, Hkv: int) -> Tuple[torch.Tensor, torch
 class _PackedAttn(Function):
     """Attention straight on the fused QKV projection output [B, S, (H+2Hkv)*D]:
     q/k/v are strided views (no copies), optional RoPE is applied in place to
-    the q|k columns of one rotated copy, and backward writes dq/dk/dv into ONE
+    the q|k columns of one rotated copy (or of ``qkv`` itself with ``inplace``: the
+    caller owns the projection output and nothing else reads it -- the Linear
+    backward saves its input, not its output -- saving a 96 MB copy per Llama
+    layer), and backward writes dq/dk/dv into ONE
     packed gradient buffer -- autograd never has to zero-fill and add three
     slice gradients into the projection output's gradient."""
 
     @staticmethod
     def forward(ctx: Any, qkv: torch.Tensor, H: int, Hkv: int, causal: bool, scale: float, cos: torch.Tensor,
-                sin: torch.Tensor) -> torch.Tensor:
+                sin: torch.Tensor, inplace: bool = False) -> torch.Tensor:
         B, S, W = qkv.shape
         D = W // (H + 2 * Hkv)
         if cos is not None:
-            qkv = qkv.clone()
+            if not inplace:
+                qkv = qkv.clone()
             native().rope_(qkv.view(B, S, H + 2 * Hkv, D)[:, :, :H + Hkv], cos, sin, False, -1)
         q, k, v = _split_qkv(qkv, H, Hkv)
         o, lse = native().attn_fwd(q, k, v, bool(causal), float(scale), -1)
@@ -117,12 +121,14 @@ class _PackedAttn(Function):
         native().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, -1, dq, dk, dv)
         if has_rope:  # d(rope(x))/dx = inverse rotation
             native().rope_(dqkv.view(B, S, H + 2 * Hkv, D)[:, :, :H + Hkv], cos, sin, True, -1)
-        return dqkv, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
 
 
 def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: bool = True, scale: Optional[float] = None,
-                     rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
-    """``qkv`` [B, S, (H + 2 Hkv) D] -> attention output [B, S, H, D] (RoPE on q, k if given)."""
+                     rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, rope_inplace: bool = False) -> torch.Tensor:
+    """``qkv`` [B, S, (H + 2 Hkv) D] -> attention output [B, S, H, D] (RoPE on q, k if given).
+    ``rope_inplace``: rotate the q|k columns of ``qkv`` itself on GPU (the caller's projection output,
+    read by nothing else) instead of a rotated copy."""
     B, S, W = qkv.shape
     D = W // (n_head + 2 * n_kv_head)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -131,7 +137,7 @@ def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: boo
         cos, sin = cos.float(), sin.float()
     if qkv.is_cuda:
         _need_bf16(qkv)
-        return _PackedAttn.apply(qkv, n_head, n_kv_head, causal, scale, cos, sin)
+        return _PackedAttn.apply(qkv, n_head, n_kv_head, causal, scale, cos, sin, bool(rope_inplace))
     q, k, v = _split_qkv(qkv, n_head, n_kv_head)
     if rope is not None:
         q, k = rope_reference(q, cos, sin), rope_reference(k, cos, sin)
@@ -309,7 +315,7 @@ def gemm_candidates(M: int, N: int, K: int) -> list:
     return [K64 + t for t in K64_TILES if C.gemm64_tile(M, N, K, t)]
 
 
-def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]]) -> int:
+def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]], prefer: float = _PREFER_DTA) -> int:
     """Implementation for one (possibly fused) GEMM shape: ``cands`` maps implementation ids to
     callables computing the SAME fused result (0 = hipBLASLt + separate epilogue kernels); the
     fastest by interleaved timing (median of rounds), hand-written on near-ties (_PREFER_DTA).
@@ -332,7 +338,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
     else:
         times = _time_us(cands)
         best = min(dta, key=times.get)
-        c = best if 0 not in times or times[best] <= _PREFER_DTA * times[0] else 0
+        c = best if 0 not in times or times[best] <= prefer * times[0] else 0
     _GEMM_CHOICE[key] = c
     if mode == "auto":
         _save_cache()
@@ -404,7 +410,10 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
         for t in K64_TILES:
             if C.gemm64_tile(M, N, K, t):
                 cands[K64 + t] = (lambda t=t: run_k64(t))
-        impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands)
+        # the dual store must win by 15 %: its two output streams cost more inside the step than in
+        # the back-to-back timing (GPT-2 fc: 85.8 us in-step vs 69-76 us timed; hipBLASLt + GELU
+        # kernel 47.1 + 23.1 us in-step -- profiles/gpt2_ddp_1gpu_kernels_r4.txt, _r4c.txt)
+        impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands, prefer=0.85)
     if impl:
         GEMM_STATS["dta"] += 1
         return run_k64(impl - K64)

@@ -242,6 +242,11 @@ def test_packed_attention_with_rope(H, Hkv, D, rope):
     orf.backward(do.float())
     assert _rel(o, orf) < 1e-2
     assert _rel(qkv.grad, ref_in.grad) < 2e-2
+    if rope:  # in-place RoPE on an intermediate (the model's projection output): bit-identical
+        leaf = qkv.detach().clone().requires_grad_()
+        o2 = lm.attention_packed(leaf * 1, H, Hkv, causal=True, rope=(cos, sin), rope_inplace=True)
+        o2.backward(do)
+        assert torch.equal(o2, o) and torch.equal(leaf.grad, qkv.grad)
 
 
 @pytest.mark.parametrize("N,C", [(300, 768), (1000, 4096)])
