@@ -462,10 +462,12 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     // tile image: row r at 2 BN r, its 16-B chunk c (CPR per row) at c ^ (r % CPR).  The residual /
     // GELU-input tile (EPI_RES / EPI_DGELU) comes into the same image first with whole-row loads (instead
     // of one 8-B read per lane per fragment), each lane replacing its four values by the result in place
-    // (GPT-2 fc2 input gradient x gelu'(h): 78.1 -> 67.8 us).  The GELU dual store keeps the per-fragment
-    // epilogue: through the LDS in two passes it measured 76.8 vs 69.2 us (scripts/bench_fused_epi.py).
+    // (GPT-2 fc2 input gradient x gelu'(h): 78.1 -> 67.8 us).  The GELU dual store stages the rounded h and
+    // computes gelu(h) from each row chunk as it leaves (one pass: through the LDS twice it measured 76.8 vs
+    // 69.2 us per fragment, scripts/bench_fused_epi.py).
     constexpr int RB = 2 * BN, CPR = BN / 8, RPI = 64 / CPR;  // row bytes, chunks per row, rows per store
     const bool has_res = g.epi == EPI_DGELU || g.epi == EPI_RES;
+    const bool dual = g.epi == EPI_GELU && g.c2 != nullptr;
     bar();  // every wave's last fragment reads and DMA are done: the LDS is free
     if (has_res) {
 #pragma unroll
@@ -498,6 +500,12 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
       const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
       *reinterpret_cast<bf16x8*>(g.c + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) = v;
+      if (dual) {
+        const bf16x4 lo = pk4_bf16(gelu_fast(bf2f(v[0])), gelu_fast(bf2f(v[1])), gelu_fast(bf2f(v[2])), gelu_fast(bf2f(v[3])));
+        const bf16x4 hi = pk4_bf16(gelu_fast(bf2f(v[4])), gelu_fast(bf2f(v[5])), gelu_fast(bf2f(v[6])), gelu_fast(bf2f(v[7])));
+        *reinterpret_cast<bf16x8*>(g.c2 + (int64_t)(m0 + row) * g.ldc2 + n0 + 8 * c) =
+            bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
     }
     return;
   }
@@ -673,7 +681,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   bool buf = (tile & k64::kFlatDma) == 0;
   // staged: whole 16-B row chunks of c (and c2, res): 8-element row strides, 16-byte aligned bases
   auto rows16 = [](const void* p, int64_t ld) { return p == nullptr || (ld % 8 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0); };
-  const bool stg = (tile & k64::kNoStg) == 0 && c32 == nullptr && !(epi == k64::EPI_GELU && c2 != nullptr) && rows16(c, ldc) &&
+  const bool stg = (tile & k64::kNoStg) == 0 && c32 == nullptr && rows16(c, ldc) && rows16(c2, ldc2) &&
                    ((epi != k64::EPI_DGELU && epi != k64::EPI_RES) || rows16(res, ldr));
   tile &= ~(k64::kBufDma | k64::kFlatDma | k64::kNoStg);
   if (buf) {  // 32-bit offsets: every byte of A and B within 2 GiB of its base (descriptor range)

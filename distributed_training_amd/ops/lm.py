@@ -411,8 +411,9 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
             if C.gemm64_tile(M, N, K, t):
                 cands[K64 + t] = (lambda t=t: run_k64(t))
         # the dual store must win by 15 %: its two output streams cost more inside the step than in
-        # the back-to-back timing (GPT-2 fc: 85.8 us in-step vs 69-76 us timed; hipBLASLt + GELU
-        # kernel 47.1 + 23.1 us in-step -- profiles/gpt2_ddp_1gpu_kernels_r4.txt, _r4c.txt)
+        # the back-to-back timing (GPT-2 fc: per-fragment 85.8 us in-step vs 69-76 timed, staged 78-82
+        # vs 64.8; hipBLASLt + GELU kernel 47.1 + 23.1 us in-step -- profiles/gpt2_ddp_1gpu_kernels_r4.txt,
+        # _r4c.txt, _r4f.txt)
         impl = _pick("fwd_gelu" + ("b" if b is not None else ""), M, N, K, cands, prefer=0.85)
     if impl:
         GEMM_STATS["dta"] += 1
