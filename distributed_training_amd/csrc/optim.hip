@@ -101,7 +101,23 @@ __device__ __forceinline__ float4 load_g4(const bf16* g, int64_t i) {
 __device__ __forceinline__ float load_g1(const float* g, int64_t i) { return g[i]; }
 __device__ __forceinline__ float load_g1(const bf16* g, int64_t i) { return bf2f(g[i]); }
 
-template <typename GT>
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* a, int64_t i) {
+  if constexpr (NT) {
+    const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(a) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return reinterpret_cast<const float4*>(a)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* a, int64_t i, const float4 x) {
+  if constexpr (NT) __builtin_nontemporal_store(nt_f4{x.x, x.y, x.z, x.w}, reinterpret_cast<nt_f4*>(a) + i);
+  else reinterpret_cast<float4*>(a)[i] = x;
+}
+
+template <typename GT, bool NT = false>
 __global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, const GT* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         float* __restrict__ vmax, bf16* __restrict__ p_bf16,
@@ -113,19 +129,19 @@ __global__ void __launch_bounds__(256) flat_adam_kernel(float* __restrict__ p, c
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = h.vec ? (n >> 2) : 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 pp = ld4<NT>(p, i);
     float4 gg = load_g4(g, i);
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float4 mm = ld4<NT>(m, i);
+    float4 vv = ld4<NT>(v, i);
     float4 xx = make_float4(0.f, 0.f, 0.f, 0.f);
     if (vmax) xx = reinterpret_cast<float4*>(vmax)[i];
     pp.x = adam_one(pp.x, gg.x, &mm.x, &vv.x, &xx.x, bc1, bc2_sqrt, h);
     pp.y = adam_one(pp.y, gg.y, &mm.y, &vv.y, &xx.y, bc1, bc2_sqrt, h);
     pp.z = adam_one(pp.z, gg.z, &mm.z, &vv.z, &xx.z, bc1, bc2_sqrt, h);
     pp.w = adam_one(pp.w, gg.w, &mm.w, &vv.w, &xx.w, bc1, bc2_sqrt, h);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
+    st4<NT>(p, i, pp);
+    st4<NT>(m, i, mm);
+    st4<NT>(v, i, vv);
     if (vmax) reinterpret_cast<float4*>(vmax)[i] = xx;
     if (p_bf16) {
       bf16x4 o = {f2bf(pp.x), f2bf(pp.y), f2bf(pp.z), f2bf(pp.w)};
@@ -268,8 +284,10 @@ hipError_t dta_flat_adam(float* p, const void* g, int g_bf16, float* m, float* v
   auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) % a) == 0; };
   const int vec = al(p, 16) && al(g, g_bf16 ? 8 : 16) && al(m, 16) && al(v, 16) && al(vmax, 16) && al(p_bf16, 8);
   AdamHyper h{lr, beta1, beta2, eps, wd, grad_scale, adamw, maximize, amsgrad, vec};
+  // bf16 gradients (the mixed-precision engines): the fp32 master / m / v streams non-temporal -- 38.2-38.3 vs
+  // 38.9-39.5 ms on Llama-3 8B's 8.03 G parameters, equal at 2 G (scripts/bench_adam.py, profiles/adam_nt_r4.jsonl)
   if (g_bf16)
-    hipLaunchKernelGGL(flat_adam_kernel<bf16>, dim3(nb), dim3(256), 0, st, p,
+    hipLaunchKernelGGL((flat_adam_kernel<bf16, true>), dim3(nb), dim3(256), 0, st, p,
                        reinterpret_cast<const bf16*>(g), m, v, vmax, reinterpret_cast<bf16*>(p_bf16), n, step, h);
   else
     hipLaunchKernelGGL(flat_adam_kernel<float>, dim3(nb), dim3(256), 0, st, p,
