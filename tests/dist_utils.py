@@ -16,6 +16,20 @@ def free_port() -> int:
     return port
 
 
+def setup_env_on_free_port(env, attempts: int = 5):
+    """``env.setup()`` (one-rank rendezvous on 127.0.0.1) on a fresh free port, retried on a fresh port
+    when another process took the probed one before the store bound it (EADDRINUSE on a shared box)."""
+    for i in range(attempts):
+        os.environ["MASTER_PORT"] = str(free_port())
+        try:
+            env.setup()
+            return env
+        except dist.DistNetworkError as e:
+            if "EADDRINUSE" not in str(e) or i == attempts - 1:
+                raise
+    return env
+
+
 def _entry(rank, ws, port, fn, args, errq):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
                        "WORLD_SIZE": str(ws), "LOCAL_RANK": str(rank)})

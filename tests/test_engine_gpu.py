@@ -114,12 +114,10 @@ def test_trainer_end_to_end_gpu(tmp_path):
     from distributed_training_amd.ops.optim import FusedSGD
     from distributed_training_amd.parallel.env import DistributedEnvironment
 
-    from dist_utils import free_port
+    from dist_utils import setup_env_on_free_port
 
-    os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": str(free_port())})
-    env = DistributedEnvironment("cuda")
-    env.setup()
+    os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1"})
+    env = setup_env_on_free_port(DistributedEnvironment("cuda"))
     try:
         torch.manual_seed(0)
         ds = MyTrainDataset(512, 20, 1, seed=0)
@@ -154,12 +152,10 @@ def test_trainer_step_graph_matches_eager(tmp_path):
     from distributed_training_amd.ops.optim import FusedSGD
     from distributed_training_amd.parallel.env import DistributedEnvironment
 
-    from dist_utils import free_port
+    from dist_utils import setup_env_on_free_port
 
-    os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": str(free_port())})
-    env = DistributedEnvironment("cuda")
-    env.setup()
+    os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1"})
+    env = setup_env_on_free_port(DistributedEnvironment("cuda"))
     try:
         finals = []
         for graph in (False, True):

@@ -135,16 +135,14 @@ def test_trainer_default_config_uses_fused_linear(tmp_path):
     from distributed_training_amd.parallel.env import DistributedEnvironment
 
     os.environ.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1"})
-    from dist_utils import free_port
+    from dist_utils import setup_env_on_free_port
 
-    os.environ["MASTER_PORT"] = str(free_port())
     snap = tmp_path / "snap.pt"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cfg = compose(os.path.join(root, "conf"), "config",
                   ["train.total_epochs=3", f"train.snapshot_path={snap}", "train.loss=mse", "train.seed=0"],
                   runtime={"output_dir": str(tmp_path)})
-    env = DistributedEnvironment("cuda")
-    env.setup()
+    env = setup_env_on_free_port(DistributedEnvironment("cuda"))
     try:
         ds, model, opt = load_train_objs(cfg)
         tc = training_config_from(cfg, model)
