@@ -42,7 +42,7 @@ hipError_t dta_gemm_k64_wgrad_group(int, const void* const*, const int64_t*, con
                                     hipStream_t);
 int dta_gemm_k64_tile(int, int, int, int);
 hipError_t dta_gemm_k64(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, void*, int64_t, float*,
-                        int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t);
+                        int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t, const float*);
 size_t dta_linear_step_lds_bytes(int, int, int, int);
 int dta_linear_step_supported(int, int, int, int);
 
@@ -200,11 +200,13 @@ void check_out2d(const torch::Tensor& c, int64_t M, int64_t N, c10::ScalarType d
 
 // The 64-deep-stage GEMM (csrc/gemm_k64.hip).  C[M, N] = alpha * op(A) op(B)^T (+ bias) with epilogue
 // epi: 0 none, 2 GELU (out2 given: out = pre-activation h, out2 = gelu(h) -- both returned), 16 x gelu'(res),
-// 32 + res.  a: [M, K] (a_t: [K, M]); b: [N, K] (b_t: [K, N]).  Returns (out, out2 or None).
+// 32 + res.  a: [M, K] (a_t: [K, M]); b: [N, K] (b_t: [K, N]).  alpha_dev: an fp32 device scalar multiplying
+// alpha (a loss scale that stays on the GPU).  Returns (out, out2 or None).
 std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, bool b_t,
                                     c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> out2,
                                     bool out_f32, double alpha, c10::optional<torch::Tensor> bias, int64_t epi,
-                                    c10::optional<torch::Tensor> res, int64_t tile, int64_t stream) {
+                                    c10::optional<torch::Tensor> res, int64_t tile, int64_t stream,
+                                    c10::optional<torch::Tensor> alpha_dev) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm64: GPU tensors");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm64: bf16 operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm64: 2-D, unit inner stride");
@@ -249,10 +251,16 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
     rp = res->data_ptr();
     ldr = res->stride(0);
   }
+  const float* ad = nullptr;
+  if (alpha_dev && alpha_dev->defined()) {
+    TORCH_CHECK(alpha_dev->is_cuda() && alpha_dev->scalar_type() == torch::kFloat32 && alpha_dev->numel() == 1,
+                "gemm64: alpha_dev must be a one-element fp32 GPU tensor");
+    ad = alpha_dev->data_ptr<float>();
+  }
   ok(dta_gemm_k64(a.data_ptr(), a.stride(0), a_t, b.data_ptr(), b.stride(0), b_t, out_f32 ? nullptr : c.data_ptr(),
                   c.stride(0), two ? c2.data_ptr() : nullptr, two ? c2.stride(0) : 0,
                   out_f32 ? c.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (float)alpha, bp, (int)epi, rp, ldr,
-                  (int)tile, stream_of(stream)),
+                  (int)tile, stream_of(stream), ad),
      "gemm64");
   if (two) return {c, c2};
   return {c};
@@ -273,7 +281,7 @@ void dta_register_ext(pybind11::module_& m) {
   m.def("gemm64", &gemm_k64, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
         py::arg("out") = py::none(), py::arg("out2") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("res") = py::none(), py::arg("tile") = 0,
-        py::arg("stream") = -1);
+        py::arg("stream") = -1, py::arg("alpha_dev") = py::none());
   m.def("gemm64_tile", [](int M, int N, int K, int tile) { return dta_gemm_k64_tile(M, N, K, tile); },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
   m.def("linear_step_supported", [](int I, int C, int B, bool mom) { return dta_linear_step_supported(I, C, B, mom) != 0; });

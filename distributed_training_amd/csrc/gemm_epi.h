@@ -27,6 +27,7 @@ struct Args {
   float alpha;
   int epi;
   bf16* db;  // weight-gradient groups: the bias gradient db[m] = sum_k A(m, k) (nullptr: none)
+  const float* alpha_dev;  // nullptr, or a device scalar multiplying alpha (a loss scale known only on the GPU)
 #ifdef DTA_K64_STAMP
   unsigned long long* stamps;  // diagnostic build only: per-wave cycle sums of the two-phase loop's segments
 #endif
@@ -58,10 +59,13 @@ __device__ __forceinline__ void load_bias4(const Args& g, int n, float (&bv)[4])
 
 // The bf16 values of output `which` (0: c, 1: c2 of the GELU dual store) at row m, columns n .. n+3 -- the
 // fused epilogue of store4 below without the store (the LDS-staged epilogue of csrc/gemm_w4.hip stores them)
+__device__ __forceinline__ float alpha_of(const Args& g) { return g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha; }
+
 __device__ __forceinline__ bf16x4 val4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4], int which) {
   float v[4];
+  const float al = alpha_of(g);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
+  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], al, bv[r]);
   if (g.epi == EPI_GELU) {
     if (g.c2) {
       const bf16x4 h4 = pk4_bf16(v[0], v[1], v[2], v[3]);
@@ -88,8 +92,9 @@ __device__ __forceinline__ bf16x4 val4(const Args& g, int m, int n, const f32x4&
 // LDS-staged epilogue of csrc/gemm_k64.hip stages the res tile with whole-row loads first)
 __device__ __forceinline__ bf16x4 val4_res(const Args& g, const f32x4& acc, const float (&bv)[4], const bf16x4 r4) {
   float v[4];
+  const float al = alpha_of(g);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
+  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], al, bv[r]);
   if (g.epi == EPI_DGELU) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_fast(bf2f(r4[r]));
@@ -102,8 +107,9 @@ __device__ __forceinline__ bf16x4 val4_res(const Args& g, const f32x4& acc, cons
 
 __device__ __forceinline__ void store4(const Args& g, int m, int n, const f32x4& acc, const float (&bv)[4]) {
   float v[4];
+  const float al = alpha_of(g);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], g.alpha, bv[r]);
+  for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[r], al, bv[r]);
   if (g.c32) {
     *reinterpret_cast<float4*>(g.c32 + (int64_t)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
     return;

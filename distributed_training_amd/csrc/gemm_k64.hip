@@ -645,7 +645,8 @@ unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k
 // epi: 0 none, 2 GELU (c2 != nullptr: c = pre-activation, c2 = gelu), 16 x gelu'(res), 32 + res
 hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
                         int64_t ldc, void* c2, int64_t ldc2, float* c32, int M, int N, int K, float alpha,
-                        const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st) {
+                        const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st,
+                        const float* alpha_dev) {
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
   if (tile == k64::kW4 || tile == k64::kW4S) {
@@ -673,6 +674,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
     g.N = N;
     g.K = K;
     g.alpha = alpha;
+    g.alpha_dev = alpha_dev;
     g.epi = epi;
     g.tiles_m = (M + 255) / 256;
     g.tiles_n = (N + 255) / 256;
@@ -707,6 +709,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   g.N = N;
   g.K = K;
   g.alpha = alpha;
+  g.alpha_dev = alpha_dev;
   g.epi = epi;
 #ifdef DTA_K64_STAMP
   g.stamps = dta_k64_stamp_buf;

@@ -346,8 +346,9 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
 
 
 def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
-              alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    return native().gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64)[0]
+              alpha: float = 1.0, bias: Optional[torch.Tensor] = None,
+              alpha_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    return native().gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64, -1, alpha_dev)[0]
 
 
 def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -358,9 +359,12 @@ def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = No
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False, bias: Optional[torch.Tensor] = None,
-         alpha: float = 1.0, kind: str = "", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+         alpha: float = 1.0, kind: str = "", out: Optional[torch.Tensor] = None,
+         scale_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 ``alpha * op(a) op(b)^T (+ bias)`` on GPU, a: [M, K] (a_t: [K, M]), b: [N, K] (b_t: [K, N]);
-    hand-written kernel or hipBLASLt per shape (see module doc)."""
+    hand-written kernel or hipBLASLt per shape (see module doc).  ``scale_dev`` (fp32 [1] on the GPU, no
+    bias): the product is also multiplied by it -- inside the hand-written kernel's epilogue, or by a
+    separate pass after the library GEMM."""
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
 
@@ -382,9 +386,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
         impl = _pick(kind + ("b" if bias is not None else ""), M, N, K, cands)
     if impl:
         GEMM_STATS["dta"] += 1
-        return _run_gemm(impl, a, b, a_t, b_t, out, alpha, bias)
+        return _run_gemm(impl, a, b, a_t, b_t, out, alpha, bias, scale_dev)
     GEMM_STATS["torch"] += 1
-    return run_torch()
+    y = run_torch()
+    return y if scale_dev is None else y.mul_(scale_dev.to(y.dtype))
 
 
 def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -1014,14 +1019,15 @@ class _LinearCrossEntropy(Function):
     @staticmethod
     def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         x2, w, dlogits, count = ctx.saved_tensors
-        s = (g / count).to(dlogits.dtype)  # stays on the device (no host sync in backward)
+        # grad / count stays on the device (no host sync in backward); it scales the two GEMM products in
+        # the hand-written kernels' epilogues (no extra pass: 0.36 ms per Llama step for the [V, C] weight
+        # gradient), after the library GEMM otherwise
+        s = (g.float() / count).reshape(1)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(dlogits, w, False, True, kind="head_dgrad").mul_(s).view(ctx.xshape)
+            dx = gemm(dlogits, w, False, True, kind="head_dgrad", scale_dev=s).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            # (the scale on the [N, C] operand instead of this [V, C] product measured no better: same-box
-            # GPT-2 pairs 11.12-12.46 vs 11.05-11.39 ms, round 2)
-            dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam)).mul_(s)
+            dw = gemm(dlogits, x2, True, True, kind="head_wgrad", out=_grad_dest(ctx.wparam), scale_dev=s)
         return dx, dw, None, None
 
 

@@ -309,6 +309,27 @@ def test_linear_cross_entropy_fused_head(V):
     assert _rel(x.grad, xf.grad) < 3e-2 and _rel(w.grad, wf.grad) < 3e-2
 
 
+def test_linear_cross_entropy_scale_in_epilogue(monkeypatch):
+    """The hand-written head GEMMs (DTA_GEMM=dta) fold the loss-gradient scale grad / count, a device
+    scalar, into their epilogues (gemm64 alpha_dev) -- no separate scaling pass -- and match fp32."""
+    monkeypatch.setenv("DTA_GEMM", "dta")
+    torch.manual_seed(7)
+    N, C, V = 768, 384, 2048  # (shapes no other test times: the per-shape choice is memoised)
+    x = (0.5 * torch.randn(N, C, device=DEV)).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[::5] = -100
+    calls = dict(lm.GEMM_STATS)
+    loss = lm.linear_cross_entropy(x, w, t)
+    (loss * 2.5).backward()
+    assert lm.GEMM_STATS["dta"] - calls.get("dta", 0) == 3  # forward, input and weight gradients
+    xf, wf = (z.detach().float().requires_grad_() for z in (x, w))
+    lr = F.cross_entropy(xf @ wf.t(), t, ignore_index=-100)
+    (lr * 2.5).backward()
+    assert abs(loss.item() - lr.item()) < 2e-2 * abs(lr.item())
+    assert _rel(x.grad, xf.grad) < 3e-2 and _rel(w.grad, wf.grad) < 3e-2
+
+
 @pytest.mark.parametrize("arch", ["gpt2", "llama"])
 def test_fused_model_matches_fp32_reference(arch):
     """The whole fused GPU model (packed attention, fused residual norms, native
