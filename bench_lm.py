@@ -285,6 +285,7 @@ def main() -> None:
         routes = getattr(getattr(wrapped, "comm", None), "routes", None)
         if routes is not None:
             out["comm_routes"] = routes()
+            out["comm_classes_at_wrap"] = getattr(wrapped.comm, "prepared_log", [])
         out["gemm_calls"] = {"dta": _lm.GEMM_STATS["dta"], "hipblaslt": _lm.GEMM_STATS["torch"]}
         out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": ("hipblaslt" if not v else
                                                              f"k64/t{v - _lm.K64}" if v >= _lm.K64 else f"r2/t{v}")

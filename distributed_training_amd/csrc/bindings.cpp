@@ -22,13 +22,6 @@ hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, floa
 hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
                         void*, void*, int64_t, int, int, int, const void*, hipStream_t);
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
-int dta_gemm_tn_split(int, int, int);
-int dta_gemm_tn_cs_workers(int);
-int dta_gemm_tn_gd_split(int, int, int);
-hipError_t dta_gemm_tn_gd(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*,
-                          void*, hipStream_t);
-hipError_t dta_gemm_tn(const void*, int64_t, const void*, int64_t, void*, int64_t, int, int, int, int, float*, int, float*, void*,
-                       hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
 hipError_t dta_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int, int, int64_t, int64_t,
@@ -477,78 +470,6 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   return {dx, dw, db};
 }
 
-// C[M, N] = A^T B for A [K, M], B [K, N] bf16 row-major (the weight gradient dY^T X);
-// split = 0: LDS-DMA split-K kernel with its own split choice, > 0: that kernel with `split`,
-// < 0: the register-staged split-K kernel over -split slabs
-bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) { return dta_gemm_tn_split((int)M, (int)N, (int)K) > 0; }
-
-// C = A^T B (and, with_colsum, the column sums of A: the bias gradient of the same Linear)
-// c_out / db_out (optional): write the results there (e.g. the parameter's
-// slice of a flat gradient buffer) instead of fresh tensors
-std::vector<torch::Tensor> gemm_tn_impl(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream,
-                                        bool with_colsum, c10::optional<torch::Tensor> c_out = c10::nullopt,
-                                        c10::optional<torch::Tensor> db_out = c10::nullopt) {
-  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16,
-              "gemm_tn: bf16 GPU operands");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0), "gemm_tn: A [K, M], B [K, N]");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
-                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
-              "gemm_tn: 16-byte aligned rows required");
-  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  TORCH_CHECK(dta_gemm_tn_split((int)M, (int)N, (int)K) > 0, "gemm_tn: M, N % 128 == 0 and K % 64 == 0 required");
-  const auto odt = out_f32 ? torch::kFloat32 : torch::kBFloat16;
-  torch::Tensor c;
-  if (c_out.has_value()) {
-    c = *c_out;
-    TORCH_CHECK(c.is_cuda() && c.scalar_type() == odt && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
-                    c.is_contiguous(),
-                "gemm_tn: c_out must be a contiguous [M, N] tensor of the output dtype");
-  } else {
-    c = torch::empty({M, N}, a.options().dtype(odt));
-  }
-  torch::Tensor slab, cs, db;
-  if (with_colsum) {
-    cs = torch::empty({dta_gemm_tn_cs_workers((int)K), M}, a.options().dtype(torch::kFloat32));
-    if (db_out.has_value()) {
-      db = *db_out;
-      TORCH_CHECK(db.is_cuda() && db.scalar_type() == odt && db.numel() == M && db.is_contiguous(),
-                  "gemm_tn: db_out must be a contiguous [M] tensor of the output dtype");
-    } else {
-      db = torch::empty({M}, a.options().dtype(odt));
-    }
-  }
-  float* csp = with_colsum ? cs.data_ptr<float>() : nullptr;
-  void* dbp = with_colsum ? db.data_ptr() : nullptr;
-  if (split >= 0) {  // LDS-DMA split-K kernel (default)
-    const int sp = split > 0 ? (int)split : dta_gemm_tn_gd_split((int)M, (int)N, (int)K);
-    TORCH_CHECK(sp >= 1 && sp <= K / 32, "gemm_tn: split must be in [1, K / 32]");
-    if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
-    hip_ok(dta_gemm_tn_gd(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K,
-                          sp, sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, csp, dbp, pick_stream(stream)),
-           "gemm_tn");
-  } else {  // register-staged split-K kernel over -split slabs (kept for A/B measurements)
-    const int sp = (int)-split;
-    TORCH_CHECK((K / 64) % sp == 0, "gemm_tn: register-staged split must divide K / 64");
-    if (sp > 1) slab = torch::empty({sp, M, N}, a.options().dtype(torch::kFloat32));
-    hip_ok(dta_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), N, (int)M, (int)N, (int)K, sp,
-                       sp > 1 ? slab.data_ptr<float>() : nullptr, out_f32 ? 1 : 0, csp, dbp, pick_stream(stream)),
-           "gemm_tn");
-  }
-  if (with_colsum) return {c, db};
-  return {c};
-}
-
-torch::Tensor gemm_tn(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split, int64_t stream,
-                      c10::optional<torch::Tensor> c_out) {
-  return gemm_tn_impl(a, b, out_f32, split, stream, false, c_out)[0];
-}
-
-std::vector<torch::Tensor> gemm_tn_colsum(torch::Tensor a, torch::Tensor b, bool out_f32, int64_t split,
-                                          int64_t stream, c10::optional<torch::Tensor> c_out,
-                                          c10::optional<torch::Tensor> db_out) {
-  return gemm_tn_impl(a, b, out_f32, split, stream, true, c_out, db_out);
-}
 
 // bias gradient = column sums of dy [N, C] (bf16), returned in `dtype`'s float type (bf16 or f32)
 torch::Tensor bias_grad(torch::Tensor dy, bool out_f32, int64_t stream) {
@@ -1119,12 +1040,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
-  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out_f32") = false, py::arg("split") = 0,
-        py::arg("stream") = -1, py::arg("c_out") = py::none());
-  m.def("gemm_tn_colsum", &gemm_tn_colsum, py::arg("a"), py::arg("b"), py::arg("out_f32") = false,
-        py::arg("split") = 0, py::arg("stream") = -1, py::arg("c_out") = py::none(), py::arg("db_out") = py::none());
-  m.def("gemm_tn_supported", &gemm_tn_supported);
-  m.def("gemm_tn_split", &dta_gemm_tn_gd_split);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),

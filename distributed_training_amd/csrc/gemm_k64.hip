@@ -499,7 +499,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     for (int r = 0; r < BM / (RPI * NW); ++r) {
       const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
+#if defined(DTA_K64_EPI_DIAG) && DTA_K64_EPI_DIAG == 1
+      if (g.alpha == -1234.5f)  // diagnostic build (scripts/k64_epi_diag.hip): stores skipped, values live
+#endif
+#if defined(DTA_K64_EPI_DIAG) && DTA_K64_EPI_DIAG == 2
+      __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(g.c + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c));
+#else
       *reinterpret_cast<bf16x8*>(g.c + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) = v;
+#endif
       if (dual) {
         const bf16x4 lo = pk4_bf16(gelu_fast(bf2f(v[0])), gelu_fast(bf2f(v[1])), gelu_fast(bf2f(v[2])), gelu_fast(bf2f(v[3])));
         const bf16x4 hi = pk4_bf16(gelu_fast(bf2f(v[4])), gelu_fast(bf2f(v[5])), gelu_fast(bf2f(v[6])), gelu_fast(bf2f(v[7])));

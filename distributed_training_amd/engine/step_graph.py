@@ -72,7 +72,10 @@ class GraphedStep:
         self.warmup_losses = []
         with torch.cuda.stream(self.stream):
             for _ in range(max(1, warmup)):
-                self.warmup_losses.append(step_fn(*self.static))
+                # detached: a kept loss would keep its autograd graph -- and the parameters'
+                # AccumulateGrad nodes, created on THIS stream -- alive, and a later eager step on
+                # another stream would then accumulate through a node of the wrong stream
+                self.warmup_losses.append(step_fn(*self.static).detach())
         torch.cuda.current_stream(dev).wait_stream(self.stream)
         torch.cuda.synchronize(dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = torch.cuda.CUDAGraph()
@@ -80,7 +83,7 @@ class GraphedStep:
         self.loss: Optional[torch.Tensor] = None
         try:
             with torch.cuda.graph(self.graph, stream=self.stream):
-                self.loss = step_fn(*self.static)
+                self.loss = step_fn(*self.static).detach()  # (as above: no graph kept alive)
         except Exception as e:  # noqa: BLE001 - reported through .ok / .error after the agreement
             self.error = e
             self._abandon()

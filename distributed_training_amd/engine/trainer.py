@@ -310,8 +310,11 @@ class Trainer:
                 targets = targets.to(dev, non_blocking=True)
                 loss = self._run_batch(source, targets)
                 if self.config.log_throughput and loss is not None:
-                    lf = loss.detach().float()
-                    loss_sum = lf if loss_sum is None else loss_sum + lf
+                    # accumulate into a buffer of our own: a replayed step graph returns its static loss
+                    # tensor (overwritten by the next replay), and .float() of an fp32 loss is no copy
+                    if loss_sum is None:
+                        loss_sum = torch.zeros((), dtype=torch.float32, device=loss.device)
+                    loss_sum += loss.detach().float()
                 steps += 1
                 self._maybe_inject_fault(epoch, steps)
         if self.config.log_throughput or self.config.desync_check_every:
@@ -325,6 +328,13 @@ class Trainer:
                 if loss_sum is not None and steps:
                     self.last_epoch_stats["loss"] = float(loss_sum.item()) / steps
                     msg += f" | loss {self.last_epoch_stats['loss']:.4f}"
+                if steps:
+                    self.last_epoch_stats["ms_per_step"] = dt * 1e3 / steps
+                    msg += f" | {dt * 1e3 / steps:.2f} ms/step"
+                seq = getattr(getattr(self.train_data, "dataset", None), "seq_len", None)
+                if seq:  # token LMs: tokens/s over all ranks
+                    self.last_epoch_stats["tokens_per_s"] = samples * int(seq) / dt
+                    msg += f" | {samples * int(seq) / dt:,.0f} tokens/s"
                 logger.info(msg)
         if self.config.desync_check_every and (epoch + 1) % self.config.desync_check_every == 0:
             from ..utils.desync import check_replicas_in_sync
@@ -347,7 +357,8 @@ class Trainer:
     def train(self, max_epochs: int) -> None:
         for epoch in range(self.epochs_run, max_epochs):
             self._run_epoch(epoch)
-            if epoch % self.config.save_every == 0:
+            # (save_every <= 0: no snapshots -- an extension; the reference's modulo would divide by zero)
+            if self.config.save_every > 0 and epoch % self.config.save_every == 0:
                 self._sync_fused_to_module()
                 self.checkpoint.save(self.model, epoch, self.optimizer)
         self._sync_fused_to_module()

@@ -173,6 +173,17 @@ class GPT2(nn.Module):
             return lm.linear_cross_entropy(y, self.lm_head.weight, targets)
         return self.lm_head(y)
 
+    def activation_bytes_per_token(self, checkpointed: bool = False) -> int:
+        """Bytes the forward keeps for the backward, per token (bf16; estimate for the
+        ``activation_checkpointing: auto`` decision, app.py): per block the input, two LayerNorm
+        outputs, qkv, the attention output, the residual sum, the MLP pre-activation and its GELU
+        (16 C), plus fp32 row statistics; checkpointed: the block input only.  Logits on top."""
+        c = self.cfg
+        per_block = 2 * 16 * c.n_embd + 4 * (4 + c.n_head)
+        if checkpointed:
+            per_block = 2 * c.n_embd
+        return c.n_layer * per_block + 2 * c.padded_vocab + 2 * c.n_embd
+
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (6N + attention), PaLM-style accounting."""
         n = self.num_params() - self.wpe.weight.numel()

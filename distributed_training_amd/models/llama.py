@@ -161,6 +161,20 @@ class Llama(nn.Module):
         _, y = self.norm.add_forward(x, h)
         return self.output(y, targets)
 
+    def activation_bytes_per_token(self, checkpointed: bool = False) -> int:
+        """Bytes the forward keeps for the backward, per token (bf16 activations; estimate for the
+        ``activation_checkpointing: auto`` decision, app.py).  Per block: block input, norm outputs,
+        packed QKV, attention output, residual sum, gate|up and the SwiGLU output, plus the fp32 row
+        statistics; checkpointed: the block input only.  The LM head's logits (rewritten in place as
+        the logit gradient) come on top in both cases."""
+        c = self.cfg
+        d = c.n_embd // c.n_head
+        qkv = (c.n_head + 2 * c.n_kv_head) * d
+        per_block = 2 * (c.n_embd * 5 + qkv + 3 * c.ffn_hidden) + 4 * (4 + c.n_head)
+        if checkpointed:
+            per_block = 2 * c.n_embd
+        return c.n_layer * per_block + 2 * c.vocab_size + 2 * c.n_embd
+
     def flops_per_token(self, seq_len: int) -> float:
         c = self.cfg
         n = self.num_params() - self.tok_embeddings.weight.numel()

@@ -9,9 +9,10 @@ of the GPU tests.
 Projection GEMMs (forward x W^T + b, input gradient dy W, weight gradient
 dy^T x, the LM head) go through :func:`gemm`: the gfx950 GEMMs of
 ``csrc/gemm_k64.hip`` / ``csrc/gemm_w4.hip`` (bias / scale / GELU / residual fused
-in their epilogues) or hipBLASLt, whichever measured faster for that shape on this
-GPU (timed once per shape and process, ``DTA_GEMM=auto``; ``dta`` / ``torch`` force one).  Weight
-gradients with small outputs keep the split-K kernel of ``csrc/gemm.hip``.
+in their epilogues) or hipBLASLt, per shape (see :func:`_pick`: a tracked per-shape table
+measured on MI355X, in-run timing only for shapes it lacks; ``DTA_GEMM=dta`` / ``torch`` force
+one).  Single-use weight gradients are deferred and computed in grouped launches of the 64-deep
+kernel (``gemm_k64_group_kernel``, bias gradients from the same MFMA pipe).
 """
 from __future__ import annotations
 
@@ -264,8 +265,8 @@ def _cache_path() -> Optional[str]:
 
 
 def _load_cache() -> None:
-    """``DTA_GEMM_CACHE=file.json``: per-shape choices measured by an earlier run on this
-    kind of GPU (keys ``kind MxNxK``), so a run (or a profile) skips the timing."""
+    """``DTA_GEMM_CACHE=file.json``: per-shape choices of an earlier run (keys ``kind MxNxK``),
+    used before the tracked table -- an explicit override for experiments."""
     _CACHE_LOADED[0] = True
     path = _cache_path()
     if not path or not os.path.exists(path):
@@ -297,6 +298,46 @@ def _save_cache() -> None:
         pass
 
 
+# ---- the tracked per-shape table (verdict r4: picks must not depend on a first-use timing inside a running
+# step -- two boxes must pick the same kernel).  ops/gemm_table_mi355x.json is measured by
+# scripts/gemm_table.py on an idle MI355X: every candidate of every GPT-2 / Llama-3 8B GEMM shape and kind,
+# interleaved rounds on random operands, the fastest median kept.  A shape in the table takes its pick with no
+# timing at all; a shape missing from it is timed in-run (more rounds than before) and logged.
+# DTA_GEMM_TABLE=0 ignores the table; DTA_GEMM_VERIFY=1 also times table shapes in-run and warns when the
+# table's pick measures more than 3 % slower than the best candidate there.
+TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_table_mi355x.json")
+_TABLE: Dict[tuple, int] = {}
+_TABLE_LOADED = [False]
+GEMM_PICK_SOURCE: Dict[tuple, str] = {}  # key -> "table" | "timed" | "forced" | "cache"
+GEMM_TIMES: Dict[tuple, Dict[int, float]] = {}  # key -> median us per candidate (timed / verified keys)
+
+
+def _gfx950() -> bool:
+    try:
+        return "gfx950" in torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+    except Exception:  # noqa: BLE001 - no device / no attribute: no table
+        return False
+
+
+def gemm_table() -> Dict[tuple, int]:
+    """The tracked table as {(kind, M, N, K): impl id} ({} off gfx950 or with DTA_GEMM_TABLE=0)."""
+    if not _TABLE_LOADED[0]:
+        _TABLE_LOADED[0] = True
+        if os.environ.get("DTA_GEMM_TABLE", "1") != "0" and os.path.exists(TABLE_PATH) and _gfx950():
+            import json
+
+            with open(TABLE_PATH) as f:
+                for k, v in json.load(f)["entries"].items():
+                    kind, dims = k.rsplit(" ", 1)
+                    M, N, K = (int(x) for x in dims.split("x"))
+                    _TABLE[(kind, M, N, K)] = int(v["pick"])
+    return _TABLE
+
+
+def _rounds() -> int:
+    v = os.environ.get("DTA_GEMM_ROUNDS", "").strip()
+    return max(3, int(v)) if v else 9
+
 # implementation ids in _GEMM_CHOICE: 0 = hipBLASLt (torch), 10 + t = csrc/gemm_k64.hip tile t (64-deep
 # stages; tiles 9 / 10 = csrc/gemm_w4.hip, which also covers K % 64 != 0 -- the round-2 kernel that did is gone)
 K64 = 10
@@ -317,32 +358,64 @@ def gemm_candidates(M: int, N: int, K: int) -> list:
 
 def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]], prefer: float = _PREFER_DTA) -> int:
     """Implementation for one (possibly fused) GEMM shape: ``cands`` maps implementation ids to
-    callables computing the SAME fused result (0 = hipBLASLt + separate epilogue kernels); the
-    fastest by interleaved timing (median of rounds), hand-written on near-ties (_PREFER_DTA).
-    Memoised per (kind, M, N, K) and process; ``DTA_GEMM_CACHE`` persists it."""
+    callables computing the SAME fused result (0 = hipBLASLt + separate epilogue kernels).  In
+    order: a ``DTA_GEMM_CACHE`` entry; ``DTA_GEMM=torch`` / ``dta`` (forced); the tracked table
+    (:func:`gemm_table`); else in-run interleaved timing (median of :func:`_rounds` rounds): the
+    fastest hand-written candidate unless the library is faster (``prefer``: the factor by which
+    the hand-written one may be slower and still win -- 0.85 for the GELU dual store, whose in-step
+    cost exceeds its timed cost).  Memoised per (kind, M, N, K) and process."""
     if not _CACHE_LOADED[0]:
         _load_cache()
     key = (kind, M, N, K)
     c = _GEMM_CHOICE.get(key)
     if c is not None and (c in cands or c == 0):
+        GEMM_PICK_SOURCE.setdefault(key, "cache")
         return c
     mode = os.environ.get("DTA_GEMM", "auto")
     dta = [k for k in cands if k != 0]
+    src = "forced"
+    t = gemm_table().get(key) if mode == "auto" else None
+    if t is not None and not (t == 0 or t in cands):
+        t = None
     if mode == "torch" or not dta:
         c = 0
+    elif t is not None:
+        c, src = t, "table"
+        if os.environ.get("DTA_GEMM_VERIFY", "0") == "1" and not torch.cuda.is_current_stream_capturing():
+            times = _time_us(cands, rounds=_rounds())
+            GEMM_TIMES[key] = times
+            best = min(times, key=times.get)
+            if times[c] > 1.03 * times[best]:
+                import logging
+
+                logging.getLogger(__name__).warning(
+                    "GEMM %s %dx%dx%d: tracked pick %s measures %.1f us here, %s %.1f us", kind, M, N, K,
+                    _impl_name(c), times[c], _impl_name(best), times[best])
     elif mode == "dta" or torch.cuda.is_current_stream_capturing():
         c = dta[0]
         auto = native().gemm64_tile(M, N, K, 0)
         if K64 + auto in dta:
             c = K64 + auto
     else:
-        times = _time_us(cands)
+        times = _time_us(cands, rounds=_rounds())
+        GEMM_TIMES[key] = times
         best = min(dta, key=times.get)
         c = best if 0 not in times or times[best] <= prefer * times[0] else 0
+        src = "timed"
+        if _TABLE:  # (a table exists but lacks this shape: say so)
+            import logging
+
+            logging.getLogger(__name__).info("GEMM %s %dx%dx%d not in the tracked table: timed in-run -> %s",
+                                             kind, M, N, K, _impl_name(c))
     _GEMM_CHOICE[key] = c
+    GEMM_PICK_SOURCE[key] = src
     if mode == "auto":
         _save_cache()
     return c
+
+
+def _impl_name(c: int) -> str:
+    return "hipblaslt" if not c else f"k64/t{c - K64}"
 
 
 def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
@@ -363,8 +436,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
          scale_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 ``alpha * op(a) op(b)^T (+ bias)`` on GPU, a: [M, K] (a_t: [K, M]), b: [N, K] (b_t: [K, N]);
     hand-written kernel or hipBLASLt per shape (see module doc).  ``scale_dev`` (fp32 [1] on the GPU, no
-    bias): the product is also multiplied by it -- inside the hand-written kernel's epilogue, or by a
-    separate pass after the library GEMM."""
+    bias): the product is also multiplied by it -- inside the hand-written kernel's epilogue (in fp32,
+    before the rounding), or by a separate pass after the library GEMM (after it; the LM head's scale is
+    1 / token count, a power of two at the configs' token counts, so both round identically there).
+    Every timed candidate includes its scaling, so the pick compares the costs the step pays."""
     M, K = (a.shape[1], a.shape[0]) if a_t else (a.shape[0], a.shape[1])
     N = b.shape[1] if b_t else b.shape[0]
 
@@ -376,20 +451,21 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
         y = torch.mm(A, B) if out is None else torch.mm(A, B, out=out)
         if alpha != 1.0:
             y.mul_(alpha)
+        if scale_dev is not None:
+            y.mul_(scale_dev.to(y.dtype))
         return y if bias is None else y.add_(bias)
 
     impl = 0
     if _gemm_ok(a, b, bias, out):
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
         for t in gemm_candidates(M, N, K):
-            cands[t] = (lambda t=t: _run_gemm(t, a, b, a_t, b_t, out, alpha, bias))
+            cands[t] = (lambda t=t: _run_gemm(t, a, b, a_t, b_t, out, alpha, bias, scale_dev))
         impl = _pick(kind + ("b" if bias is not None else ""), M, N, K, cands)
     if impl:
         GEMM_STATS["dta"] += 1
         return _run_gemm(impl, a, b, a_t, b_t, out, alpha, bias, scale_dev)
     GEMM_STATS["torch"] += 1
-    y = run_torch()
-    return y if scale_dev is None else y.mul_(scale_dev.to(y.dtype))
+    return run_torch()
 
 
 def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -428,9 +504,6 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
 
 
 # ------------------------------------------------------------------ linear
-_WGRAD_NATIVE_MAX_TILES = 192  # 128x128 output tiles; above this the general GEMM fills the chip by itself
-
-
 def _grad_dest(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     """The slice of the DDP engine's flat gradient buffer that ``p``'s gradient
     goes to, when this backward may write it there directly: the engine hands
@@ -590,27 +663,30 @@ def wgrad_flush() -> None:
         fn()
 
 
+_DEFER_MAX_TILES = 48  # 256 x 256 output tiles: larger weight gradients fill the chip by themselves (gemm())
+
+
 def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w: Optional[torch.Tensor] = None,
                  b: Optional[torch.Tensor] = None) -> Union[torch.Tensor, Tuple[torch.Tensor, Optional[torch.Tensor]]]:
     """dW = dy^T x (and, ``with_bias``, db = column sums of dy: returns (dW, db)).
-    Small outputs with a long token reduction (GPT-2: 768 x 768 .. 3072 x 768
-    over 8192 tokens) go to the split-K MFMA kernel (csrc/gemm.hip), which fills
-    256 CUs where a library GEMM tiling only the output does not (measured
-    1.3-2.0x on the four GPT-2 shapes) and sums the bias gradient in extra
-    workgroups of the same launch; large outputs stay on hipBLASLt.  With the
-    parameters ``w`` / ``b`` given, the results go straight into their flat
-    gradient slices when :func:`_grad_dest` allows it."""
+    A single-use weight whose gradient goes straight into its flat-gradient slice is DEFERRED
+    (queued for a grouped launch of the 64-deep kernel, bias gradient from the same MFMA pipe:
+    see ``_DEFER``) -- at GPT-2 sizes one weight gradient (768 x 768 .. 3072 x 768 over 8192
+    tokens) cannot fill 256 CUs by itself, a group of them can.  Anything else (a weight used
+    twice, no flat slice, shapes off the 256 grid) goes through :func:`gemm` (hand-written or
+    hipBLASLt per shape) and the bias-gradient kernel.  With the parameters ``w`` / ``b`` given,
+    the results go straight into their flat gradient slices when :func:`_grad_dest` allows it."""
     K, M = dy2.shape
     N = x2.shape[1]
-    if (M % 128 == 0 and N % 128 == 0 and K % 64 == 0 and (M // 128) * (N // 128) <= _WGRAD_NATIVE_MAX_TILES
-            and dy2.stride(1) == 1 and x2.stride(1) == 1 and native().gemm_tn_supported(M, N, K)):
+    if M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1 \
+            and (M // 256) * (N // 256) <= _DEFER_MAX_TILES:
         x2 = x2.contiguous() if x2.stride(0) % 8 else x2
         cw = _grad_dest(w)
         cb = _grad_dest(b) if with_bias else None
         thr = _group_threshold()
         if thr and cw is not None and (cb is not None or not with_bias) \
                 and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
-                and _single_use(w) and M % 256 == 0 and N % 256 == 0 and cw.stride(0) % 8 == 0 \
+                and _single_use(w) and cw.stride(0) % 8 == 0 \
                 and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
             # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
             # holds ALIASES of the slices, never the tensors returned to autograd: a second
@@ -625,10 +701,14 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
             if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm64_group_max():
                 wgrad_flush()
             return (cw, cb) if with_bias else cw
+        dw = gemm(dy2, x2, True, True, kind="wgrad", out=cw)
         if with_bias:
-            dw, db = native().gemm_tn_colsum(dy2, x2, False, 0, -1, cw, cb)
+            db = native().bias_grad(dy2, False, -1)
+            if cb is not None:
+                cb.copy_(db)
+                db = cb
             return dw, db
-        return native().gemm_tn(dy2, x2, False, 0, -1, cw)
+        return dw
     dw = gemm(dy2, x2, True, True, kind="wgrad", out=_grad_dest(w))
     if with_bias:
         return dw, native().bias_grad(dy2, False, -1)
@@ -637,8 +717,8 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
 
 class _Linear(Function):
     """y = x W^T (+ b): forward and input-gradient GEMMs through :func:`gemm`
-    (bias fused in the epilogue), weight (and bias) gradients from the split-K
-    kernel or :func:`gemm` (see _weight_grad)."""
+    (bias fused in the epilogue), weight (and bias) gradients deferred into a grouped
+    launch or through :func:`gemm` (see _weight_grad)."""
 
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

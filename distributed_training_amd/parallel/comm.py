@@ -58,14 +58,19 @@ class CommWork:
         self._done = False
 
     def wait(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Order ``stream`` (default: the current stream) after the collective.  A torch work's
+        ``wait()`` orders the CURRENT stream, so with an explicit ``stream`` it runs with that
+        stream made current (and so does the post-processing, e.g. the avg division)."""
         if self._done:
             return
-        if self._work is not None:
-            self._work.wait()
-        if self._event is not None:
-            (stream or torch.cuda.current_stream()).wait_event(self._event)
-        if self._post is not None:
-            self._post()
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            if self._work is not None:
+                self._work.wait()
+            if self._event is not None:
+                (stream or torch.cuda.current_stream()).wait_event(self._event)
+            if self._post is not None:
+                self._post()
         self._done = True
 
 

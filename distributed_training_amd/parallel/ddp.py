@@ -96,6 +96,11 @@ class DistributedDataParallel(nn.Module):
         if init_sync and self.world_size > 1:
             self._verify_shapes()
             self._sync_module_states()
+        prepare = getattr(self.comm, "prepare", None)
+        if prepare is not None and self.world_size > 1:
+            # size-routed data planes (parallel/routed.py): every bucket's route calibrated now, not in a step
+            esz = self.flat.grad.element_size()
+            prepare([("all_reduce", self.flat.grad.dtype, (b.end - b.start) * esz) for b in self.buckets])
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i))
                        for i, p in enumerate(self.flat.params)]
         self.require_sync = True
@@ -130,7 +135,12 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------ per step
     def reset_iteration(self) -> None:
         """Forget a step that stopped midway (e.g. a failed graph capture): hook counts,
-        queued buckets and pending optimizer ranges."""
+        queued buckets and pending optimizer ranges.  A bucket all-reduce of the abandoned step
+        that is still in flight writes its bucket slice on the comm stream: the current stream
+        is ordered after it first, so it cannot land on top of the next step's gradients."""
+        for w in self._works:
+            if w is not None:
+                w.wait()
         self._ov_pending = []
         self._reset_iteration()
 

@@ -460,6 +460,15 @@ class FullyShardedDataParallel(nn.Module):
                 if b.numel():
                     self.rep.broadcast(b.data, src=0)
 
+        prepare = getattr(self.comm, "prepare", None)
+        if prepare is not None and self.world_size > 1:
+            # size-routed data planes (parallel/routed.py): the route of every unit's all-gather and
+            # reduce-scatter is calibrated now, at the real sizes -- not inside the first step
+            pe = torch.empty((), dtype=param_dtype).element_size()
+            re_ = torch.empty((), dtype=self.reduce_dtype).element_size()
+            prepare([m for u in self.units for m in (("all_gather", param_dtype, u.total * pe),
+                                                      ("reduce_scatter", self.reduce_dtype, u.total * re_))])
+
         # ---- hooks ----
         for u in self.units:
             if not u.is_root:
@@ -571,7 +580,11 @@ class FullyShardedDataParallel(nn.Module):
         failed mid-backward (engine/step_graph.py): its queued final callback, pending and waiting
         reduce-scatters, per-unit backward state and gathered copies.  Without this the next
         backward never queues ``_finalize_backward`` (``_cb_queued`` stuck), so gradients are not
-        bound or zero-filled and ``_pending_rs`` grows without bound."""
+        bound or zero-filled and ``_pending_rs`` grows without bound.  Reduce-scatters (and replica
+        all-reduces) of the abandoned backward still in flight write into the flat gradient on
+        their own stream: the current stream is ordered after each before they are forgotten."""
+        for _u, work, _out, _g in self._pending_rs:
+            work.wait()
         for u in self.units:
             u.wait()  # (a prefetch still in flight lands before its storage can be freed)
             u.in_backward = False
@@ -683,6 +696,11 @@ class FullyShardedDataParallel(nn.Module):
         s = self._rep_stream
         if s is None:
             s = self._rep_stream = torch.cuda.Stream(self.device)
+        # the gradient was written on the compute stream: with one rank per shard group there is no
+        # reduce-scatter event to order the all-reduce behind it (rs_work is an empty CommWork), so the
+        # side stream waits for the compute stream first, then for the reduce-scatter (whose work, for a
+        # torch communicator, orders the stream made current in CommWork.wait)
+        s.wait_stream(torch.cuda.current_stream(self.device))
         rs_work.wait(s)
         with torch.cuda.stream(s), prof.range_(f"fsdp.unit{u.index}.replica_all_reduce"):
             return self.rep.all_reduce(out, op="avg", async_op=True)

@@ -13,13 +13,16 @@ when the communicator is built:
   over the ranks (so every rank takes the SAME decision: collectives are issued in the
   same order on every rank of each data plane), and the faster one (IPC only when it
   wins by ``margin``) serves every message of that class;
-* each message then goes to the route of the smallest class at least its size.  A message
-  LARGER than every class (FSDP units: 436 MB per Llama-3 8B layer, 1.05 GB for the embedding
-  / head) adds a class of its own on first use -- the next power of two -- calibrated on the
-  spot for every op and dtype (all ranks meet the same first such message: the engines issue
-  identical collective sequences), so the routes of the real message sizes are measured, not
-  extrapolated; inside a graph capture the largest class is used instead.  Broadcast,
-  all-to-all and barrier stay on the primary.
+* each message then goes to the route of the smallest class at least its size.  The engines
+  know every message they will send when they wrap the model -- DDP its bucket sizes, FSDP its
+  unit sizes (436 MB per Llama-3 8B layer, 1.05 GB for the embedding / head) -- and hand them to
+  :meth:`RoutedComm.prepare` there: every message larger than the default classes gets a class
+  of its own (its size rounded up to 16 MiB), calibrated at wrap time for the (op, dtype) pairs
+  that will use it -- before the first step, outside any capture, while no activation is
+  allocated.  A message past every class that was NOT prepared still adds a class on first use
+  (the next power of two; a logged fallback -- it times multi-GB scratch inside a running
+  step); inside a graph capture the largest class is used instead.  Broadcast, all-to-all and
+  barrier stay on the primary.
 * calibration failures are agreed on key by key (a MIN of the success flag over the ranks
   after each timed key), so every rank stops timing the fast plane at the same key.
 
@@ -73,6 +76,7 @@ class RoutedComm(Communicator):
         else:
             self.table = {(op, dt): ["primary"] * len(self.sizes) for op in OPS for dt in DTYPES}
         self.counts = {"primary": 0, "fast": 0}
+        self.prepared_log: List[Dict[str, Any]] = []  # classes added after construction (bench_lm.py JSON)
 
     # ------------------------------------------------------------ routing
     def _route(self, op: str, dtype: torch.dtype, nbytes: int) -> Communicator:
@@ -81,6 +85,9 @@ class RoutedComm(Communicator):
             return self.primary
         if nbytes > self.sizes[-1] and self.lazy_max and nbytes <= self.lazy_max \
                 and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            logger.warning("routed comm: %s %s message of %.1f MiB is past every prepared size class: "
+                           "calibrating a class inside the running step (the engine should prepare() it "
+                           "at wrap)", op, str(dtype).replace("torch.", ""), nbytes / MiB)
             self._add_class(1 << (int(nbytes) - 1).bit_length())
             routes = self.table[(op, dtype)]
         k = next((i for i, s in enumerate(self.sizes) if nbytes <= s), len(self.sizes) - 1)
@@ -96,15 +103,45 @@ class RoutedComm(Communicator):
         k = next((i for i, s in enumerate(self.sizes) if nbytes <= s), len(self.sizes) - 1)
         return routes[k]
 
-    def _add_class(self, size: int) -> None:
-        """A new size class (every op and dtype calibrated at ``size``), kept in ascending order."""
-        new = self._calibrate([size], self.iters)
+    def _add_class(self, size: int, pairs: Optional[List[Tuple[str, torch.dtype]]] = None,
+                   why: str = "on first use") -> None:
+        """A new size class, kept in ascending order: the (op, dtype) ``pairs`` (default: every one)
+        calibrated at ``size``; the other pairs take the route of the next smaller class."""
+        new = self._calibrate([size], self.iters, pairs)
         k = next((i for i, s in enumerate(self.sizes) if size < s), len(self.sizes))
         self.sizes.insert(k, size)
         for key, rs in self.table.items():
-            rs.insert(k, new.get(key, ["primary"])[0])
-        logger.info("routed comm: size class %d MiB added on first use (rank %d): %s", size // MiB, self.rank,
-                    {f"{op} {str(dt).replace('torch.', '')}": r[0] for (op, dt), r in new.items()})
+            rs.insert(k, new[key][0] if key in new else rs[max(k - 1, 0)])
+        self.prepared_log.append({"MiB": size // MiB, "when": why,
+                                  "routes": {f"{op} {str(dt).replace('torch.', '')}": r[0]
+                                             for (op, dt), r in new.items()}})
+        logger.info("routed comm: size class %d MiB added %s (rank %d): %s", size // MiB, why, self.rank,
+                    self.prepared_log[-1]["routes"])
+
+    def prepare(self, messages: Any) -> List[int]:
+        """Calibrate, now, a size class for every message of ``messages`` -- ``(op, dtype, nbytes)``
+        triples, the collectives an engine will send each step -- that is larger than every class,
+        so no calibration runs inside a step.  COLLECTIVE: every rank passes the same messages
+        (the engines derive them from the model structure, identical on every rank).  Returns the
+        sizes of the classes added."""
+        if not self.lazy_max:  # (fixed table / calibration off: nothing is ever timed)
+            return []
+        want: Dict[int, List[Tuple[str, torch.dtype]]] = {}
+        for op, dt, n in messages:
+            if op not in OPS or (op, dt) not in self.table or int(n) <= self.sizes[-1] or int(n) > self.lazy_max:
+                continue
+            gran = min(16 * MiB, max(4096, self.sizes[-1] // 4))  # (16 MiB past the default 64 MiB classes)
+            size = -(-int(n) // gran) * gran
+            if size in self.sizes:
+                continue
+            pairs = want.setdefault(size, [])
+            if (op, dt) not in pairs:
+                pairs.append((op, dt))
+        added = []
+        for size in sorted(want):
+            self._add_class(size, sorted(want[size], key=lambda p: (p[0], str(p[1]))), why="at wrap")
+            added.append(size)
+        return added
 
     def routes(self) -> Dict[str, str]:
         """``"all_reduce bf16 <=4MiB" -> "ipc" | "rccl"`` for the log / bench JSON."""
@@ -146,11 +183,14 @@ class RoutedComm(Communicator):
         sync()
         return (time.perf_counter() - t0) / iters
 
-    def _calibrate(self, sizes: List[int], iters: int) -> Dict[Tuple[str, torch.dtype], List[str]]:
-        """Time every (op, dtype, size) on both planes; per key the ranks agree (MAX of the times, MIN
-        of the success flag) before the next key is timed, so a failure on one rank stops the timing
-        of the fast plane on every rank at that key (no rank left waiting inside an IPC collective)."""
-        keys = [(op, dt, s) for op in OPS for dt in DTYPES for s in sizes]
+    def _calibrate(self, sizes: List[int], iters: int, pairs: Optional[List[Tuple[str, torch.dtype]]] = None
+                   ) -> Dict[Tuple[str, torch.dtype], List[str]]:
+        """Time every (op, dtype, size) (``pairs``: only those (op, dtype)) on both planes; per key the
+        ranks agree (MAX of the times, MIN of the success flag) before the next key is timed, so a
+        failure on one rank stops the timing of the fast plane on every rank at that key (no rank
+        left waiting inside an IPC collective)."""
+        pairs = pairs if pairs is not None else [(op, dt) for op in OPS for dt in DTYPES]
+        keys = [(op, dt, s) for op, dt in pairs for s in sizes]
         table: Dict[Tuple[str, torch.dtype], List[str]] = {}
         dev = self.device if self.device.type == "cuda" else torch.device("cpu")
         for op, dt, s in keys:

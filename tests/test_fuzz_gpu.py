@@ -38,21 +38,6 @@ def test_norm_shapes(n, c8, rms):
 
 
 @FUZZ
-@given(mt=st.integers(1, 12), nt=st.integers(1, 8), kt=st.integers(1, 64), split=st.integers(0, 9))
-def test_gemm_tn_shapes(mt, nt, kt, split):
-    from distributed_training_amd.ops import native
-
-    M, N, K = 128 * mt, 128 * nt, 64 * kt
-    split = min(split, K // 32)
-    g = torch.Generator(device=DEV).manual_seed(M * 7 + N * 3 + K)
-    a = torch.randn(K, M, device=DEV, generator=g).bfloat16()
-    b = torch.randn(K, N, device=DEV, generator=g).bfloat16()
-    c, db = native().gemm_tn_colsum(a, b, True, split)
-    assert _rel(c, a.float().t() @ b.float()) < 1e-3
-    assert _rel(db, a.float().sum(0)) < 1e-4
-
-
-@FUZZ
 @given(s=st.integers(1, 700), heads=st.sampled_from([(4, 4), (4, 2), (8, 1), (6, 3)]), d=st.sampled_from([64, 128]),
        causal=st.booleans())
 def test_attention_shapes(s, heads, d, causal):

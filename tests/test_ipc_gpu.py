@@ -495,22 +495,25 @@ def _routed_worker(rank, ws):
                 assert torch.equal(out.cpu(), torch.arange(1, ws + 1).repeat_interleave(m).to(dt))
                 assert torch.equal(o.cpu(), torch.full((m,), float(ws)).to(dt))
         assert rc.counts[route] == before + 12
-    # a message past every class (> 64 MiB, the size of an FSDP unit) adds a class calibrated on the
-    # spot on both planes; then each route is forced and checked exactly at that size
-    big = 36 << 20  # 36 Mi bf16 elements = 72 MiB
-    y = torch.full((big,), 1.0, dtype=torch.bfloat16, device=dev)
-    rc.all_reduce(y, "sum")
-    assert rc.sizes[-1] == 128 * MiB, rc.sizes
+    # the FSDP unit sizes are prepared at wrap (parallel/routed.py prepare): a 512 MiB all-gather and
+    # reduce-scatter get a class calibrated on both planes before any step; then each route is forced and
+    # checked exactly at that size, and no further class appears
+    big = 256 << 20  # 256 Mi bf16 elements = 512 MiB
+    added = rc.prepare([("all_gather", torch.bfloat16, 2 * big), ("reduce_scatter", torch.bfloat16, 2 * big)])
+    assert added == [512 * MiB] and rc.sizes[-1] == 512 * MiB, rc.sizes
+    n_classes = len(rc.sizes)
     for route in ("primary", "fast"):
         rc.table = {k: [route] * len(rc.sizes) for k in rc.table}
-        y.fill_(float(rank + 1))
-        rc.all_reduce(y, "sum")
+        y = torch.empty(big, dtype=torch.bfloat16, device=dev)
+        rc.all_gather_into(y, torch.full((big // ws,), float(rank + 1), dtype=torch.bfloat16, device=dev))
         o = torch.empty(big // ws, dtype=torch.bfloat16, device=dev)
         rc.reduce_scatter_into(o, torch.ones(big, dtype=torch.bfloat16, device=dev), "sum")
         torch.cuda.synchronize()
-        assert torch.equal(y[:: 1 << 16].cpu(), torch.full((big >> 16,), float(sum(range(1, ws + 1))),
-                                                          dtype=torch.bfloat16)), route
+        want = torch.arange(1, ws + 1, dtype=torch.bfloat16, device=dev).repeat_interleave(big // ws)
+        assert torch.equal(y, want), route
         assert bool((o == float(ws)).all()), route
+        del want
+    assert len(rc.sizes) == n_classes
     del y, o
     rc.poll_errors()
     rc.destroy()

@@ -358,48 +358,6 @@ def test_fused_model_matches_fp32_reference(arch):
         assert _rel(p.grad, q.grad.to(DEV)) < 6e-2, n
 
 
-@pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
-                                         (4096, 2304, 768, 0), (4096, 2304, 768, -2), (1024, 384, 256, 7),
-                                         (512, 256, 128, 0), (2048, 512, 384, 64), (2048, 512, 384, 22),
-                                         (2048, 512, 384, 32), (1024, 384, 256, -1)])
-def test_gemm_tn_weight_gradient(K, M, N, split):
-    """C = A^T B (dW = dY^T X) vs fp32 torch: the LDS-DMA split-K kernel (split 0: its own choice; splits that
-    do not divide K; 1-3 stages per split, i.e. the ring's prologue/tail counts) and the register-staged
-    kernel (split < 0)."""
-    from distributed_training_amd.ops import native
-
-    torch.manual_seed(8)
-    a = torch.randn(K, M, device=DEV).bfloat16()
-    b = torch.randn(K, N, device=DEV).bfloat16()
-    ref = a.float().t() @ b.float()
-    c = native().gemm_tn(a, b, False, split)
-    assert c.shape == (M, N) and c.dtype == torch.bfloat16
-    assert _rel(c, ref) < 1e-2
-    c32 = native().gemm_tn(a, b, True, split)
-    assert _rel(c32, ref) < 1e-3
-    # A as a row-strided view (e.g. a slice of a wider activation)
-    wide = torch.randn(K, M + 128, device=DEV).bfloat16()
-    c2 = native().gemm_tn(wide[:, 64:64 + M], b, True, split)
-    assert _rel(c2, wide[:, 64:64 + M].float().t() @ b.float()) < 1e-3
-
-
-@pytest.mark.parametrize("K,M,N,split", [(8192, 768, 3072, 0), (512, 256, 128, 1), (1024, 384, 256, 4),
-                                         (4096, 2304, 768, 0), (1024, 384, 256, 7), (1024, 384, 256, -4)])
-def test_gemm_tn_fused_bias_gradient(K, M, N, split):
-    """dW = dY^T X and db = column sums of dY from one split-K launch vs fp32 torch."""
-    from distributed_training_amd.ops import native
-
-    torch.manual_seed(9)
-    a = torch.randn(K, M, device=DEV).bfloat16()
-    b = torch.randn(K, N, device=DEV).bfloat16()
-    c, db = native().gemm_tn_colsum(a, b, True, split)
-    assert _rel(c, a.float().t() @ b.float()) < 1e-3
-    assert db.shape == (M,) and db.dtype == torch.float32
-    assert _rel(db, a.float().sum(0)) < 1e-4
-    c16, db16 = native().gemm_tn_colsum(a, b, False, split)
-    assert db16.dtype == torch.bfloat16 and _rel(db16, a.float().sum(0)) < 1e-2
-
-
 @pytest.mark.parametrize("mode", ["dta", "torch"])
 def test_gelu_linear_fused_backward(mode, monkeypatch):
     """gelu(h) W^T + b with the GELU backward in the input-gradient GEMM's epilogue (DTA_GEMM=dta)

@@ -490,6 +490,40 @@ def test_routed_comm_cpu():
     run_gloo(_routed_cpu, 2)
 
 
+def _routed_prepare_cpu(rank, ws):
+    """The engines hand their message sizes to RoutedComm.prepare when they wrap the model: every
+    message past the default classes gets a class calibrated THEN (the DDP buckets here), and the
+    training steps that follow add none (no in-step calibration, verdict r4 item 6)."""
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.routed import MiB, RoutedComm
+
+    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB // 64,), iters=1)
+    added = rc.prepare([("all_reduce", torch.float32, 100_000), ("all_gather", torch.float32, 99_000),
+                        ("reduce_scatter", torch.float32, 1000), ("broadcast", torch.float32, 10 ** 6)])
+    assert added == [102_400] and rc.sizes == [MiB // 64, 102_400], rc.sizes  # one class, 4 KB multiple
+    assert [e["when"] for e in rc.prepared_log] == ["at wrap"]
+    assert set(rc.prepared_log[0]["routes"]) == {"all_gather float32", "all_reduce float32"}
+    assert rc.prepare([("all_reduce", torch.float32, 100_000)]) == []  # already covered
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 512))
+    ddp = DistributedDataParallel(net, comm=rc, bucket_cap_mb=0.3, first_bucket_mb=0.05)
+    sizes = sorted((b.end - b.start) * 4 for b in ddp.buckets)
+    assert sizes[-1] > MiB // 64  # a bucket past the default class: prepared at wrap
+    n_classes = len(rc.sizes)
+    assert n_classes > 2
+    g = torch.Generator().manual_seed(rank)
+    for _ in range(2):
+        ddp.zero_grad()
+        ddp(torch.randn(8, 64, generator=g)).square().mean().backward()
+    assert len(rc.sizes) == n_classes, "a class was calibrated inside a training step"
+    assert all(e["when"] == "at wrap" for e in rc.prepared_log)
+
+
+def test_routed_prepare_at_wrap_cpu():
+    run_gloo(_routed_prepare_cpu, 2)
+
+
 def _routed_lazy_cpu(rank, ws):
     """A message larger than every size class adds a class of its own on first use (calibrated for every
     op / dtype on all ranks at the same point), kept sorted; the same table on every rank; a calibration
