@@ -290,6 +290,8 @@ def main() -> None:
         out["gemm_impl"] = {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": ("hipblaslt" if not v else
                                                              f"k64/t{v - _lm.K64}" if v >= _lm.K64 else f"r2/t{v}")
                             for k, v in sorted(_lm._GEMM_CHOICE.items())}
+        src = list(_lm.GEMM_PICK_SOURCE.values())
+        out["gemm_pick_source"] = {s_: src.count(s_) for s_ in sorted(set(src))}  # tracked table vs in-run timing
     if rank == 0:
         print(json.dumps(out), flush=True)
         if args.json_out:

@@ -381,7 +381,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
         c = 0
     elif t is not None:
         c, src = t, "table"
-        if os.environ.get("DTA_GEMM_VERIFY", "0") == "1" and not torch.cuda.is_current_stream_capturing():
+        if os.environ.get("DTA_GEMM_VERIFY", "0") == "1" and not _capturing():
             times = _time_us(cands, rounds=_rounds())
             GEMM_TIMES[key] = times
             best = min(times, key=times.get)
@@ -391,7 +391,7 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
                 logging.getLogger(__name__).warning(
                     "GEMM %s %dx%dx%d: tracked pick %s measures %.1f us here, %s %.1f us", kind, M, N, K,
                     _impl_name(c), times[c], _impl_name(best), times[best])
-    elif mode == "dta" or torch.cuda.is_current_stream_capturing():
+    elif mode == "dta" or _capturing():
         c = dta[0]
         auto = native().gemm64_tile(M, N, K, 0)
         if K64 + auto in dta:
@@ -412,6 +412,10 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
     if mode == "auto":
         _save_cache()
     return c
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
 def _impl_name(c: int) -> str:
@@ -678,41 +682,38 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
     the results go straight into their flat gradient slices when :func:`_grad_dest` allows it."""
     K, M = dy2.shape
     N = x2.shape[1]
-    if M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1 \
-            and (M // 256) * (N // 256) <= _DEFER_MAX_TILES:
-        x2 = x2.contiguous() if x2.stride(0) % 8 else x2
-        cw = _grad_dest(w)
-        cb = _grad_dest(b) if with_bias else None
-        thr = _group_threshold()
-        if thr and cw is not None and (cb is not None or not with_bias) \
-                and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
-                and _single_use(w) and cw.stride(0) % 8 == 0 \
-                and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
-            # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
-            # holds ALIASES of the slices, never the tensors returned to autograd: a second
-            # reference to a returned gradient makes AccumulateGrad clone it instead of
-            # adopting it -- a copy of the slice taken BEFORE the deferred GEMM wrote it,
-            # which the DDP bucket copy then moved back over the GEMM's result whenever a
-            # flush fell between this backward and the bucket's launch (stale gradients)
-            _DEFER.append((dy2, x2, cw.view(cw.shape), None if cb is None else cb.view(cb.shape)))
-            _DEFER_TILES[0] += (M // 256) * (N // 256)
-            GEMM_STATS["deferred_wgrad"] += 1
-            _queue_end_join()
-            if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm64_group_max():
-                wgrad_flush()
-            return (cw, cb) if with_bias else cw
-        dw = gemm(dy2, x2, True, True, kind="wgrad", out=cw)
-        if with_bias:
-            db = native().bias_grad(dy2, False, -1)
-            if cb is not None:
-                cb.copy_(db)
-                db = cb
-            return dw, db
+    cw = _grad_dest(w)
+    cb = _grad_dest(b) if with_bias else None
+    thr = _group_threshold()
+    if thr and M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1 \
+            and (M // 256) * (N // 256) <= _DEFER_MAX_TILES and x2.stride(0) % 8 == 0 \
+            and cw is not None and (cb is not None or not with_bias) \
+            and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
+            and _single_use(w) and cw.stride(0) % 8 == 0 \
+            and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
+        # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
+        # holds ALIASES of the slices, never the tensors returned to autograd: a second
+        # reference to a returned gradient makes AccumulateGrad clone it instead of
+        # adopting it -- a copy of the slice taken BEFORE the deferred GEMM wrote it,
+        # which the DDP bucket copy then moved back over the GEMM's result whenever a
+        # flush fell between this backward and the bucket's launch (stale gradients)
+        _DEFER.append((dy2, x2, cw.view(cw.shape), None if cb is None else cb.view(cb.shape)))
+        _DEFER_TILES[0] += (M // 256) * (N // 256)
+        GEMM_STATS["deferred_wgrad"] += 1
+        _queue_end_join()
+        if _DEFER_TILES[0] >= thr or len(_DEFER) >= 4 * native().gemm64_group_max():
+            wgrad_flush()
+        return (cw, cb) if with_bias else cw
+    if cw is not None and not (cw.is_contiguous() and cw.data_ptr() % 16 == 0):
+        cw = None  # (an unaligned slice stays claimed: autograd's result is copied in)
+    dw = gemm(dy2, x2, True, True, kind="wgrad", out=cw)
+    if not with_bias:
         return dw
-    dw = gemm(dy2, x2, True, True, kind="wgrad", out=_grad_dest(w))
-    if with_bias:
-        return dw, native().bias_grad(dy2, False, -1)
-    return dw
+    db = native().bias_grad(dy2, False, -1)
+    if cb is not None:
+        cb.copy_(db)
+        db = cb
+    return dw, db
 
 
 class _Linear(Function):

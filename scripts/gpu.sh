@@ -12,6 +12,7 @@
 #   bash scripts/gpu.sh shared <n> <tag> <script args>  n ranks sharing this GPU (DTA_SHARED_GPU=1, IPC comm)
 #   bash scripts/gpu.sh gemm [models] [rounds]      scripts/bench_gemm64.py -> gpurun_out/gemm64_bench.jsonl
 #   bash scripts/gpu.sh w4 [models] [rounds] [tiles]  scripts/bench_w4.py (forward GEMMs) -> gpurun_out/w4_bench.jsonl
+#   bash scripts/gpu.sh table [--out F] [--check F]   scripts/gemm_table.py (the tracked GEMM table) -> gpurun_out/gemm_table.jsonl
 #
 # Every GPU step runs under its own timeout; a failing step ends the script (set -e).
 set -euo pipefail
@@ -70,6 +71,10 @@ case "$task" in
     timeout -k 10 600 python scripts/bench_w4.py ${1:-llama,gpt2} ${2:-5} ${3:-5,6,7,8,3} ${4:-fwd,dgrad,wgrad} > gpurun_out/w4_bench.jsonl \
       2> gpurun_out/w4_bench.err || { tail -20 gpurun_out/w4_bench.err; exit 1; }
     cut -c1-240 gpurun_out/w4_bench.jsonl ;;
+  table)
+    timeout -k 10 1200 python -u scripts/gemm_table.py "$@" > gpurun_out/gemm_table.jsonl 2> gpurun_out/gemm_table.err \
+      || { tail -30 gpurun_out/gemm_table.err; exit 1; }
+    tail -3 gpurun_out/gemm_table.jsonl | cut -c1-300 ;;
   *)
     echo "unknown task $task" >&2; exit 2 ;;
 esac

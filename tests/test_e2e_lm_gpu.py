@@ -47,7 +47,7 @@ GPU_WIDTH = ["model.n_embd=256"]
 
 
 @pytest.mark.parametrize("name,args", [
-    ("llama_fsdp", TINY_LLAMA + GPU_WIDTH + ["model.ffn_hidden=512", "train=llama3_8b_fsdp", "+train.step_graph=true",
+    ("llama_fsdp", TINY_LLAMA + GPU_WIDTH + ["model.ffn_hidden=512", "train=llama3_8b_fsdp", "train.step_graph=true",
                                              "train.dataset_size=64"]),
     ("gpt2_ddp", TINY_GPT2 + GPU_WIDTH + ["train=gpt2_ddp", "train.dataset_size=128"]),
 ])

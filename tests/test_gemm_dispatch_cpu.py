@@ -1,0 +1,91 @@
+"""The GEMM dispatcher's tracked per-shape table (ops/gemm_table_mi355x.json; verdict r4 item 1c):
+a shape in the table takes the table's pick with NO in-run timing (two boxes pick the same kernel),
+a shape missing from it is timed; the table's picks are valid implementation ids, and the table
+covers every GEMM kind / shape of the GPT-2 small and Llama-3 8B steps."""
+import json
+
+import pytest
+import torch
+
+from distributed_training_amd.ops import lm
+
+
+def _fresh(monkeypatch, table_on=True):
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    monkeypatch.setattr(lm, "GEMM_PICK_SOURCE", {})
+    monkeypatch.setattr(lm, "GEMM_TIMES", {})
+    monkeypatch.setattr(lm, "_TABLE", {})
+    monkeypatch.setattr(lm, "_TABLE_LOADED", [False])
+    monkeypatch.setattr(lm, "_CACHE_LOADED", [True])
+    monkeypatch.setattr(lm, "_gfx950", lambda: table_on)
+    monkeypatch.delenv("DTA_GEMM", raising=False)
+    monkeypatch.delenv("DTA_GEMM_TABLE", raising=False)
+    monkeypatch.delenv("DTA_GEMM_CACHE", raising=False)
+
+
+def test_table_is_valid_and_covers_the_lm_steps():
+    doc = json.load(open(lm.TABLE_PATH))
+    assert "gfx950" in doc["arch"] and doc["rounds"] >= 9
+    valid = {0} | {lm.K64 + t for t in lm.K64_TILES}
+    kinds = set()
+    for key, e in doc["entries"].items():
+        kind, dims = key.rsplit(" ", 1)
+        M, N, K = (int(x) for x in dims.split("x"))
+        assert M > 0 and N > 0 and K > 0
+        assert e["pick"] in valid, key
+        # the pick is the fastest median measured (hipBLASLt wins only when it is faster)
+        us = e["us"]
+        if kind not in ("fwd_gelu", "fwd_gelub"):  # (the GELU dual store keeps its 15 % handicap)
+            assert us[e["pick_name"]] <= min(us.values()) * 1.0001, key
+        kinds.add(kind)
+    assert {"fwd", "fwdb", "dgrad", "wgrad", "head_fwd", "head_dgrad", "head_wgrad", "dgelu",
+            "fwd_gelub"} <= kinds
+    for key in ("fwd 8192x4096x4096", "dgrad 8192x14336x4096", "wgrad 28672x4096x8192", "head_fwd 8192x128256x4096",
+                "fwdb 8192x2304x768", "head_fwd 8192x50304x768", "dgelu 8192x3072x768"):
+        assert key in doc["entries"], key
+
+
+def test_table_pick_needs_no_timing(monkeypatch):
+    _fresh(monkeypatch)
+
+    def boom(*a, **k):
+        raise AssertionError("timed a shape that is in the tracked table")
+
+    monkeypatch.setattr(lm, "_time_us", boom)
+    table = lm.gemm_table()
+    key = ("fwd", 8192, 4096, 4096)
+    assert key in table
+    cands = {0: lambda: None, **{lm.K64 + t: (lambda: None) for t in lm.K64_TILES}}
+    c = lm._pick(*key, cands)
+    assert c == table[key] and lm.GEMM_PICK_SOURCE[key] == "table"
+
+
+def test_shape_missing_from_table_is_timed(monkeypatch):
+    _fresh(monkeypatch)
+    monkeypatch.setattr(lm, "_time_us", lambda cands, rounds=5, reps=4: {k: (10.0 if k else 12.0) for k in cands})
+    cands = {0: lambda: None, lm.K64 + 5: lambda: None}
+    c = lm._pick("fwd", 1024, 1024, 1024, cands)  # not a GPT-2 / Llama shape
+    assert c == lm.K64 + 5 and lm.GEMM_PICK_SOURCE[("fwd", 1024, 1024, 1024)] == "timed"
+    # library faster -> library
+    monkeypatch.setattr(lm, "_time_us", lambda cands, rounds=5, reps=4: {k: (12.0 if k else 10.0) for k in cands})
+    assert lm._pick("fwd", 2048, 1024, 1024, cands) == 0
+
+
+def test_table_off_switch(monkeypatch):
+    _fresh(monkeypatch)
+    monkeypatch.setenv("DTA_GEMM_TABLE", "0")
+    assert lm.gemm_table() == {}
+    _fresh(monkeypatch, table_on=False)  # not a gfx950: no table
+    assert lm.gemm_table() == {}
+
+
+@pytest.mark.parametrize("mode", ["torch", "dta"])
+def test_forced_modes_ignore_table(monkeypatch, mode):
+    _fresh(monkeypatch)
+    monkeypatch.setenv("DTA_GEMM", mode)
+    if mode == "dta":
+        monkeypatch.setattr(lm, "native", lambda: type("N", (), {"gemm64_tile": staticmethod(lambda M, N, K, t: 5)})())
+    cands = {0: lambda: None, lm.K64 + 5: lambda: None}
+    c = lm._pick("fwd", 8192, 4096, 4096, cands)
+    assert c == (0 if mode == "torch" else lm.K64 + 5)
+    assert torch.cuda.is_available() or True

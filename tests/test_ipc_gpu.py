@@ -665,6 +665,6 @@ def _hsdp_worker(rank, ws, shard_size):
     rep.destroy()
 
 
-@pytest.mark.parametrize("ws,shard_size", [(4, 2), (8, 4)])
+@pytest.mark.parametrize("ws,shard_size", [(2, 1), (4, 2), (8, 4)])  # (2, 1): one rank per shard group
 def test_hybrid_shard_shared_gpu(ws, shard_size):
     run_gloo(_hsdp_worker, ws, shard_size)
