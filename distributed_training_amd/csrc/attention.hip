@@ -178,6 +178,48 @@ __device__ __forceinline__ void tile_store(const TileRegs<R, D, NT>& t, bf16* ld
   }
 }
 
+// Buffer-descriptor form of tile_load: each thread's byte offsets within the tile are computed ONCE per
+// kernel (tile_offsets) and a load is one buffer_load_dwordx4 at offset + the tile's first-row byte offset
+// (one VALU add).  Rows past the matrix read as zeros through the descriptor's range check (num_records =
+// the bytes up to the last row's D columns) -- instead of tile_load's per-load 64-bit address arithmetic
+// and the exec-masked branch around every load (~150 instructions per 64-query slice of the dK/dV kernel,
+// next to its 64 MFMAs at one wave per SIMD).  The host checks every such span is below 2 GiB.
+template <int R, int D, int NT>
+struct TileOffs {
+  unsigned o[TileRegs<R, D, NT>::N];
+};
+
+template <int R, int D, int NT>
+__device__ __forceinline__ void tile_offsets(TileOffs<R, D, NT>& t, int64_t rs, int tid) {
+#pragma unroll
+  for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
+    int r, c8;
+    stage_rc<D>(tid + l * NT, r, c8);
+    t.o[l] = (unsigned)((r * rs + c8) * 2);
+  }
+}
+
+// descriptor over rows [0, nrows) of an [nrows][rs] bf16 matrix at `base` (D columns used per row)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const bf16* base, int64_t rs, int nrows, int D) {
+  const uint64_t v = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const int64_t bytes = nrows > 0 ? ((int64_t)(nrows - 1) * rs + D) * 2 : 0;
+  const uint32_t num = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<bf16*>(((uint64_t)hi << 32) | lo), 0, num, 0x00020000);
+}
+
+template <int R, int D, int NT>
+__device__ __forceinline__ void tile_load_buf(TileRegs<R, D, NT>& t, __amdgpu_buffer_rsrc_t rsrc,
+                                              const TileOffs<R, D, NT>& o, unsigned row_bytes) {
+#pragma unroll
+  for (int l = 0; l < TileRegs<R, D, NT>::N; ++l) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o.o[l] + row_bytes, 0, 0);
+    t.v[l] = __builtin_bit_cast(bf16x8, v);
+  }
+}
+
 __device__ __forceinline__ f32x16 splat16(float x) {
   return f32x16{x, x, x, x, x, x, x, x, x, x, x, x, x, x, x, x};
 }
@@ -338,24 +380,25 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
       __builtin_amdgcn_sched_barrier(0);
     });
   };
+  const __amdgpu_buffer_rsrc_t rsK = rows_rsrc(kbase, a.k_ss, a.S, D), rsV = rows_rsrc(vbase, a.v_ss, a.S, D);
+  TileOffs<BN, D, NT> offK, offV;
+  tile_offsets(offK, a.k_ss, tid);
+  tile_offsets(offV, a.v_ss, tid);
+  auto kv_load = [&](TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr, int row0) {
+    tile_load_buf(kr, rsK, offK, (unsigned)(row0 * a.k_ss * 2));
+    tile_load_buf(vr, rsV, offV, (unsigned)(row0 * a.v_ss * 2));
+  };
   if constexpr (D == 64) {
   constexpr int AHEAD = 2;
   TileRegs<BN, D, NT> krA, vrA, krB, vrB;
-  tile_load(krA, kbase, a.k_ss, 0, a.S, tid);
-  tile_load(vrA, vbase, a.v_ss, 0, a.S, tid);
-  if (nblk > 1) {
-    tile_load(krB, kbase, a.k_ss, BN, a.S, tid);
-    tile_load(vrB, vbase, a.v_ss, BN, a.S, tid);
-  }
+  kv_load(krA, vrA, 0);
+  if (nblk > 1) kv_load(krB, vrB, BN);
   auto block = [&](int j, TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr) {
     const int buf = j & 1;
     tile_store(kr, Ks[buf], tid);
     tile_store(vr, Vs[buf], tid);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (j + AHEAD < nblk) {  // this set's next tile; its latency hides behind AHEAD blocks of MFMAs
-      tile_load(kr, kbase, a.k_ss, (j + AHEAD) * BN, a.S, tid);
-      tile_load(vr, vbase, a.v_ss, (j + AHEAD) * BN, a.S, tid);
-    }
+    if (j + AHEAD < nblk) kv_load(kr, vr, (j + AHEAD) * BN);  // its latency hides behind AHEAD blocks of MFMAs
       const int k0 = j * BN;
       if (CAUSAL && k0 > q0w + 31) return;  // every key of the block is after this wave's queries
       attend(Ks[buf], Vs[buf], k0);
@@ -366,17 +409,13 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   }
   } else {
     TileRegs<BN, D, NT> kr, vr;
-    tile_load(kr, kbase, a.k_ss, 0, a.S, tid);
-    tile_load(vr, vbase, a.v_ss, 0, a.S, tid);
+    kv_load(kr, vr, 0);
     for (int j = 0; j < nblk; ++j) {
       const int buf = j & 1;
       tile_store(kr, Ks[buf], tid);
       tile_store(vr, Vs[buf], tid);
       __syncthreads();
-      if (j + 1 < nblk) {  // next tile's HBM latency hides behind this tile's MFMAs
-        tile_load(kr, kbase, a.k_ss, (j + 1) * BN, a.S, tid);
-        tile_load(vr, vbase, a.v_ss, (j + 1) * BN, a.S, tid);
-      }
+      if (j + 1 < nblk) kv_load(kr, vr, (j + 1) * BN);  // next tile's HBM latency hides behind this tile's MFMAs
       const int k0 = j * BN;
       if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
       const bf16* Kb = Ks[buf];
@@ -464,6 +503,32 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
 // the barriers per MFMA and doubles the compute behind each slice's prefetch
 // (D = 128 runs one wave per SIMD: K/V fragments + dK/dV accumulators fill the
 // register file; D = 64 keeps two; 32-row slices measured 5 % slower at GPT-2).
+// Op order of a backward block of two 32-row tiles (ILV, the dK/dV slice and the dQ block): tile 0's NA
+// score ops (S / dP) | tile 1's NA score ops + tile 0's softmax | tile 0's NC gradient ops + tile 1's softmax |
+// tile 1's NC gradient ops.  op o -> (tile, op within the tile); without IL the tiles run one after the other.
+template <bool IL, int NA, int NC>
+__host__ __device__ constexpr int ilv_qt(int o) {
+  return !IL ? o / (NA + NC) : (o < NA ? 0 : o < 2 * NA ? 1 : o < 2 * NA + NC ? 0 : 1);
+}
+template <bool IL, int NA, int NC>
+__host__ __device__ constexpr int ilv_k(int o) {
+  return !IL ? o % (NA + NC)
+             : (o < NA ? o : o < 2 * NA ? o - NA : o < 2 * NA + NC ? NA + (o - 2 * NA) : NA + (o - 2 * NA - NC));
+}
+// the softmax part that op o carries (IL): {tile, part, elements per part} or tile -1 (none)
+template <int NA, int NC>
+__host__ __device__ constexpr int ilv_fill_tile(int o) {
+  return o >= NA && o < 2 * NA ? 0 : o >= 2 * NA && o < 2 * NA + NC ? 1 : -1;
+}
+template <int NA, int NC>
+__host__ __device__ constexpr int ilv_fill_part(int o) {
+  return o < 2 * NA ? o - NA : o - 2 * NA;
+}
+template <int NA, int NC>
+__host__ __device__ constexpr int ilv_fill_epp(int o) {
+  return o < 2 * NA ? 16 / NA : 16 / NC;
+}
+
 template <int D>
 struct DkdvCfg {
   static constexpr int kBM = 64;
@@ -472,7 +537,7 @@ struct DkdvCfg {
   static constexpr int kAhead = D == 64 ? 2 : 1;   // slices between a tile's global load and its LDS store
 };
 
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool ILV>
 __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int BM = DkdvCfg<D>::kBM;  // query rows per slice
   constexpr int NQT = BM / 32;         // 32-row query tiles per slice
@@ -552,11 +617,17 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     float rc = 0.f;
   };
   Stage sA, sB;
+  TileOffs<BM, D, 256> offQ, offD;  // (per-thread byte offsets, once: the slices only move the row offset)
+  tile_offsets(offQ, a.q_ss, tid);
+  tile_offsets(offD, a.do_ss, tid);
   auto load = [&](int it, Stage& st) {
     const int hq = hk * group + it / nslice;
     const int q0 = qstart + (it % nslice) * BM;
-    tile_load(st.q, static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, q0, a.S, tid);
-    tile_load(st.d, static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, q0, a.S, tid);
+    tile_load_buf(st.q, rows_rsrc(static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, a.S, D),
+                  offQ, (unsigned)(q0 * a.q_ss * 2));
+    tile_load_buf(st.d,
+                  rows_rsrc(static_cast<const bf16*>(a.dout) + (int64_t)b * a.do_sb + (int64_t)hq * D, a.do_ss, a.S, D),
+                  offD, (unsigned)(q0 * a.do_ss * 2));
     if (tid < 2 * BM) {
       const int qq = q0 + tid % BM;
       const int64_t ri = ((int64_t)b * a.H + hq) * a.S + qq;
@@ -586,23 +657,29 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     // compiler's own schedule put an lgkmcnt(0) before every MFMA of the D = 128 kernel.
     constexpr int NA = 2 * NKS, NC = 4 * NDT, NOP = NA + NC, TOT = NQT * NOP;
     constexpr int PF = DkdvCfg<D>::kPrefetch, RING = PF + 1;
+    // ILV (two 32-query tiles, NA == NC): the op order tile-0 S/dP | tile-1 S/dP | tile-0 dV/dK | tile-1 dV/dK,
+    // with tile 0's softmax spread over the tile-1 S/dP MFMAs and tile 1's over the tile-0 dV/dK MFMAs
+    // (16 / NA score elements per MFMA gap: one exp2, two multiplies and half a bf16 pair-conversion each --
+    // within the ~5 single-issue instructions a 32-cycle MFMA gap hides at one wave per SIMD,
+    // MI355X_MICROARCH.md cycle constants; cdna_hip_programming.md T15).  Without it the softmax of a tile
+    // sat between its S/dP and its dV/dK MFMAs with no MFMA in flight: ~130 VALU per tile, exposed.
+    constexpr bool IL = ILV && NQT == 2 && 16 % NA == 0 && 16 % NC == 0;
     bf16x8 ring[RING][2];
-    f32x16 s, dp;
-    bf16x8 pb[2], db[2];
+    f32x16 s[NQT], dp[NQT];
+    bf16x8 pb[NQT][2], db[NQT][2];
     auto issue = [&](auto oc) {
-      constexpr int o = decltype(oc)::value, qt = o / NOP, k = o % NOP;
+      constexpr int o = decltype(oc)::value, qt = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       bf16x8(&f)[2] = ring[o % RING];
       if (k == 0) {
         // row constants of this lane's 16 accumulator rows as the initial accumulators: rows
-        // qt*32 + 8g + 4hh + 0..3 are 4 consecutive floats (s / dp are free: the previous tile's
-        // softmax consumed them)
+        // qt*32 + 8g + 4hh + 0..3 are 4 consecutive floats
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int q4 = qt * 32 + 8 * g + 4 * hh;
           const float4 sv = *reinterpret_cast<const float4*>(&rc[buf][0][q4]);
           const float4 dv = *reinterpret_cast<const float4*>(&rc[buf][1][q4]);
-          s[4 * g] = sv.x; s[4 * g + 1] = sv.y; s[4 * g + 2] = sv.z; s[4 * g + 3] = sv.w;
-          dp[4 * g] = dv.x; dp[4 * g + 1] = dv.y; dp[4 * g + 2] = dv.z; dp[4 * g + 3] = dv.w;
+          s[qt][4 * g] = sv.x; s[qt][4 * g + 1] = sv.y; s[qt][4 * g + 2] = sv.z; s[qt][4 * g + 3] = sv.w;
+          dp[qt][4 * g] = dv.x; dp[qt][4 * g + 1] = dv.y; dp[qt][4 * g + 2] = dv.z; dp[qt][4 * g + 3] = dv.w;
         }
       }
       if constexpr (k < NA) {
@@ -613,48 +690,68 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
         f[0] = tr_frag<D>((cc & 1) ? Qb : Db, qt * 32, dt * 32, st, lane);
       }
     };
+    // softmax of tile t, part j: score elements [j * E, (j + 1) * E) -> P = exp2(c S'), dS = P dP, and
+    // their bf16 pairs (the B operands of the dV^T / dK^T MFMAs)
+    auto sm_part = [&](auto tc, auto jc, auto ec) {
+      constexpr int t = decltype(tc)::value, j = decltype(jc)::value, E = decltype(ec)::value;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        constexpr int i0 = j * E;
+        const int i = i0 + e;
+        const float pv = fexp2(s[t][i] * c);
+        s[t][i] = pv;              // P
+        dp[t][i] = pv * dp[t][i];  // dS (unscaled)
+        if (i & 1) {  // a finished pair -> packed bf16 (one v_cvt_pk each)
+          pb[t][i >> 3][(i & 7) - 1] = f2bf(s[t][i - 1]);
+          pb[t][i >> 3][i & 7] = f2bf(s[t][i]);
+          db[t][i >> 3][(i & 7) - 1] = f2bf(dp[t][i - 1]);
+          db[t][i >> 3][i & 7] = f2bf(dp[t][i]);
+        }
+        if constexpr (IL) {
+          // pinned in this MFMA gap: the compiler would otherwise sink the whole softmax down to its first
+          // use (the tile's dV / dK MFMAs), past the gaps it is meant to fill
+          if (i & 1) asm volatile("" : "+v"(pb[t][i >> 3]), "+v"(db[t][i >> 3]));
+          else asm volatile("" : "+v"(s[t][i]), "+v"(dp[t][i]));
+        }
+      }
+      // pb / db are VALU results read by the asm MFMAs of the tile's dV / dK ops: wait states the compiler
+      // cannot know to add
+      if constexpr (KREG && (j + 1) * E == 16) asm volatile("s_nop 4" ::: "memory");
+    };
     auto compute = [&](auto oc) {
-      constexpr int o = decltype(oc)::value, qt = o / NOP, k = o % NOP;
+      constexpr int o = decltype(oc)::value, qt = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       const bf16x8(&f)[2] = ring[o % RING];
       if constexpr (k < NA) {
         if constexpr (KREG) {
-          if (k & 1) dp = mfma32x32x16(f[0], vf[k >> 1], dp);
-          else s = mfma32x32x16(f[0], kf[k >> 1], s);
+          if (k & 1) dp[qt] = mfma32x32x16(f[0], vf[k >> 1], dp[qt]);
+          else s[qt] = mfma32x32x16(f[0], kf[k >> 1], s[qt]);
         } else {
-          if (k & 1) dp = mfma32x32x16(f[0], f[1], dp);
-          else s = mfma32x32x16(f[0], f[1], s);
+          if (k & 1) dp[qt] = mfma32x32x16(f[0], f[1], dp[qt]);
+          else s[qt] = mfma32x32x16(f[0], f[1], s[qt]);
         }
         if constexpr (k == NA - 1) {
+          // the causal mask of the tile as soon as its scores are complete (a wave-uniform branch: diagonal
+          // tiles only), before any part of its softmax: key > query q0 + row(i) + 4hh <=> dl > row(i)
           const int q0 = q0s + qt * 32;
-          // key > query q0 + row(i) + 4hh <=> dl > row(i): one compare against an immediate
-          // (a wave-uniform branch around the compare / select: only the diagonal slices pay them)
           if (CAUSAL && q0 < kw0 + 31) {
             const int dl = key - q0 - 4 * hh;
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-              if (dl > mfma32_row(i, 0)) s[i] = kNegBig;  // exp2 -> P = 0
+              if (dl > mfma32_row(i, 0)) s[qt][i] = kNegBig;  // exp2 -> P = 0
           }
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float pv = fexp2(s[i] * c);
-            s[i] = pv;             // P
-            dp[i] = pv * dp[i];    // dS (unscaled)
-          }
-#pragma unroll
-          for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              pb[st][j] = f2bf(s[8 * st + j]);
-              db[st][j] = f2bf(dp[8 * st + j]);
-            }
-          // pb / db are VALU results read by the asm MFMAs below: wait states the compiler cannot know to add
-          if constexpr (KREG) asm volatile("s_nop 4" ::: "memory");
+          if constexpr (!IL)  // (the whole softmax of the tile right after its S / dP)
+            sm_part(std::integral_constant<int, qt>{}, std::integral_constant<int, 0>{},
+                    std::integral_constant<int, 16>{});
         }
       } else {
         constexpr int cc = k - NA, st = (cc >> 1) / NDT, dt = (cc >> 1) % NDT;
-        if constexpr (cc & 1) mma_acc(dkacc[dt], f[0], db[st]);
-        else mma_acc(dvacc[dt], f[0], pb[st]);
+        if constexpr (cc & 1) mma_acc(dkacc[dt], f[0], db[qt][st]);
+        else mma_acc(dvacc[dt], f[0], pb[qt][st]);
       }
+      if constexpr (IL && ilv_fill_tile<NA, NC>(o) >= 0)
+        sm_part(std::integral_constant<int, ilv_fill_tile<NA, NC>(o)>{},
+                std::integral_constant<int, ilv_fill_part<NA, NC>(o)>{},
+                std::integral_constant<int, ilv_fill_epp<NA, NC>(o)>{});
     };
     static_for<PF>([&](auto oc) { issue(oc); });
     static_for<TOT>([&](auto oc) {
@@ -707,7 +804,7 @@ struct DqCfg {
   static constexpr int kAhead = D == 64 ? 2 : 1;
 };
 
-template <int D, bool CAUSAL, int NW>
+template <int D, bool CAUSAL, int NW, bool ILV>
 __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   constexpr int QB = NW * 32;
@@ -773,22 +870,23 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
     TileRegs<BN, D, NT> k, v;
   };
   Stage sA, sB;
-  tile_load(sA.k, kbase, a.k_ss, 0, a.S, tid);
-  tile_load(sA.v, vbase, a.v_ss, 0, a.S, tid);
-  if (AHEAD == 2 && nblk > 1) {
-    tile_load(sB.k, kbase, a.k_ss, BN, a.S, tid);
-    tile_load(sB.v, vbase, a.v_ss, BN, a.S, tid);
-  }
+  const __amdgpu_buffer_rsrc_t rsK = rows_rsrc(kbase, a.k_ss, a.S, D), rsV = rows_rsrc(vbase, a.v_ss, a.S, D);
+  TileOffs<BN, D, NT> offK, offV;
+  tile_offsets(offK, a.k_ss, tid);
+  tile_offsets(offV, a.v_ss, tid);
+  auto kv_load = [&](Stage& st, int row0) {
+    tile_load_buf(st.k, rsK, offK, (unsigned)(row0 * a.k_ss * 2));
+    tile_load_buf(st.v, rsV, offV, (unsigned)(row0 * a.v_ss * 2));
+  };
+  kv_load(sA, 0);
+  if (AHEAD == 2 && nblk > 1) kv_load(sB, BN);
   auto block_it = [&](int j, Stage& cur) {
     const int buf = j & 1;
     tile_store(cur.k, Ks[buf], tid);
     tile_store(cur.v, Vs[buf], tid);
     if constexpr (AHEAD == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else __syncthreads();
-    if (j + AHEAD < nblk) {
-      tile_load(cur.k, kbase, a.k_ss, (j + AHEAD) * BN, a.S, tid);
-      tile_load(cur.v, vbase, a.v_ss, (j + AHEAD) * BN, a.S, tid);
-    }
+    if (j + AHEAD < nblk) kv_load(cur, (j + AHEAD) * BN);
     const int k0 = j * BN;
     if (CAUSAL && k0 > q0w + 31) return;
     const bf16* Kb = Ks[buf];
@@ -801,11 +899,14 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
     // is read PF ops ahead into a register ring (sched_barriers pin the order).
     constexpr int NA = 2 * NKS, NC = 2 * NDT, NOP = NA + NC, TOT = 2 * NOP;
     constexpr int PF = DqCfg<D>::kPrefetch, RING = PF + 1;
+    // ILV: the dK/dV slice's op order (ilv_qt): tile 0's softmax in the tile-1 S^T / dP^T MFMA gaps, tile 1's
+    // in the tile-0 dQ^T gaps, instead of a VALU block between a tile's score and gradient MFMAs
+    constexpr bool IL = ILV && 16 % NA == 0 && 16 % NC == 0;
     bf16x8 ring[RING];
-    f32x16 s, dp;
-    bf16x8 db[2];
+    f32x16 s[2], dp[2];
+    bf16x8 db[2][2];
     auto issue = [&](auto oc) {
-      constexpr int o = decltype(oc)::value, t = o / NOP, k = o % NOP;
+      constexpr int o = decltype(oc)::value, t = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       if constexpr (k < NA) {
         ring[o % RING] = row_frag<D>((k & 1) ? Vb : Kb, t * 32 + r32, k >> 1, hh);
       } else {
@@ -813,38 +914,51 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
         ring[o % RING] = tr_frag<D>(Kb, t * 32, (cc % NDT) * 32, cc / NDT, lane);
       }
     };
+    // softmax of tile t, part j (elements [j E, (j + 1) E)): dS^T = exp2(c S'^T) dP'^T and its bf16 pairs
+    auto sm_part = [&](auto tc, auto jc, auto ec) {
+      constexpr int t = decltype(tc)::value, j = decltype(jc)::value, E = decltype(ec)::value;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = j * E + e;
+        dp[t][i] *= fexp2(s[t][i] * c);  // dS^T
+        if (i & 1) {
+          db[t][i >> 3][(i & 7) - 1] = f2bf(dp[t][i - 1]);
+          db[t][i >> 3][i & 7] = f2bf(dp[t][i]);
+          if constexpr (IL) asm volatile("" : "+v"(db[t][i >> 3]));  // pinned in this gap (see the dK/dV slice)
+        } else if constexpr (IL) {
+          asm volatile("" : "+v"(dp[t][i]));
+        }
+      }
+    };
     auto compute = [&](auto oc) {
-      constexpr int o = decltype(oc)::value, t = o / NOP, k = o % NOP;
+      constexpr int o = decltype(oc)::value, t = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       const bf16x8& f = ring[o % RING];
       if constexpr (k < NA) {
         if constexpr (k == 0) {
-          s = splat16(s_init);
-          dp = splat16(dp_init);
+          s[t] = splat16(s_init);
+          dp[t] = splat16(dp_init);
         }
-        if constexpr (k & 1) dp = mfma32x32x16(f, df[k >> 1], dp);
-        else s = mfma32x32x16(f, qf[k >> 1], s);
+        if constexpr (k & 1) dp[t] = mfma32x32x16(f, df[k >> 1], dp[t]);
+        else s[t] = mfma32x32x16(f, qf[k >> 1], s[t]);
         if constexpr (k == NA - 1) {
           // key k0 + t*32 + row(i) + 4hh > qrow <=> row(i) > ql
           if (need_mask) {  // wave-uniform: the diagonal blocks only
             const int ql = qrow - k0 - t * 32 - 4 * hh;
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-              if (mfma32_row(i, 0) > ql) s[i] = kNegBig;  // exp2 -> P = 0
+              if (mfma32_row(i, 0) > ql) s[t][i] = kNegBig;  // exp2 -> P = 0
           }
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float pv = fexp2(s[i] * c);
-            dp[i] *= pv;  // dS^T
-          }
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) db[s2][jj] = f2bf(dp[8 * s2 + jj]);
+          if constexpr (!IL)
+            sm_part(std::integral_constant<int, t>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 16>{});
         }
       } else {
         constexpr int cc = k - NA;
-        dqacc[cc % NDT] = mfma32x32x16(f, db[cc / NDT], dqacc[cc % NDT]);
+        dqacc[cc % NDT] = mfma32x32x16(f, db[t][cc / NDT], dqacc[cc % NDT]);
       }
+      if constexpr (IL && ilv_fill_tile<NA, NC>(o) >= 0)
+        sm_part(std::integral_constant<int, ilv_fill_tile<NA, NC>(o)>{},
+                std::integral_constant<int, ilv_fill_part<NA, NC>(o)>{},
+                std::integral_constant<int, ilv_fill_epp<NA, NC>(o)>{});
     };
     static_for<PF>([&](auto oc) { issue(oc); });
     static_for<TOT>([&](auto oc) {
@@ -915,12 +1029,23 @@ static hipError_t fwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the backward kernels' interleaved softmax (ILV) by default; DTA_ATTN_BWD_ILV=0: the round-4 op order (A/B)
+static bool bwd_ilv() {
+  const char* e = getenv("DTA_ATTN_BWD_ILV");
+  return !(e && e[0] == '0');
+}
+
 template <int D, int NW>
 static void dq_launch(const AttnArgs& a, bool causal, hipStream_t st) {
   const int nqb = (a.S + NW * 32 - 1) / (NW * 32);
   dim3 grid((unsigned)(nqb * a.B * a.H));
-  if (causal) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true, NW>), grid, dim3(NW * 64), 0, st, a);
-  else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false, NW>), grid, dim3(NW * 64), 0, st, a);
+  if (bwd_ilv()) {
+    if (causal) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true, NW, true>), grid, dim3(NW * 64), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false, NW, true>), grid, dim3(NW * 64), 0, st, a);
+  } else {
+    if (causal) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true, NW, false>), grid, dim3(NW * 64), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false, NW, false>), grid, dim3(NW * 64), 0, st, a);
+  }
 }
 
 template <int D>
@@ -934,8 +1059,13 @@ static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
     dq_launch<D, 4>(a, causal, st);
   }
   dim3 gkv((unsigned)(((a.S + 127) / 128) * a.B * a.Hkv));
-  if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true>), gkv, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false>), gkv, dim3(256), 0, st, a);
+  if (bwd_ilv()) {
+    if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true, true>), gkv, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false, true>), gkv, dim3(256), 0, st, a);
+  } else {
+    if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true, false>), gkv, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false, false>), gkv, dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 

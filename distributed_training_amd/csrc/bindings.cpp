@@ -332,6 +332,9 @@ void check_bshd(const torch::Tensor& t, const char* name, int64_t B, int64_t S, 
   TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == D, name, ": last dim contiguous and head stride == D required");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0,
               name, ": rows must be 16-byte aligned");
+  // the kernels load K / V / Q / dO tiles through buffer descriptors with 32-bit byte offsets from each
+  // (batch, head)'s first row (csrc/attention.hip rows_rsrc)
+  TORCH_CHECK(((S - 1) * t.stride(1) + D) * 2 < (int64_t)0x7fffffff, name, ": S x token stride must span < 2 GiB");
 }
 
 std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, bool causal, double scale,

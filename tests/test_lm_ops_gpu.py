@@ -21,8 +21,10 @@ def _rel(a, b):
                                                  (1, 1024, 2, 2, 128, True), (1, 320, 4, 2, 128, False),
                                                  (1, 600, 4, 2, 64, False)])
 @pytest.mark.parametrize("fwd_waves", ["4", "8"])
-def test_flash_attention_fwd_bwd(B, S, H, Hkv, D, causal, fwd_waves, monkeypatch):
+@pytest.mark.parametrize("bwd_ilv", ["1", "0"])
+def test_flash_attention_fwd_bwd(B, S, H, Hkv, D, causal, fwd_waves, bwd_ilv, monkeypatch):
     monkeypatch.setenv("DTA_ATTN_FWD_WAVES", fwd_waves)  # both forward workgroup shapes
+    monkeypatch.setenv("DTA_ATTN_BWD_ILV", bwd_ilv)  # backward softmax interleaved with the MFMAs (default) or not
     torch.manual_seed(0)
     q = torch.randn(B, S, H, D, device=DEV).bfloat16().requires_grad_()
     k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
