@@ -54,6 +54,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--overlap-opt", action="store_true",
                     help="native DDP / FSDP: AdamW per bucket / unit inside the backward (overlap_optimizer of "
                          "DistributedDataParallel / FullyShardedDataParallel) instead of after it; bit-identical")
+    ap.add_argument("--head-ce-chunk", type=int, default=0,
+                    help="LM head + CE in row blocks of this many tokens, never holding the [T, V] logits "
+                         "(ops/lm.py _ChunkedLinearCrossEntropy); 0 = one block")
     ap.add_argument("--tunableop", action="store_true",
                     help="let PyTorch's TunableOp pick the hipBLASLt/rocBLAS solution per GEMM shape (tuned in warmup)")
     return ap.parse_args()
@@ -119,6 +122,8 @@ def main() -> None:
     if args.impl == "native":
         from distributed_training_amd.ops import lm
         from distributed_training_amd.ops.optim import FusedAdamW
+
+        lm.set_head_ce_chunk(args.head_ce_chunk)
         from distributed_training_amd.parallel.comm import make_comm
 
         comm = make_comm(dev, bulk=True)  # DDP / FSDP traffic: RCCL or the IPC push plane per message size
@@ -282,6 +287,7 @@ def main() -> None:
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
         out["optimizer_in_backward"] = bool(overlap_opt)
         out["step_graph"] = graphed is not None
+        out["head_ce_chunk"] = _lm.HEAD_CE_CHUNK
         routes = getattr(getattr(wrapped, "comm", None), "routes", None)
         if routes is not None:
             out["comm_routes"] = routes()

@@ -192,6 +192,10 @@ def run(cfg: Any) -> Trainer:
         if hasattr(model, "enable_activation_checkpointing") and \
                 activation_checkpointing_wanted(cfg, model, env):
             model.enable_activation_checkpointing()
+        head_chunk = _get(cfg.train, "head_ce_chunk", None)
+        if head_chunk is not None:  # LM head + CE in row blocks (ops/lm.py _ChunkedLinearCrossEntropy)
+            from .ops import lm as _lm_ops
+            _lm_ops.set_head_ce_chunk(int(head_chunk))
         train_config = training_config_from(cfg, model)
         train_data = prepare_dataloader(dataset, train_config.batch_size)
         trainer = Trainer(model, train_data, optimizer, train_config, env)

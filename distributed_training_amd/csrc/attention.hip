@@ -225,6 +225,41 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 }
 
 // ------------------------------------------------------------------ forward
+#ifndef DTA_FWD_RESCALE_BRANCH
+#define DTA_FWD_RESCALE_BRANCH 1
+#endif
+// Online-softmax rescale of O and l when some row's max grew by more than kRescaleThr (log2 units):
+// otherwise m stays and the block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md T13; the
+// decision precedes every exponentiation of the block, so nothing at the old max is left unscaled).
+// The first block always rescales (m starts at -1e30).  DTA_FWD_RESCALE_BRANCH=0 (diagnostic builds,
+// scripts/attn_diag.hip): no branch -- alpha = 1 on the common path, and no PHI copies of the O
+// accumulators at the loop's back edge (the branchy form costs 32-64 v_mov_b64 per block at D = 128).
+template <int NDT>
+__device__ __forceinline__ void fwd_rescale(float mblk_c, float& m, float& l, f32x16 (&oacc)[NDT]) {
+#if DTA_FWD_RESCALE_BRANCH
+  if (__builtin_amdgcn_ballot_w64(mblk_c - m > kRescaleThr)) {
+    const float mnew = fmaxf(m, mblk_c);
+    const float alpha = fexp2(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+    m = mnew;
+  }
+#else
+  const bool up = __builtin_amdgcn_ballot_w64(mblk_c - m > kRescaleThr) != 0;
+  const float mnew = up ? fmaxf(m, mblk_c) : m;
+  const float alpha = fexp2(m - mnew);
+  l *= alpha;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+  m = mnew;
+#endif
+}
+
 // Occupancy the register budget is fitted to (waves per SIMD): the K/V double
 // buffer is 32 KB (D = 64) / 64 KB (D = 128) per workgroup.
 template <int D>
@@ -297,13 +332,13 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   // read PF ops ahead into a register ring and sched_barriers pin the order.  (D = 128 keeps
   // the compiler's schedule below: at two waves per SIMD in 256 registers the ring spilled
   // and that forward ran 10-29 % slower.)
-  auto attend = [&](const bf16* Kb, const bf16* Vb, int k0) {
+  auto attend = [&](const bf16* Kb, const bf16* Vb, int k0) __attribute__((always_inline)) {
     constexpr int NS = 2 * NKS, NP = 4 * NDT, TOT = NS + NP;
     constexpr int PF = FwdCfg<D>::kPrefetch, RING = PF + 1;
     bf16x8 ring[RING];
     f32x16 st[2];
     bf16x8 pb[2][2];
-    auto issue = [&](auto oc) {
+    auto issue = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value;
       if constexpr (o < NS) {
         ring[o % RING] = row_frag<D>(Kb, (o / NKS) * 32 + r32, o % NKS, hh);
@@ -312,7 +347,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
         ring[o % RING] = tr_frag<D>(Vb, t * 32, dt * 32, sh, lane);
       }
     };
-    auto compute = [&](auto oc) {
+    auto compute = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value;
       if constexpr (o < NS) {
         constexpr int t = o / NKS, ks = o % NKS;
@@ -338,16 +373,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
             for (int i = 0; i < 16; ++i) mblk = fmaxf(mblk, st[t2][i]);
           mblk = xor32_max(mblk);
           // rescale O and l only when some row's max grew by more than kRescaleThr (as below)
-          if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
-            const float mnew = fmaxf(m, mblk * c);
-            const float alpha = fexp2(m - mnew);
-            l *= alpha;
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-            m = mnew;
-          }
+          fwd_rescale<NDT>(mblk * c, m, l, oacc);
           float lsum = 0.f;
 #pragma unroll
           for (int t2 = 0; t2 < 2; ++t2)
@@ -384,7 +410,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   TileOffs<BN, D, NT> offK, offV;
   tile_offsets(offK, a.k_ss, tid);
   tile_offsets(offV, a.v_ss, tid);
-  auto kv_load = [&](TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr, int row0) {
+  auto kv_load = [&](TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr, int row0) __attribute__((always_inline)) {
     tile_load_buf(kr, rsK, offK, (unsigned)(row0 * a.k_ss * 2));
     tile_load_buf(vr, rsV, offV, (unsigned)(row0 * a.v_ss * 2));
   };
@@ -393,8 +419,10 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   TileRegs<BN, D, NT> krA, vrA, krB, vrB;
   kv_load(krA, vrA, 0);
   if (nblk > 1) kv_load(krB, vrB, BN);
-  auto block = [&](int j, TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr) {
-    const int buf = j & 1;
+  // (P: the block's LDS buffer parity, j & 1, as a compile-time constant: every LDS address of the block is a
+  // lane base + an immediate, no per-block address arithmetic)
+  auto block = [&](int j, TileRegs<BN, D, NT>& kr, TileRegs<BN, D, NT>& vr, auto P) __attribute__((always_inline)) {
+    constexpr int buf = decltype(P)::value;
     tile_store(kr, Ks[buf], tid);
     tile_store(vr, Vs[buf], tid);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -404,20 +432,20 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
       attend(Ks[buf], Vs[buf], k0);
   };
   for (int j = 0; j < nblk; j += 2) {
-    block(j, krA, vrA);
-    if (j + 1 < nblk) block(j + 1, krB, vrB);
+    block(j, krA, vrA, std::integral_constant<int, 0>{});
+    if (j + 1 < nblk) block(j + 1, krB, vrB, std::integral_constant<int, 1>{});
   }
   } else {
     TileRegs<BN, D, NT> kr, vr;
     kv_load(kr, vr, 0);
-    for (int j = 0; j < nblk; ++j) {
-      const int buf = j & 1;
+    auto blk = [&](int j, auto P) __attribute__((always_inline)) {
+      constexpr int buf = decltype(P)::value;  // (compile-time LDS buffer parity, as the D = 64 path)
       tile_store(kr, Ks[buf], tid);
       tile_store(vr, Vs[buf], tid);
       __syncthreads();
       if (j + 1 < nblk) kv_load(kr, vr, (j + 1) * BN);  // next tile's HBM latency hides behind this tile's MFMAs
       const int k0 = j * BN;
-      if (CAUSAL && k0 > q0w + 31) continue;  // every key of the block is after this wave's queries
+      if (CAUSAL && k0 > q0w + 31) return;  // every key of the block is after this wave's queries
       const bf16* Kb = Ks[buf];
       const bf16* Vb = Vs[buf];
       // ---- S^T tiles (raw scores): rows = keys k0 + t*32 + row, cols = this wave's queries ----
@@ -448,16 +476,7 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
       // otherwise m stays and this block's P are bounded by 2^kRescaleThr (cdna_hip_programming.md
       // T13; the decision precedes every exponentiation of the block, so nothing at the old max
       // is left unscaled).  The first block always rescales (m starts at -1e30).
-      if (__builtin_amdgcn_ballot_w64(mblk * c - m > kRescaleThr)) {
-        const float mnew = fmaxf(m, mblk * c);
-        const float alpha = fexp2(m - mnew);
-        l *= alpha;
-  #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt)
-  #pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-        m = mnew;
-      }
+      fwd_rescale<NDT>(mblk * c, m, l, oacc);
       float lsum = 0.f;
   #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -479,6 +498,10 @@ __global__ void __launch_bounds__(NW * 64, FwdCfg<D>::kWavesPerSimd) attn_fwd_ke
   #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma32x32x16(tr_frag<D>(Vb, t * 32, dt * 32, s, lane), pb, oacc[dt]);
         }
+    };
+    for (int j = 0; j < nblk; j += 2) {
+      blk(j, std::integral_constant<int, 0>{});
+      if (j + 1 < nblk) blk(j + 1, std::integral_constant<int, 1>{});
     }
   }
   // ---- epilogue: O = O^T^T / l ; LSE ----
@@ -620,7 +643,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   TileOffs<BM, D, 256> offQ, offD;  // (per-thread byte offsets, once: the slices only move the row offset)
   tile_offsets(offQ, a.q_ss, tid);
   tile_offsets(offD, a.do_ss, tid);
-  auto load = [&](int it, Stage& st) {
+  auto load = [&](int it, Stage& st) __attribute__((always_inline)) {
     const int hq = hk * group + it / nslice;
     const int q0 = qstart + (it % nslice) * BM;
     tile_load_buf(st.q, rows_rsrc(static_cast<const bf16*>(a.q) + (int64_t)b * a.q_sb + (int64_t)hq * D, a.q_ss, a.S, D),
@@ -637,8 +660,8 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   };
   load(0, sA);
   if (AHEAD == 2 && total > 1) load(1, sB);
-  auto slice_it = [&](int it, Stage& cur) {
-    const int buf = it & 1;
+  auto slice_it = [&](int it, Stage& cur, auto P) __attribute__((always_inline)) {
+    constexpr int buf = decltype(P)::value;  // it & 1, compile-time: LDS addresses as immediates
     tile_store(cur.q, Qs[buf], tid);
     tile_store(cur.d, dOs[buf], tid);
     if (tid < 2 * BM) rc[buf][tid / BM][tid % BM] = cur.rc;
@@ -667,7 +690,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     bf16x8 ring[RING][2];
     f32x16 s[NQT], dp[NQT];
     bf16x8 pb[NQT][2], db[NQT][2];
-    auto issue = [&](auto oc) {
+    auto issue = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value, qt = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       bf16x8(&f)[2] = ring[o % RING];
       if (k == 0) {
@@ -692,7 +715,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
     };
     // softmax of tile t, part j: score elements [j * E, (j + 1) * E) -> P = exp2(c S'), dS = P dP, and
     // their bf16 pairs (the B operands of the dV^T / dK^T MFMAs)
-    auto sm_part = [&](auto tc, auto jc, auto ec) {
+    auto sm_part = [&](auto tc, auto jc, auto ec) __attribute__((always_inline)) {
       constexpr int t = decltype(tc)::value, j = decltype(jc)::value, E = decltype(ec)::value;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -718,7 +741,7 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
       // cannot know to add
       if constexpr (KREG && (j + 1) * E == 16) asm volatile("s_nop 4" ::: "memory");
     };
-    auto compute = [&](auto oc) {
+    auto compute = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value, qt = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       const bf16x8(&f)[2] = ring[o % RING];
       if constexpr (k < NA) {
@@ -764,11 +787,14 @@ __global__ void __launch_bounds__(256, DkdvCfg<D>::kWavesPerSimd) attn_bwd_dkdv_
   };
   if constexpr (AHEAD == 2) {
     for (int it = 0; it < total; it += 2) {
-      slice_it(it, sA);
-      if (it + 1 < total) slice_it(it + 1, sB);
+      slice_it(it, sA, std::integral_constant<int, 0>{});
+      if (it + 1 < total) slice_it(it + 1, sB, std::integral_constant<int, 1>{});
     }
   } else {
-    for (int it = 0; it < total; ++it) slice_it(it, sA);
+    for (int it = 0; it < total; it += 2) {
+      slice_it(it, sA, std::integral_constant<int, 0>{});
+      if (it + 1 < total) slice_it(it + 1, sA, std::integral_constant<int, 1>{});
+    }
   }
   // the last MFMAs' results are still in the matrix pipe: wait states, then every accumulator through an
   // empty asm (the epilogue's reads depend on those outputs)
@@ -874,14 +900,14 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
   TileOffs<BN, D, NT> offK, offV;
   tile_offsets(offK, a.k_ss, tid);
   tile_offsets(offV, a.v_ss, tid);
-  auto kv_load = [&](Stage& st, int row0) {
+  auto kv_load = [&](Stage& st, int row0) __attribute__((always_inline)) {
     tile_load_buf(st.k, rsK, offK, (unsigned)(row0 * a.k_ss * 2));
     tile_load_buf(st.v, rsV, offV, (unsigned)(row0 * a.v_ss * 2));
   };
   kv_load(sA, 0);
   if (AHEAD == 2 && nblk > 1) kv_load(sB, BN);
-  auto block_it = [&](int j, Stage& cur) {
-    const int buf = j & 1;
+  auto block_it = [&](int j, Stage& cur, auto P) __attribute__((always_inline)) {
+    constexpr int buf = decltype(P)::value;  // j & 1, compile-time: LDS addresses as immediates
     tile_store(cur.k, Ks[buf], tid);
     tile_store(cur.v, Vs[buf], tid);
     if constexpr (AHEAD == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -905,7 +931,7 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
     bf16x8 ring[RING];
     f32x16 s[2], dp[2];
     bf16x8 db[2][2];
-    auto issue = [&](auto oc) {
+    auto issue = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value, t = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       if constexpr (k < NA) {
         ring[o % RING] = row_frag<D>((k & 1) ? Vb : Kb, t * 32 + r32, k >> 1, hh);
@@ -915,7 +941,7 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
       }
     };
     // softmax of tile t, part j (elements [j E, (j + 1) E)): dS^T = exp2(c S'^T) dP'^T and its bf16 pairs
-    auto sm_part = [&](auto tc, auto jc, auto ec) {
+    auto sm_part = [&](auto tc, auto jc, auto ec) __attribute__((always_inline)) {
       constexpr int t = decltype(tc)::value, j = decltype(jc)::value, E = decltype(ec)::value;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -930,7 +956,7 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
         }
       }
     };
-    auto compute = [&](auto oc) {
+    auto compute = [&](auto oc) __attribute__((always_inline)) {
       constexpr int o = decltype(oc)::value, t = ilv_qt<IL, NA, NC>(o), k = ilv_k<IL, NA, NC>(o);
       const bf16x8& f = ring[o % RING];
       if constexpr (k < NA) {
@@ -971,11 +997,14 @@ __global__ void __launch_bounds__(NW * 64, DqCfg<D>::kWavesPerSimd) attn_bwd_dq_
   };
   if constexpr (AHEAD == 2) {
     for (int j = 0; j < nblk; j += 2) {
-      block_it(j, sA);
-      if (j + 1 < nblk) block_it(j + 1, sB);
+      block_it(j, sA, std::integral_constant<int, 0>{});
+      if (j + 1 < nblk) block_it(j + 1, sB, std::integral_constant<int, 1>{});
     }
   } else {
-    for (int j = 0; j < nblk; ++j) block_it(j, sA);
+    for (int j = 0; j < nblk; j += 2) {
+      block_it(j, sA, std::integral_constant<int, 0>{});
+      if (j + 1 < nblk) block_it(j + 1, sA, std::integral_constant<int, 1>{});
+    }
   }
   if (qrow < a.S) {
     bf16* dqr = static_cast<bf16*>(a.dq) + (int64_t)b * a.dq_sb + (int64_t)qrow * a.dq_ss + (int64_t)h * D;
@@ -1029,17 +1058,21 @@ static hipError_t fwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
   return hipGetLastError();
 }
 
-// the backward kernels' interleaved softmax (ILV) by default; DTA_ATTN_BWD_ILV=0: the round-4 op order (A/B)
-static bool bwd_ilv() {
+// the backward kernels' interleaved softmax (ILV): the default at D = 128 (Llama-3 shape backward 1916-1954
+// -> 1898-1944 us), not at D = 64 (GPT-2 shape 72.9 -> 76.4 us: its kernels have the registers and waves to
+// hide the softmax already; profiles/attn_diag_r5e.jsonl).  DTA_ATTN_BWD_ILV=0 / 1 forces either (A/B).
+static bool bwd_ilv(int D) {
   const char* e = getenv("DTA_ATTN_BWD_ILV");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return D == 128;
 }
 
 template <int D, int NW>
 static void dq_launch(const AttnArgs& a, bool causal, hipStream_t st) {
   const int nqb = (a.S + NW * 32 - 1) / (NW * 32);
   dim3 grid((unsigned)(nqb * a.B * a.H));
-  if (bwd_ilv()) {
+  if (bwd_ilv(D)) {
     if (causal) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true, NW, true>), grid, dim3(NW * 64), 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false, NW, true>), grid, dim3(NW * 64), 0, st, a);
   } else {
@@ -1059,7 +1092,7 @@ static hipError_t bwd_d(const AttnArgs& a, bool causal, hipStream_t st) {
     dq_launch<D, 4>(a, causal, st);
   }
   dim3 gkv((unsigned)(((a.S + 127) / 128) * a.B * a.Hkv));
-  if (bwd_ilv()) {
+  if (bwd_ilv(D)) {
     if (causal) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, true, true>), gkv, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, false, true>), gkv, dim3(256), 0, st, a);
   } else {

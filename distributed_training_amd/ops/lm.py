@@ -1112,11 +1112,87 @@ class _LinearCrossEntropy(Function):
         return dx, dw, None, None
 
 
-def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
-    """Mean token cross-entropy of ``x @ w.T`` against ``target`` (the LM head + loss)."""
+class _ChunkedLinearCrossEntropy(Function):
+    """The LM head + CE in row blocks of ``chunk`` tokens, with both gradients formed in the
+    FORWARD: per block, the head GEMM writes the block's logits into one reused [chunk, V]
+    buffer, the CE kernel turns them into the (unscaled) logit gradient in place, and the
+    input-gradient GEMM (rows of dX) and the weight-gradient GEMM (accumulated over the
+    blocks, hipBLASLt beta = 1 after the first) consume it before the next block overwrites
+    it.  No [T, V] tensor exists at any time: peak memory drops by (T - chunk) x V x 2 B
+    (the head's weight gradient, which backward needs anyway, exists from the forward on).
+    Backward only scales: dX and dW by grad / count (device scalars, no host sync), dW
+    written straight into the engine's gradient slice when it may be (:func:`_grad_dest`).
+    Same GEMM count as :class:`_LinearCrossEntropy`; what it costs is the block GEMMs'
+    efficiency (narrower input-gradient outputs, a bf16 read-modify-write of dW per block).
+    Reference: the loss of ``/root/reference/src/distributed_trainer.py:163`` (F.cross_entropy)."""
+
+    @staticmethod
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int,
+                chunk: int) -> torch.Tensor:
+        x2 = x.reshape(-1, x.shape[-1])
+        T, V = x2.shape[0], w.shape[0]
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        count = (target != ignore_index).sum().clamp_min(1).float()
+        loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
+        buf = torch.empty(min(chunk, T), V, dtype=x.dtype, device=x.device)
+        dx = torch.empty_like(x2) if need_dx else None
+        dw = torch.empty_like(w) if need_dw else None
+        C = native()
+        for i, r0 in enumerate(range(0, T, chunk)):
+            r1 = min(T, r0 + chunk)
+            lg = buf[:r1 - r0]
+            xc = x2[r0:r1]
+            gemm(xc, w, kind="head_fwd", out=lg)
+            loss_rows[r0:r1] = C.cross_entropy_fwd_bwd(lg, lg, target[r0:r1], 1.0, ignore_index, -1)
+            if need_dx:
+                gemm(lg, w, False, True, kind="head_dgrad", out=dx[r0:r1])
+            if need_dw:
+                if i == 0:
+                    gemm(lg, xc, True, True, kind="head_wgrad", out=dw)
+                else:
+                    dw.addmm_(lg.t(), xc)
+        del buf
+        ctx.count = count
+        ctx.dx, ctx.dw = dx, dw  # (this op's own results, not inputs or outputs: plain attributes)
+        ctx.xshape = x.shape
+        ctx.wparam = w
+        return loss_rows.sum() / count
+
+    @staticmethod
+    def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
+        s = (g.float() / ctx.count).reshape(())
+        dx, dw = ctx.dx, ctx.dw
+        ctx.dx = ctx.dw = None
+        if dx is not None:
+            dx = dx.mul_(s).view(ctx.xshape)
+        if dw is not None:
+            dest = _grad_dest(ctx.wparam)
+            dw = torch.mul(dw, s, out=dest) if dest is not None else dw.mul_(s)
+        return dx, dw, None, None, None
+
+
+HEAD_CE_CHUNK = int(os.environ.get("DTA_HEAD_CE_CHUNK", "0"))
+
+
+def set_head_ce_chunk(rows: int) -> None:
+    """Row-block size of the LM head + CE (:class:`_ChunkedLinearCrossEntropy`); 0 = one block
+    holding the whole [T, V] logits (:class:`_LinearCrossEntropy`).  ``train.head_ce_chunk``."""
+    global HEAD_CE_CHUNK
+    HEAD_CE_CHUNK = max(0, int(rows))
+
+
+def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                         chunk: Optional[int] = None) -> torch.Tensor:
+    """Mean token cross-entropy of ``x @ w.T`` against ``target`` (the LM head + loss).  ``chunk``
+    (default :data:`HEAD_CE_CHUNK`): row blocks that never hold the [T, V] logits, see
+    :class:`_ChunkedLinearCrossEntropy`."""
     if x.is_cuda:
         _need_bf16(x, w)
-        return _LinearCrossEntropy.apply(x, w, target.reshape(-1).contiguous(), ignore_index)
+        chunk = HEAD_CE_CHUNK if chunk is None else chunk
+        t = target.reshape(-1).contiguous()
+        if chunk and chunk % 8 == 0 and t.numel() > chunk:
+            return _ChunkedLinearCrossEntropy.apply(x, w, t, ignore_index, int(chunk))
+        return _LinearCrossEntropy.apply(x, w, t, ignore_index)
     logits = F.linear(x, w).reshape(-1, w.shape[0])
     return F.cross_entropy(logits.float(), target.reshape(-1), ignore_index=ignore_index)
 

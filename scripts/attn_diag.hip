@@ -71,8 +71,8 @@ int main(int argc, char** argv) {
     std::sort(tf.begin(), tf.end());
     std::sort(tb.begin(), tb.end());
     const double fl = 2.0 * sh.B * sh.H * (double)sh.S * sh.S * sh.D;
-    printf("{\"tag\": \"%s\", \"shape\": \"%s\", \"dkdv_pf\": %d, \"fwd_us\": %.1f, \"bwd_us\": %.1f, \"fwd_tf\": %.0f, "
-           "\"bwd_tf\": %.0f}\n", tag, sh.name, DTA_DKDV_PF, tf[3], tb[3], fl / tf[3] * 1e-6, 2.5 * fl / tb[3] * 1e-6);
+    printf("{\"tag\": \"%s\", \"shape\": \"%s\", \"dkdv_pf\": %d, \"rescale_branch\": %d, \"fwd_us\": %.1f, \"bwd_us\": %.1f, \"fwd_tf\": %.0f, "
+           "\"bwd_tf\": %.0f}\n", tag, sh.name, DTA_DKDV_PF, DTA_FWD_RESCALE_BRANCH, tf[3], tb[3], fl / tf[3] * 1e-6, 2.5 * fl / tb[3] * 1e-6);
     fflush(stdout);
     hipFree(q); hipFree(k); hipFree(v); hipFree(o); hipFree(dout); hipFree(dq); hipFree(dk); hipFree(dv);
     hipFree(lse); hipFree(delta);

@@ -24,7 +24,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("bwd_ilv", ["1", "0"])
 def test_flash_attention_fwd_bwd(B, S, H, Hkv, D, causal, fwd_waves, bwd_ilv, monkeypatch):
     monkeypatch.setenv("DTA_ATTN_FWD_WAVES", fwd_waves)  # both forward workgroup shapes
-    monkeypatch.setenv("DTA_ATTN_BWD_ILV", bwd_ilv)  # backward softmax interleaved with the MFMAs (default) or not
+    monkeypatch.setenv("DTA_ATTN_BWD_ILV", bwd_ilv)  # backward softmax interleaved with the MFMAs (D 128 default) or not
     torch.manual_seed(0)
     q = torch.randn(B, S, H, D, device=DEV).bfloat16().requires_grad_()
     k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16().requires_grad_()
@@ -294,21 +294,47 @@ def test_linear_native_bias_grad():
     assert _rel(w.grad, wf.grad) < 1e-2 and _rel(x.grad, xf.grad) < 1e-2
 
 
+@pytest.mark.parametrize("chunk", [0, 128])
 @pytest.mark.parametrize("V", [50304, 1000])
-def test_linear_cross_entropy_fused_head(V):
+def test_linear_cross_entropy_fused_head(V, chunk):
+    """The head + CE against fp32 autograd: one block (the [T, V] logits) and row blocks of 128
+    tokens (chunk=128: blocks of 128, 128 and 1 rows; both gradients formed in the forward)."""
     torch.manual_seed(6)
     N, C = 257, 256
     x = (0.5 * torch.randn(N, C, device=DEV)).bfloat16().requires_grad_()
     w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
     t = torch.randint(0, V, (N,), device=DEV)
     t[::7] = -100
-    loss = lm.linear_cross_entropy(x, w, t)
+    loss = lm.linear_cross_entropy(x, w, t, chunk=chunk)
     (loss * 3.0).backward()
     xf, wf = (z.detach().float().requires_grad_() for z in (x, w))
     lr = F.cross_entropy(xf @ wf.t(), t, ignore_index=-100)
     (lr * 3.0).backward()
     assert abs(loss.item() - lr.item()) < 2e-2 * abs(lr.item())
     assert _rel(x.grad, xf.grad) < 3e-2 and _rel(w.grad, wf.grad) < 3e-2
+
+
+def test_chunked_head_ce_peak_memory():
+    """Row blocks never hold the [T, V] logits: the op's peak allocation falls by about
+    (T - chunk) x V x 2 B against the one-block form."""
+    torch.manual_seed(8)
+    T, C, V, chunk = 4096, 512, 50304, 1024
+    x = (0.5 * torch.randn(T, C, device=DEV)).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (T,), device=DEV)
+    peaks, grads = [], []
+    for ch in (0, chunk):
+        x.grad = w.grad = None
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        lm.linear_cross_entropy(x, w, t, chunk=ch).backward()
+        torch.cuda.synchronize()
+        peaks.append(torch.cuda.max_memory_allocated() - base)
+        grads.append((x.grad.float(), w.grad.float()))
+    saved = peaks[0] - peaks[1]
+    assert saved > 0.8 * (T - chunk) * V * 2, (peaks, saved)
+    assert _rel(grads[1][0], grads[0][0]) < 1e-2 and _rel(grads[1][1], grads[0][1]) < 1e-2
 
 
 def test_linear_cross_entropy_scale_in_epilogue(monkeypatch):
@@ -332,12 +358,16 @@ def test_linear_cross_entropy_scale_in_epilogue(monkeypatch):
     assert _rel(x.grad, xf.grad) < 3e-2 and _rel(w.grad, wf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("head_chunk", [0, 64])
 @pytest.mark.parametrize("arch", ["gpt2", "llama"])
-def test_fused_model_matches_fp32_reference(arch):
+def test_fused_model_matches_fp32_reference(arch, head_chunk, monkeypatch):
     """The whole fused GPU model (packed attention, fused residual norms, native
-    bias grads, fused head+CE) against the same weights run through the
+    bias grads, fused head+CE -- one block or row blocks of 64 tokens, GPT-2's tied
+    head/embedding gradient summed) against the same weights run through the
     unfused CPU fp32 path."""
     import copy
+
+    monkeypatch.setattr(lm, "HEAD_CE_CHUNK", head_chunk)
 
     from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
     from distributed_training_amd.models.llama import Llama, LlamaConfig
