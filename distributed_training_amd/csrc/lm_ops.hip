@@ -25,6 +25,21 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16* __restrict__ 
   const bf16* xr = x + row * C;
   float v[NV][8];
   float s = 0.f;
+  // gamma / beta requested with the row (not after the two reductions): each wave handles one row of
+  // the single round of rows, so a load issued late is a whole extra L2 round trip on its chain
+  // (NV <= 4, GPT-2 sized rows: Llama-3 rows (NV 8) already stream at ~5.3 TB/s, and the hoisted vectors
+  // would cost them occupancy)
+  constexpr bool HOIST = NV <= 4;
+  bf16x8 wraw[NV], braw[NV];
+  auto load_wb = [&](int i) {
+    const int c = min((i * 64 + lane) * 8, C - 8);
+    wraw[i] = *reinterpret_cast<const bf16x8*>(w + c);
+    if (!RMS) braw[i] = *reinterpret_cast<const bf16x8*>(bias + c);
+  };
+  if constexpr (HOIST) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) load_wb(i);
+  }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 8;
@@ -71,11 +86,10 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16* __restrict__ 
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 8;
     if (c < C) {
-      float wv[8], bv[8], o[8];
-      load8(w + c, wv);
-      if (!RMS) load8(bias + c, bv);
+      if constexpr (!HOIST) load_wb(i);
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * wv[j] + (RMS ? 0.f : bv[j]);
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * bf2f(wraw[i][j]) + (RMS ? 0.f : bf2f(braw[i][j]));
       store8(yr + c, o);
     }
   }
