@@ -218,16 +218,19 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
   TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm64: dims too large");
   TORCH_CHECK(dta_gemm_k64_tile((int)M, (int)N, (int)K, (int)tile) != 0,
               "gemm64: shape not covered (M, N multiples of the tile, K a multiple of 64)");
-  TORCH_CHECK(epi == 0 || epi == 2 || epi == 16 || epi == 32, "gemm64: epi 0, 2 (gelu), 16 (x gelu'(res)), 32 (+res)");
+  TORCH_CHECK(epi == 0 || epi == 2 || epi == 16 || epi == 32 || epi == 64,
+              "gemm64: epi 0, 2 (gelu), 16 (x gelu'(res)), 32 (+res), 64 (SwiGLU backward)");
+  const bool swg = epi == 64;  // res = [a | b] rows and out = [da | db] rows: both [M, 2N]
+  TORCH_CHECK(!swg || (!(bias && bias->defined()) && !(out2 && out2->defined())), "gemm64: epi 64 takes no bias / out2");
   TORCH_CHECK(!out_f32 || epi == 0, "gemm64: fp32 output without epilogue only");
   const bool two = out2 && out2->defined();
   TORCH_CHECK(!two || epi == 2, "gemm64: out2 (dual store) with the GELU epilogue only");
   torch::Tensor c, c2;
   if (out && out->defined()) {
     c = *out;
-    check_out2d(c, M, N, out_f32 ? torch::kFloat32 : torch::kBFloat16, "gemm64 out");
+    check_out2d(c, M, swg ? 2 * N : N, out_f32 ? torch::kFloat32 : torch::kBFloat16, "gemm64 out");
   } else {
-    c = torch::empty({M, N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
+    c = torch::empty({M, swg ? 2 * N : N}, a.options().dtype(out_f32 ? torch::kFloat32 : torch::kBFloat16));
   }
   if (two) {
     c2 = *out2;
@@ -242,10 +245,10 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
   }
   const void* rp = nullptr;
   int64_t ldr = 0;
-  TORCH_CHECK((epi == 16 || epi == 32) == (res && res->defined()), "gemm64: res exactly with epi 16 / 32");
+  TORCH_CHECK((epi == 16 || epi == 32 || swg) == (res && res->defined()), "gemm64: res exactly with epi 16 / 32 / 64");
   if (res && res->defined()) {
     TORCH_CHECK(res->is_cuda() && res->scalar_type() == torch::kBFloat16 && res->dim() == 2 && res->size(0) == M &&
-                    res->size(1) == N && res->stride(1) == 1 && res->stride(0) % 4 == 0 &&
+                    res->size(1) == (swg ? 2 * N : N) && res->stride(1) == 1 && res->stride(0) % 4 == 0 &&
                     reinterpret_cast<uintptr_t>(res->data_ptr()) % 8 == 0,
                 "gemm64: res bf16 [M, N]");
     rp = res->data_ptr();

@@ -11,7 +11,10 @@ namespace k64 {
 constexpr int BK = 64;
 constexpr int kGroupM = 8;
 
-enum Epi : int { EPI_NONE = 0, EPI_GELU = 2, EPI_DGELU = 16, EPI_RES = 32 };
+// EPI_DSWIGLU (the input gradient of silu(a) * b through the down projection, Llama's SwiGLU MLP): the
+// product is g = d(silu(a) b); res holds the rows [a | b] and c receives [da | db], both 2N wide (N = the
+// GEMM's N = the MLP's hidden width): da = g b s (1 + a (1 - s)), db = g a s, s = sigmoid(a)
+enum Epi : int { EPI_NONE = 0, EPI_GELU = 2, EPI_DGELU = 16, EPI_RES = 32, EPI_DSWIGLU = 64 };
 
 struct Args {
   const bf16* a;
@@ -20,7 +23,7 @@ struct Args {
   bf16* c2;         // EPI_GELU: the activation gelu(c) (nullptr: c holds the activation)
   float* c32;       // fp32 output instead of c (EPI_NONE only)
   const bf16* bias; // [N] or nullptr
-  const bf16* res;  // EPI_DGELU: the GELU input; EPI_RES: added after rounding
+  const bf16* res;  // EPI_DGELU: the GELU input; EPI_RES: added after rounding; EPI_DSWIGLU: [a | b] rows
   int64_t lda, ldb, ldc, ldc2, ldr;
   int M, N, K;
   int tiles_m, tiles_n;

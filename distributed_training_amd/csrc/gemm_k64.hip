@@ -148,8 +148,11 @@ struct Cfg {
 // store per lane per fragment (16 rows x 32 B per instruction).  Measured (scripts/bench_w4.py, 256 x 256):
 // Llama o-proj forward 204.6 -> 188.6 us, LM head forward 6110 -> 5806 us (hipBLASLt 5830), GPT-2 qkv forward
 // 59.2 -> 44.8 us.
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false>
+// DSW: the EPI_DSWIGLU instantiation (a compile-time form: its two-round epilogue in the shared body cost
+// every other kernel registers -- 256 VGPRs and scratch spills at the 256 x 256 tile)
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false, bool DSW = false>
 __device__ __forceinline__ void k64_body(const Args& g, const int t) {
+  static_assert(!DSW || STG, "the SwiGLU-backward epilogue is LDS-staged only");
   static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
   static_assert(!STG || BM * BN * 2 <= 2 * Cfg<BM, BN, WC, AT, BT>::BUF, "staged epilogue: the tile image fits the LDS");
   using C = Cfg<BM, BN, WC, AT, BT>;
@@ -466,6 +469,77 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     // computes gelu(h) from each row chunk as it leaves (one pass: through the LDS twice it measured 76.8 vs
     // 69.2 us per fragment, scripts/bench_fused_epi.py).
     constexpr int RB = 2 * BN, CPR = BN / 8, RPI = 64 / CPR;  // row bytes, chunks per row, rows per store
+    if constexpr (DSW) {
+      // Two rounds through the tile image (it holds one bf16 tile): the a tile comes in with whole-row loads,
+      // each lane turns its four values into db = g a s (in place) and keeps t = g s (1 + a (1 - s)) in its
+      // accumulators; the db rows leave; then the b tile comes in and leaves as da = t b.  (The unfused path:
+      // the product g stored, read back by swiglu_bwd_kernel with a and b, da / db written -- one [M, N] write
+      // and read fewer here, and g is not rounded to bf16 first.)
+      auto stage = [&](const bf16* src) {
+#pragma unroll
+        for (int r = 0; r < BM / (RPI * NW); ++r) {
+          const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (int64_t)(m0 + row) * g.ldr + n0 + 8 * c);
+          *reinterpret_cast<bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR))) = v;
+          if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // (4 rows in flight: the t values stay live)
+        }
+        lgkm0();
+        bar();
+      };
+      auto drain = [&](bf16* dst) {
+        lgkm0();
+        bar();
+#pragma unroll
+        for (int r = 0; r < BM / (RPI * NW); ++r) {
+          const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+          *reinterpret_cast<bf16x8*>(dst + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) =
+              *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
+          if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      auto frag_px = [&](int i, int j) {
+        const int nh = i / NTH, ii = i % NTH, mh = j / MTH, jj = j % MTH;
+        const int nl = nh * HB + wc * (HB / WC) + 16 * ii + 4 * (lane >> 4);
+        const int ml = mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
+        return reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ (ml % CPR)) + 8 * ((nl >> 2) & 1));
+      };
+      const float al = alpha_of(g);
+      bar();  // every wave's last fragment reads and DMA are done: the LDS is free
+      stage(g.res);
+#pragma unroll
+      for (int i = 0; i < 2 * NTH; ++i)
+#pragma unroll
+        for (int j = 0; j < 2 * MTH; ++j) {
+          bf16x4* px = frag_px(i, j);
+          const bf16x4 a4 = *px;
+          float db[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gv = acc[i][j][r] * al, a = bf2f(a4[r]);
+            const float sg = 1.f / (1.f + __expf(-a));
+            db[r] = gv * a * sg;
+            acc[i][j][r] = gv * sg * (1.f + a * (1.f - sg));
+          }
+          *px = pk4_bf16(db[0], db[1], db[2], db[3]);
+          __builtin_amdgcn_sched_barrier(0);  // one fragment at a time (hoisting every read costs registers)
+        }
+      drain(g.c + g.N);
+      lgkm0();
+      bar();  // every wave's image reads are done before the b tile overwrites it
+      stage(g.res + g.N);
+#pragma unroll
+      for (int i = 0; i < 2 * NTH; ++i)
+#pragma unroll
+        for (int j = 0; j < 2 * MTH; ++j) {
+          bf16x4* px = frag_px(i, j);
+          const bf16x4 b4 = *px;
+          *px = pk4_bf16(acc[i][j][0] * bf2f(b4[0]), acc[i][j][1] * bf2f(b4[1]), acc[i][j][2] * bf2f(b4[2]),
+                         acc[i][j][3] * bf2f(b4[3]));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      drain(g.c);
+      return;
+    }
     const bool has_res = g.epi == EPI_DGELU || g.epi == EPI_RES;
     const bool dual = g.epi == EPI_GELU && g.c2 != nullptr;
     bar();  // every wave's last fragment reads and DMA are done: the LDS is free
@@ -532,9 +606,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 }
 
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false>
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false, bool DSW = false>
 __global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
-  k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+  k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
 // Grouped weight gradients (on this kernel's 64-deep
@@ -553,6 +627,15 @@ __global__ void __launch_bounds__(512) gemm_k64_group_kernel(GroupArgs ga) {
 // stg: the staged epilogue (buffer DMA, one bf16 output)
 template <int BM, int BN, int WC, bool AT, bool BT, bool BUF>
 static hipError_t launch(const Args& g, int ph, bool stg, hipStream_t st) {
+  if constexpr (BUF && !AT && BT) {  // EPI_DSWIGLU: the input-gradient layout, buffer DMA, staged, two-phase
+    if (g.epi == EPI_DSWIGLU) {
+      if (!stg || ph != 2) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_k64_kernel<BM, BN, WC, AT, BT, 2, BUF, true, true>), dim3(g.tiles_m * g.tiles_n),
+                         dim3(128 * WC), 0, st, g);
+      return hipGetLastError();
+    }
+  }
+  if (g.epi == EPI_DSWIGLU) return hipErrorInvalidValue;
   if constexpr (BUF) {
     if (stg) {
       if (ph == 2)
@@ -649,14 +732,17 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
 unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k64_stamps.hip)
 #endif
 
-// epi: 0 none, 2 GELU (c2 != nullptr: c = pre-activation, c2 = gelu), 16 x gelu'(res), 32 + res
+// epi: 0 none, 2 GELU (c2 != nullptr: c = pre-activation, c2 = gelu), 16 x gelu'(res), 32 + res,
+// 64 SwiGLU backward (res = [a | b] rows, c = [da | db] rows, both 2N wide; no bias / c2 / c32)
 hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
                         int64_t ldc, void* c2, int64_t ldc2, float* c32, int M, int N, int K, float alpha,
                         const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st,
                         const float* alpha_dev) {
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
+  if (epi == k64::EPI_DSWIGLU && (bias || c32 || !res || c2)) return hipErrorInvalidValue;
   if (tile == k64::kW4 || tile == k64::kW4S) {
+    if (epi == k64::EPI_DSWIGLU) return hipErrorInvalidValue;  // (the 64-deep tiles only)
     // buffer-descriptor DMA with 32-bit offsets: every operand byte within 2 GiB of its base; a transposed
     // operand's extent a multiple of 8 (its DMA chunks are clamped whole)
     const int64_t a_bytes = 2 * (a_t ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
@@ -691,7 +777,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   // staged: whole 16-B row chunks of c (and c2, res): 8-element row strides, 16-byte aligned bases
   auto rows16 = [](const void* p, int64_t ld) { return p == nullptr || (ld % 8 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0); };
   const bool stg = (tile & k64::kNoStg) == 0 && c32 == nullptr && rows16(c, ldc) && rows16(c2, ldc2) &&
-                   ((epi != k64::EPI_DGELU && epi != k64::EPI_RES) || rows16(res, ldr));
+                   ((epi != k64::EPI_DGELU && epi != k64::EPI_RES && epi != k64::EPI_DSWIGLU) || rows16(res, ldr));
   tile &= ~(k64::kBufDma | k64::kFlatDma | k64::kNoStg);
   if (buf) {  // 32-bit offsets: every byte of A and B within 2 GiB of its base (descriptor range)
     const int64_t a_bytes = 2 * (a_t ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);

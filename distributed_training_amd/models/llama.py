@@ -79,7 +79,8 @@ class FeedForward(nn.Module):
         self.w2 = lm.Linear(cfg.ffn_hidden, cfg.n_embd, bias=False)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.w2(lm.swiglu(self.w13(x)))
+        # w2(swiglu(.)) as one op: its input gradient carries the SwiGLU backward in the GEMM epilogue
+        return lm.swiglu_linear(self.w13(x), self.w2.weight)
 
 
 class Block(nn.Module):

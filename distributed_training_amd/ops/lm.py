@@ -779,6 +779,78 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     return run_torch()
 
 
+_DSW_TILES = (5, 6, 7, 8)  # the two-phase 64-deep tiles: the SwiGLU-backward epilogue's instantiations
+
+
+def _swiglu_dgrad(dy2: torch.Tensor, w: torch.Tensor, ab2: torch.Tensor) -> torch.Tensor:
+    """d[a | b] of ``silu(a) * b`` through ``y = (silu(a) b) W^T``: on a hand-written GEMM whose epilogue
+    reads the [a | b] rows and writes [da | db] (``csrc/gemm_k64.hip`` EPI_DSWIGLU: no [tokens, F] round
+    trip of the product through HBM), or hipBLASLt followed by the SwiGLU-backward kernel, whichever is
+    faster for the shape (the tracked table / per-shape timing, kind ``dswiglu``)."""
+    M, K = dy2.shape
+    N = w.shape[1]
+    C = native()
+    ok = (w.is_contiguous() and w.data_ptr() % 16 == 0 and dy2.data_ptr() % 16 == 0 and ab2.is_contiguous()
+          and ab2.data_ptr() % 16 == 0 and ab2.shape[1] == 2 * N and N % 8 == 0)
+
+    def run(impl: int) -> torch.Tensor:
+        return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 64, ab2, impl - K64)[0]
+
+    def run_torch() -> torch.Tensor:
+        return C.swiglu_bwd(torch.mm(dy2, w), ab2, -1)
+
+    impl = 0
+    if ok:
+        cands: Dict[int, Callable[[], object]] = {0: run_torch}
+        for t in _DSW_TILES:
+            if C.gemm64_tile(M, N, K, t):
+                cands[K64 + t] = (lambda t=t: run(K64 + t))
+        impl = _pick("dswiglu", M, N, K, cands)
+    if impl:
+        GEMM_STATS["dta"] += 1
+        return run(impl)
+    GEMM_STATS["torch"] += 1
+    return run_torch()
+
+
+class _SwigluLinear(Function):
+    """y = (silu(a) * b) W^T for ab = [a | b] (Llama's SwiGLU MLP down projection with its activation).
+    Backward: dW from the weight-gradient path of :class:`_Linear` (the activation saved in forward),
+    d[a | b] through :func:`_swiglu_dgrad` (the SwiGLU backward folded into the input-gradient GEMM)."""
+
+    @staticmethod
+    def forward(ctx: Any, ab: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        abc = ab.contiguous()
+        act = native().swiglu_fwd(abc, -1)
+        ctx.save_for_backward(abc, act, w)
+        ctx.params = (w, None)
+        if ctx.needs_input_grad[1]:
+            _count_use(w)
+        return gemm(act.reshape(-1, act.shape[-1]), w, kind="fwd").view(*ab.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
+        ab, act, w = ctx.saved_tensors
+        pw, _ = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dab = dw = None
+        if ctx.needs_input_grad[0]:
+            dab = _swiglu_dgrad(dy2, w, ab.reshape(-1, ab.shape[-1])).view(ab.shape)
+        if ctx.needs_input_grad[1]:
+            dw = _weight_grad(dy2, act.reshape(-1, act.shape[-1]), with_bias=False, w=pw, b=None)
+        return dab, dw
+
+
+def swiglu_linear(ab: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``linear(swiglu(ab), w)`` with the SwiGLU backward fused into the input-gradient GEMM on GPU."""
+    if ab.is_cuda and ab.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 \
+            and ab.shape[-1] % 16 == 0 and w.shape[0] % 8 == 0:
+        return _SwigluLinear.apply(ab, w)
+    return linear(swiglu(ab), w)
+
+
 class _GeluLinear(Function):
     """y = gelu_tanh(h) W^T + b (the second half of a GPT-2 MLP).  Backward:
     dW / db from the weight-gradient path of :class:`_Linear`, and dh through

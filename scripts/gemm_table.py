@@ -10,6 +10,8 @@
 
     python scripts/gemm_table.py --out distributed_training_amd/ops/gemm_table_mi355x.json
     python scripts/gemm_table.py --check distributed_training_amd/ops/gemm_table_mi355x.json   # re-measure, compare
+    python scripts/gemm_table.py --only dswiglu --merge distributed_training_amd/ops/gemm_table_mi355x.json --out F
+        # measure only these kinds; the other entries copied from the --merge table
 
 ``--check`` re-measures and reports, per key, whether this box picks the same implementation and the
 hand-written / library ratio (the cross-box determinism check of verdict r4 item 1).
@@ -73,6 +75,8 @@ def probe(kind, M, N, K):
         lm.gemm_gelu_dual(_r(M, K), _r(N, K, scale=0.02), _r(N) if kind == "fwd_gelub" else None)
     elif kind == "dgelu":
         lm._dgelu_dgrad(_r(M, K), _r(K, N, scale=0.02), _r(M, N))
+    elif kind == "dswiglu":
+        lm._swiglu_dgrad(_r(M, K), _r(K, N, scale=0.02), _r(M, 2 * N, scale=2.0))
     else:
         raise ValueError(f"unknown GEMM kind {kind}")
     torch.cuda.synchronize()
@@ -103,10 +107,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     ap.add_argument("--check", default="")
+    ap.add_argument("--only", default="", help="comma-separated kinds to measure (default: every key)")
+    ap.add_argument("--merge", default="", help="table whose entries the measured ones are added to / replace")
     args = ap.parse_args()
     keys = collect_keys()
+    if args.only:
+        kinds = set(args.only.split(","))
+        keys = [k for k in keys if k[0] in kinds]
     print(f"[gemm_table] {len(keys)} keys", flush=True)
     entries = measure(keys)
+    if args.merge:
+        with open(args.merge) as f:
+            base = json.load(f)["entries"]
+        base.update(entries)
+        entries = base
     props = torch.cuda.get_device_properties(0)
     doc = {"arch": props.gcnArchName, "device": props.name, "rounds": int(os.environ["DTA_GEMM_ROUNDS"]),
            "generated": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"), "script": "scripts/gemm_table.py",

@@ -280,3 +280,33 @@ def test_gemm64_staged_fused_epilogues_bitwise(tile):
     both(lambda t: C.gemm64(x, w, epi=32, res=res_odd, tile=t))
     both(lambda t: C.gemm64(x, wn, False, True, epi=16, res=res, tile=t))
     both(lambda t: C.gemm64(x, wn, False, True, bias=bias, epi=16, res=res_odd, tile=t))
+
+
+@pytest.mark.parametrize("tile,M,N,K", [(5, 512, 512, 256), (6, 512, 384, 192), (7, 384, 256, 1088), (8, 256, 512, 64),
+                                        (5, 2048, 2048, 1024), (7, 1024, 1536, 512)])
+def test_gemm64_swiglu_backward_epilogue(tile, M, N, K):
+    """EPI_DSWIGLU (64): the product g = dy W (N-major W, the down projection's input gradient) turned
+    into [da | db] of silu(a) * b in the LDS-staged epilogue, against fp32 PyTorch on the same bf16
+    inputs; and the other tiles / the W4 tile / a bias are refused."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    gen = torch.Generator().manual_seed(tile * 7 + K)
+    dy = (0.5 * torch.randn(M, K, generator=gen)).bfloat16().cuda()
+    w = (0.05 * torch.randn(K, N, generator=gen)).bfloat16().cuda()
+    ab = (2.0 * torch.randn(M, 2 * N, generator=gen)).bfloat16().cuda()
+    got = C.gemm64(dy, w, False, True, None, None, False, 1.0, None, 64, ab, tile)[0]
+    assert got.shape == (M, 2 * N)
+    g = dy.float() @ w.float()
+    a, b = ab.float()[:, :N], ab.float()[:, N:]
+    s = torch.sigmoid(a)
+    want = torch.cat([g * b * s * (1 + a * (1 - s)), g * a * s], dim=1)
+    err = (got.float() - want).abs().max().item()
+    assert err <= 1e-2 * want.abs().max().item(), err
+    for bad in (1, 3, 10):  # four-phase / W4: not instantiated with this epilogue
+        if C.gemm64_tile(M, N, K, bad):
+            with pytest.raises(RuntimeError):
+                C.gemm64(dy, w, False, True, None, None, False, 1.0, None, 64, ab, bad)
+    with pytest.raises(RuntimeError):
+        C.gemm64(dy, w, False, True, None, None, False, 1.0, torch.zeros(N, dtype=torch.bfloat16, device="cuda"),
+                 64, ab, tile)

@@ -391,6 +391,32 @@ def test_fused_model_matches_fp32_reference(arch, head_chunk, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["dta", "torch"])
+def test_swiglu_linear_fused_backward(mode, monkeypatch):
+    """(silu(a) * b) W^T with the SwiGLU backward in the input-gradient GEMM's epilogue (DTA_GEMM=dta) or
+    hipBLASLt + the SwiGLU-backward kernel (torch) vs fp32 PyTorch autograd."""
+    import torch.nn.functional as F
+
+    monkeypatch.setenv("DTA_GEMM", mode)
+    monkeypatch.setattr(lm, "_GEMM_CHOICE", {})
+    torch.manual_seed(12)
+    F_ = 512
+    ab = torch.randn(2, 256, 2 * F_, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(384, F_, device=DEV) * 0.05).bfloat16().requires_grad_()
+    calls = dict(lm.GEMM_STATS)
+    y = lm.swiglu_linear(ab, w)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    if mode == "dta":
+        assert lm.GEMM_STATS["dta"] - calls.get("dta", 0) >= 2  # forward and the fused input gradient
+    abf, wf = (t.detach().float().requires_grad_() for t in (ab, w))
+    a, b = abf.chunk(2, dim=-1)
+    yf = F.linear(F.silu(a) * b, wf)
+    (yf * gy.float()).sum().backward()
+    assert _rel(y, yf) < 1e-2
+    assert _rel(ab.grad, abf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("mode", ["dta", "torch"])
 def test_gelu_linear_fused_backward(mode, monkeypatch):
     """gelu(h) W^T + b with the GELU backward in the input-gradient GEMM's epilogue (DTA_GEMM=dta)
     or hipBLASLt + the GELU-backward kernel (torch) vs fp32 PyTorch."""
