@@ -1190,8 +1190,10 @@ class _ChunkedLinearCrossEntropy(Function):
     buffer, the CE kernel turns them into the (unscaled) logit gradient in place, and the
     input-gradient GEMM (rows of dX) and the weight-gradient GEMM (accumulated over the
     blocks, hipBLASLt beta = 1 after the first) consume it before the next block overwrites
-    it.  No [T, V] tensor exists at any time: peak memory drops by (T - chunk) x V x 2 B
-    (the head's weight gradient, which backward needs anyway, exists from the forward on).
+    it.  No [T, V] tensor exists at any time: peak memory drops by (T - chunk) x V x 2 B where
+    the weight gradient goes straight into the engine's final gradient slice from the forward on
+    (DDP after zero_grad(set_to_none), FSDP at one rank: ``_dta_gdest_fwd``); elsewhere the op
+    holds a [V, C] buffer of its own from forward to backward.
     Backward only scales: dX and dW by grad / count (device scalars, no host sync), dW
     written straight into the engine's gradient slice when it may be (:func:`_grad_dest`).
     Same GEMM count as :class:`_LinearCrossEntropy`; what it costs is the block GEMMs'
@@ -1208,7 +1210,15 @@ class _ChunkedLinearCrossEntropy(Function):
         loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
         buf = torch.empty(min(chunk, T), V, dtype=x.dtype, device=x.device)
         dx = torch.empty_like(x2) if need_dx else None
-        dw = torch.empty_like(w) if need_dw else None
+        dw, dw_final = None, False
+        if need_dw:
+            # the weight gradient straight into the engine's gradient slice when it is final already in
+            # the forward (DDP after zero_grad(set_to_none); FSDP at one rank): no [V, C] buffer of its own
+            f = getattr(w, "_dta_gdest_fwd", None)
+            dw = f() if f is not None else (_grad_dest(w) if getattr(w, "_dta_gdest", None) is None else None)
+            dw_final = dw is not None
+            if dw is None:
+                dw = torch.empty_like(w)
         C = native()
         for i, r0 in enumerate(range(0, T, chunk)):
             r1 = min(T, r0 + chunk)
@@ -1226,6 +1236,7 @@ class _ChunkedLinearCrossEntropy(Function):
         del buf
         ctx.count = count
         ctx.dx, ctx.dw = dx, dw  # (this op's own results, not inputs or outputs: plain attributes)
+        ctx.dw_final = dw_final
         ctx.xshape = x.shape
         ctx.wparam = w
         return loss_rows.sum() / count
@@ -1238,7 +1249,7 @@ class _ChunkedLinearCrossEntropy(Function):
         if dx is not None:
             dx = dx.mul_(s).view(ctx.xshape)
         if dw is not None:
-            dest = _grad_dest(ctx.wparam)
+            dest = None if ctx.dw_final else _grad_dest(ctx.wparam)
             dw = torch.mul(dw, s, out=dest) if dest is not None else dw.mul_(s)
         return dx, dw, None, None, None
 

@@ -238,6 +238,7 @@ class _Unit:
         for e, ((mod, attr, name, _), k, shp) in enumerate(zip(self.entries, self._piece_index, self.shapes)):
             view = pieces[k].view(shp)
             view._dta_gdest = functools.partial(self.piece_dest, e)
+            view._dta_gdest_fwd = functools.partial(self.piece_dest_forward, e)
             view._dta_defer_ok = self.owner._defer_wgrad  # its weight gradient may join a grouped launch
             for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
                 setattr(m2, a2, view)
@@ -267,6 +268,23 @@ class _Unit:
             return None
         buf = self.grad_buffer()  # (first call of the backward: creates the buffer and resets the claims,
         self._claimed.add(e)      # so the claim goes in after it -- else a weight used twice got its piece twice)
+        o, n = self.offsets[e], self.numels[e]
+        return buf[o:o + n].view(self.shapes[e])
+
+    def piece_dest_forward(self, e: int) -> Optional[torch.Tensor]:
+        """:meth:`piece_dest` for an op that forms a weight gradient in its FORWARD (the row-blocked LM
+        head + CE, ops/lm.py ``_ChunkedLinearCrossEntropy``): only where the unit's gradient buffer is the
+        final flat-gradient slice (one rank, first gradient since zero_grad(set_to_none)) -- memory that
+        exists anyway, so the forward holds no extra [V, C] buffer; elsewhere None (the op keeps its own)."""
+        own = self.owner
+        if self._dest is not None or self.in_backward or own.world_size != 1 or not own._grad_fresh \
+                or self.index in own._written:
+            return None
+        fg = own.shards
+        if fg.grad_dtype != self.full.dtype or fg.grad.device != self.full.device:
+            return None
+        buf = self.grad_buffer()  # (the flat-gradient slice under the conditions above)
+        self._claimed.add(e)
         o, n = self.offsets[e], self.numels[e]
         return buf[o:o + n].view(self.shapes[e])
 

@@ -251,3 +251,51 @@ def test_graphed_step_capture_failure_agreed(local_fail):
     assert eng.resets == (1 if local_fail else 0)
     with pytest.raises(RuntimeError, match="eager"):
         g(x)
+
+
+@pytest.mark.parametrize("arch,strategy", [("gpt2", "ddp"), ("llama", "fsdp"), ("gpt2", "fsdp")])
+def test_chunked_head_ce_under_engines(arch, strategy, monkeypatch):
+    """The row-blocked LM head + CE (weight gradient formed in the forward, written straight into the
+    engine's final gradient slice: DDP's flat buffer -- GPT-2's tied embedding rows added into it in
+    place afterwards -- or the one-rank FSDP unit's flat-gradient slice) gives the same gradients and
+    loss as the one-block head under the same engine, over two steps."""
+    import copy
+
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.models.llama import Llama, LlamaConfig
+    from distributed_training_amd.ops import lm
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = _dev()
+    torch.manual_seed(3)
+    if arch == "gpt2":
+        base = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1024, block_size=128))
+    else:
+        base = Llama(LlamaConfig(n_layer=2, n_head=4, n_kv_head=2, n_embd=256, ffn_hidden=512, vocab_size=1024,
+                                 block_size=128))
+    idx = torch.randint(0, 1024, (2, 2, 129), device=dev)
+    results = []
+    for chunk in (0, 64):
+        monkeypatch.setattr(lm, "HEAD_CE_CHUNK", chunk)
+        m = copy.deepcopy(base).to(dev)
+        if strategy == "ddp":
+            w = DistributedDataParallel(m, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+        else:
+            w = FullyShardedDataParallel(m, device=dev, wrap_policy=lm_wrap_policy(m), param_dtype=torch.bfloat16)
+        losses, grads = [], []
+        for s in range(2):
+            w.zero_grad(set_to_none=True)
+            loss = w(idx[s, :, :-1], idx[s, :, 1:])
+            loss.backward()
+            torch.cuda.synchronize()
+            losses.append(loss.item())
+            grads.append([p.grad.float().clone() for p in w.parameters()])
+        results.append((losses, grads))
+    (l0, g0), (l1, g1) = results
+    for a, b in zip(l0, l1):
+        assert abs(a - b) < 1e-2 * abs(a)
+    for s in range(2):
+        for a, b in zip(g0[s], g1[s]):
+            assert ((a - b).norm() / (a.norm() + 1e-12)).item() < 2e-2
