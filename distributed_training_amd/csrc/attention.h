@@ -22,6 +22,10 @@ struct AttnArgs {
   int64_t dq_sb, dq_ss, dk_sb, dk_ss, dv_sb, dv_ss;
   int B, S, H, Hkv;
   float scale;
+  // backward only, nullptr = none: RoPE tables [S, D/2] (fp32) of the forward's rotation -- dQ / dK leave the
+  // kernels inverse-rotated (the gradient of the pre-rotation q / k), in fp32 before their rounding
+  const float* rcos;
+  const float* rsin;
 };
 
 }  // namespace dta

@@ -360,7 +360,8 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
 std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
                                     torch::Tensor o, torch::Tensor lse, bool causal, double scale, int64_t stream,
                                     c10::optional<torch::Tensor> dq_out, c10::optional<torch::Tensor> dk_out,
-                                    c10::optional<torch::Tensor> dv_out) {
+                                    c10::optional<torch::Tensor> dv_out, c10::optional<torch::Tensor> rope_cos,
+                                    c10::optional<torch::Tensor> rope_sin) {
   const int64_t B = q.size(0), S = q.size(1), H = q.size(2), D = q.size(3), Hkv = k.size(2);
   TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
   TORCH_CHECK(Hkv >= 1 && H % Hkv == 0, "attention: H must be a multiple of Hkv");
@@ -388,6 +389,16 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::
   a.dq_sb = dq.stride(0); a.dq_ss = dq.stride(1);
   a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1);
   a.B = (int)B; a.S = (int)S; a.H = (int)H; a.Hkv = (int)Hkv; a.scale = (float)scale;
+  const bool rope = rope_cos && rope_cos->defined();
+  TORCH_CHECK(rope == (rope_sin && rope_sin->defined()), "attn_bwd: rope_cos and rope_sin together");
+  if (rope) {  // dQ / dK inverse-rotated in the kernels' epilogues (the gradient of the pre-RoPE q / k)
+    for (const auto* t : {&*rope_cos, &*rope_sin})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->dim() == 2 &&
+                      t->size(0) >= S && t->size(1) == D / 2 && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "attn_bwd: RoPE tables f32 [>= S, D/2], contiguous, 16-byte aligned");
+    a.rcos = rope_cos->data_ptr<float>();
+    a.rsin = rope_sin->data_ptr<float>();
+  }
   hip_ok(dta_attn_bwd(&a, (int)D, causal, pick_stream(stream)), "attn_bwd");
   return {dq, dk, dv};
 }
@@ -1046,7 +1057,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),
-        py::arg("dk") = py::none(), py::arg("dv") = py::none());
+        py::arg("dk") = py::none(), py::arg("dv") = py::none(), py::arg("rope_cos") = py::none(),
+        py::arg("rope_sin") = py::none());
   m.def("rccl_load", &dta::rccl_load);
   m.def("rccl_loaded", &dta::rccl_loaded);
   m.def("rccl_unique_id", []() { return py::bytes(dta::rccl_unique_id()); });

@@ -119,9 +119,10 @@ class _PackedAttn(Function):
         dqkv = torch.empty_like(qkv)
         q, k, v = _split_qkv(qkv, H, Hkv)
         dq, dk, dv = _split_qkv(dqkv, H, Hkv)
-        native().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, -1, dq, dk, dv)
-        if has_rope:  # d(rope(x))/dx = inverse rotation
-            native().rope_(dqkv.view(B, S, H + 2 * Hkv, D)[:, :, :H + Hkv], cos, sin, True, -1)
+        # d(rope(x))/dx = the inverse rotation: applied to dQ / dK in the backward kernels' epilogues (in
+        # fp32, before the rounding; no separate pass over the q|k columns)
+        native().attn_bwd(do.contiguous(), q, k, v, o, lse, causal, scale, -1, dq, dk, dv,
+                          cos if has_rope else None, sin if has_rope else None)
         return dqkv, None, None, None, None, None, None, None
 
 

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 S=scripts/gpu.sh
 T=distributed_training_amd/ops/gemm_table_mi355x.json
-bash $S tests tests/test_gemm64_gpu.py tests/test_lm_ops_gpu.py tests/test_engine_gpu.py -k "swiglu or fused_model or staged or epilogues or cross_entropy or chunked" &&
+bash $S tests tests/test_gemm64_gpu.py tests/test_lm_ops_gpu.py tests/test_engine_gpu.py -k "swiglu or fused_model or staged or epilogues or cross_entropy or chunked or rope or attention" &&
 bash $S table --only dswiglu --merge $T --out gpurun_out/gemm_table_mi355x.json &&
 cp gpurun_out/gemm_table_mi355x.json $T &&
 bash $S lm llh_fused --model llama3_8b --strategy fsdp --batch 1 --seq 8192 --steps 6 --warmup 2 &&

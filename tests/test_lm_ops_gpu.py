@@ -228,7 +228,8 @@ def test_llama_tiny_fsdp_trains_on_gpu():
 
 @pytest.mark.parametrize("H,Hkv,D,rope", [(4, 4, 64, False), (4, 2, 128, True), (8, 1, 64, True)])
 def test_packed_attention_with_rope(H, Hkv, D, rope):
-    """Attention on the packed QKV projection output: packed dQKV gradient, RoPE fused."""
+    """Attention on the packed QKV projection output: packed dQKV gradient, RoPE applied in place in the
+    forward and inverted on dQ / dK inside the backward kernels' epilogues."""
     torch.manual_seed(3)
     B, S = 2, 160
     qkv = (torch.randn(B, S, (H + 2 * Hkv) * D, device=DEV) * 0.5).bfloat16().requires_grad_()
