@@ -811,6 +811,10 @@ class FullyShardedDataParallel(nn.Module):
         gradient (later backwards accumulate into it)."""
         if not set_to_none:
             self._grad_fresh = False
+        for u in self.units:  # (a forward-time claim -- piece_dest_forward -- of a step whose backward never ran)
+            if not u.in_backward:
+                u._dest = None
+                u._claimed = set()
         self.shards.zero_grad(set_to_none)
 
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
