@@ -85,7 +85,9 @@ class GraphedStep:
             with torch.cuda.graph(self.graph, stream=self.stream):
                 self.loss = step_fn(*self.static).detach()  # (as above: no graph kept alive)
         except Exception as e:  # noqa: BLE001 - reported through .ok / .error after the agreement
-            self.error = e
+            # without its traceback: the frames hold the half-captured step's loss, whose autograd graph
+            # (and AccumulateGrad nodes made on the capture stream) the eager steps would then accumulate through
+            self.error = e.with_traceback(None)
             self._abandon()
         torch.cuda.synchronize(dev)
         if not _agree_all_ok(engine, self.error is None, dev):

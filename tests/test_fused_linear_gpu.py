@@ -31,7 +31,7 @@ def _reference(model, X, T, batches, loss, sgd_kw):
             lv = F.cross_entropy(out, T[idx]) if loss == "cross_entropy" else F.mse_loss(out, T[idx])
             lv.backward()
             grads.append([p.grad.clone() for p in ref.parameters()])
-            losses.append(float(lv))
+            losses.append(float(lv.detach()))
         for p, *gs in zip(ref.parameters(), *grads):
             p.grad = sum(gs) / len(gs)
         opt.step()
