@@ -321,7 +321,10 @@ def _gfx950() -> bool:
 
 
 def gemm_table() -> Dict[tuple, int]:
-    """The tracked table as {(kind, M, N, K): impl id} ({} off gfx950 or with DTA_GEMM_TABLE=0)."""
+    """The tracked table as {(kind, M, N, K): impl id} ({} off gfx950 or with DTA_GEMM_TABLE=0).  An entry's
+    ``in_step_pick`` (with its ``in_step_evidence``: same-box step A/B runs) overrides the isolated-timing
+    ``pick`` where the two disagree -- a kernel timed back to back on warm operands can rank differently
+    inside the training step (cold operands, the step's clock)."""
     if not _TABLE_LOADED[0]:
         _TABLE_LOADED[0] = True
         if os.environ.get("DTA_GEMM_TABLE", "1") != "0" and os.path.exists(TABLE_PATH) and _gfx950():
@@ -331,7 +334,7 @@ def gemm_table() -> Dict[tuple, int]:
                 for k, v in json.load(f)["entries"].items():
                     kind, dims = k.rsplit(" ", 1)
                     M, N, K = (int(x) for x in dims.split("x"))
-                    _TABLE[(kind, M, N, K)] = int(v["pick"])
+                    _TABLE[(kind, M, N, K)] = int(v.get("in_step_pick", v["pick"]))
     return _TABLE
 
 

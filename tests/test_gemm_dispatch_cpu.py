@@ -37,6 +37,8 @@ def test_table_is_valid_and_covers_the_lm_steps():
         us = e["us"]
         if kind not in ("fwd_gelu", "fwd_gelub"):  # (the GELU dual store keeps its 15 % handicap)
             assert us[e["pick_name"]] <= min(us.values()) * 1.0001, key
+        if "in_step_pick" in e:  # an in-step override carries its evidence (same-box step A/B)
+            assert e["in_step_pick"] in valid and e.get("in_step_evidence"), key
         kinds.add(kind)
     assert {"fwd", "fwdb", "dgrad", "wgrad", "head_fwd", "head_dgrad", "head_wgrad", "dgelu",
             "fwd_gelub"} <= kinds
