@@ -804,6 +804,13 @@ class FullyShardedDataParallel(nn.Module):
     def _mark_grads_fresh(self) -> None:
         self._grad_fresh = True
         self._written = set()
+        self._drop_forward_claims()
+
+    def _drop_forward_claims(self) -> None:
+        for u in self.units:  # (a forward-time claim -- piece_dest_forward -- of a step whose backward never ran)
+            if not u.in_backward:
+                u._dest = None
+                u._claimed = set()
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         """``set_to_none`` (default): no fill pass -- the next backward writes every
@@ -811,10 +818,7 @@ class FullyShardedDataParallel(nn.Module):
         gradient (later backwards accumulate into it)."""
         if not set_to_none:
             self._grad_fresh = False
-        for u in self.units:  # (a forward-time claim -- piece_dest_forward -- of a step whose backward never ran)
-            if not u.in_backward:
-                u._dest = None
-                u._claimed = set()
+        self._drop_forward_claims()
         self.shards.zero_grad(set_to_none)
 
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
