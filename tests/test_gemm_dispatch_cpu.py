@@ -91,3 +91,18 @@ def test_forced_modes_ignore_table(monkeypatch, mode):
     c = lm._pick("fwd", 8192, 4096, 4096, cands)
     assert c == (0 if mode == "torch" else lm.K64 + 5)
     assert torch.cuda.is_available() or True
+
+
+def test_in_step_override_wins(monkeypatch, tmp_path):
+    """An entry's documented ``in_step_pick`` (same-box step A/B) replaces its isolated-timing ``pick``."""
+    _fresh(monkeypatch)
+    doc = {"arch": "gfx950", "rounds": 15, "entries": {
+        "dgrad 8192x768x3072": {"pick": lm.K64 + 7, "pick_name": "k64/t7", "us": {"k64/t7": 1.0},
+                                "in_step_pick": lm.K64 + 6, "in_step_evidence": "test"},
+        "fwd 64x64x64": {"pick": 0, "pick_name": "hipblaslt", "us": {"hipblaslt": 1.0}}}}
+    p = tmp_path / "table.json"
+    p.write_text(json.dumps(doc))
+    monkeypatch.setattr(lm, "TABLE_PATH", str(p))
+    table = lm.gemm_table()
+    assert table[("dgrad", 8192, 768, 3072)] == lm.K64 + 6
+    assert table[("fwd", 64, 64, 64)] == 0
