@@ -21,6 +21,8 @@ hipError_t dta_norm_fwd(bool, const void*, const void*, const void*, void*, floa
                         const void*, void*, hipStream_t);
 hipError_t dta_norm_bwd(bool, const void*, const void*, const void*, const float*, const float*, void*, float*, float*,
                         void*, void*, int64_t, int, int, int, const void*, hipStream_t);
+int dta_colsum_batch_max();
+hipError_t dta_colsum_batch(int, const float* const*, const int*, const int*, void* const*, hipStream_t);
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
@@ -443,9 +445,12 @@ std::vector<torch::Tensor> norm_fwd(torch::Tensor x, torch::Tensor w, c10::optio
 // dres: gradient arriving on the residual stream, added into dx in the same pass
 // dw_out / db_out (optional): write the weight / bias gradients there (e.g. the
 // parameters' slices of a flat gradient buffer) instead of fresh tensors
+// defer: the gamma / beta gradients are NOT finished here -- returns (dx, dw partials [nblk, C] fp32, db partials)
+// for colsum_batch (ops/lm.py _NORM_DEFER)
 std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
                                     torch::Tensor rstd, bool rms, int64_t stream, c10::optional<torch::Tensor> dres,
-                                    c10::optional<torch::Tensor> dw_out, c10::optional<torch::Tensor> db_out) {
+                                    c10::optional<torch::Tensor> dw_out, c10::optional<torch::Tensor> db_out,
+                                    bool defer) {
   check_bf16_2d(dy, "dy");
   check_bf16_2d(x, "x");
   check_bf16_2d(w, "weight");
@@ -478,10 +483,37 @@ std::vector<torch::Tensor> norm_bwd(torch::Tensor dy, torch::Tensor x, torch::Te
   auto db = rms ? torch::empty({0}, w.options()) : (out_ok(db_out) ? *db_out : torch::empty({C}, w.options()));
   hip_ok(dta_norm_bwd(rms, dy.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), dx.data_ptr(), dwp.data_ptr<float>(),
-                      rms ? nullptr : dbp.data_ptr<float>(), dw.data_ptr(), rms ? nullptr : db.data_ptr(), N, (int)C,
-                      rpb, 0, has_dres ? dres->data_ptr() : nullptr, pick_stream(stream)),
+                      rms ? nullptr : dbp.data_ptr<float>(), defer ? nullptr : dw.data_ptr(),
+                      (rms || defer) ? nullptr : db.data_ptr(), N, (int)C, rpb, 0,
+                      has_dres ? dres->data_ptr() : nullptr, pick_stream(stream)),
          "norm_bwd");
+  if (defer) return {dx, dwp, dbp};
   return {dx, dw, db};
+}
+
+// out_j = column sums of the fp32 partials part_j [nrows_j, C_j] (bf16 [C_j] outputs), several per launch
+void colsum_batch(std::vector<torch::Tensor> parts, std::vector<torch::Tensor> outs, int64_t stream) {
+  TORCH_CHECK(parts.size() == outs.size() && !parts.empty(), "colsum_batch: matching non-empty lists");
+  const int mx = dta_colsum_batch_max();
+  for (size_t i0 = 0; i0 < parts.size(); i0 += mx) {
+    const int n = (int)std::min<size_t>(mx, parts.size() - i0);
+    std::vector<const float*> pp(n);
+    std::vector<int> nr(n), cc(n);
+    std::vector<void*> oo(n);
+    for (int j = 0; j < n; ++j) {
+      const auto& p = parts[i0 + j];
+      const auto& o = outs[i0 + j];
+      TORCH_CHECK(p.is_cuda() && p.scalar_type() == torch::kFloat32 && p.dim() == 2 && p.is_contiguous(),
+                  "colsum_batch: partials must be contiguous fp32 [nrows, C]");
+      TORCH_CHECK(o.is_cuda() && o.scalar_type() == torch::kBFloat16 && o.is_contiguous() && o.numel() == p.size(1),
+                  "colsum_batch: outputs must be contiguous bf16 [C]");
+      pp[j] = p.data_ptr<float>();
+      nr[j] = (int)p.size(0);
+      cc[j] = (int)p.size(1);
+      oo[j] = o.data_ptr();
+    }
+    hip_ok(dta_colsum_batch(n, pp.data(), nr.data(), cc.data(), oo.data(), pick_stream(stream)), "colsum_batch");
+  }
 }
 
 
@@ -1046,7 +1078,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream") = -1, py::arg("res") = py::none());
   m.def("norm_bwd", &norm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("rms"), py::arg("stream") = -1, py::arg("dres") = py::none(), py::arg("dw_out") = py::none(),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("defer") = false);
+  m.def("colsum_batch", &colsum_batch, py::arg("parts"), py::arg("outs"), py::arg("stream") = -1);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("embedding_bwd_", &embedding_bwd_);

@@ -306,6 +306,25 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   else colsum_block(part1, nrows, C, (blockIdx.x - nb) * 32, ob1, of1);
 }
 
+// Several partial sets finished in ONE launch (the norms' deferred gamma / beta gradients, ops/lm.py
+// _NORM_DEFER): job j owns blocks [start[j], start[j + 1]), 32 columns each.  At GPT-2 size one norm's
+// colsum_kernel is 48 workgroups and ~5 us, almost all launch and latency; a step has 25 of them.
+struct ColsumJobs {
+  static constexpr int kMax = 64;
+  int n;
+  int start[kMax + 1];
+  const float* part[kMax];
+  int nrows[kMax];
+  int C[kMax];
+  bf16* out[kMax];
+};
+
+__global__ void __launch_bounds__(256) colsum_batch_kernel(ColsumJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.start[j + 1]) ++j;
+  colsum_block(jobs.part[j], jobs.nrows[j], jobs.C[j], ((int)blockIdx.x - jobs.start[j]) * 32, jobs.out[j], nullptr);
+}
+
 // Partial column sums of a bf16 [N, C] matrix (bias gradients): a workgroup
 // is 64 column lanes (8 columns each, 16-byte loads) x 4 row lanes over one
 // row split; the [nsplit, C] fp32 partials are finished by colsum_kernel.
@@ -765,8 +784,31 @@ hipError_t dta_norm_bwd(bool rms, const void* dy, const void* x, const void* w, 
   float* w32 = grads_f32 ? (float*)dw : nullptr;
   bf16* b16 = grads_f32 ? nullptr : (bf16*)db;
   float* b32 = grads_f32 ? (float*)db : nullptr;
+  if (!dw && !db) return hipSuccess;  // deferred: the caller finishes the partials (dta_colsum_batch)
   hipLaunchKernelGGL(colsum_kernel, dim3(rms ? nb : 2 * nb), dim3(256), 0, st, dw_part, db_part, nblk, C, w16, w32, b16,
                      b32);
+  return hipGetLastError();
+}
+
+int dta_colsum_batch_max() { return ColsumJobs::kMax; }
+
+// out_j[c] = sum_r part_j[r][c] for n <= kMax jobs in one launch (bf16 outputs)
+hipError_t dta_colsum_batch(int n, const float* const* part, const int* nrows, const int* C, void* const* out,
+                            hipStream_t st) {
+  if (n < 1 || n > ColsumJobs::kMax) return hipErrorInvalidValue;
+  ColsumJobs jobs{};
+  jobs.n = n;
+  int total = 0;
+  for (int j = 0; j < n; ++j) {
+    jobs.start[j] = total;
+    jobs.part[j] = part[j];
+    jobs.nrows[j] = nrows[j];
+    jobs.C[j] = C[j];
+    jobs.out[j] = static_cast<bf16*>(out[j]);
+    total += (C[j] + 31) / 32;
+  }
+  jobs.start[n] = total;
+  hipLaunchKernelGGL(colsum_batch_kernel, dim3((unsigned)total), dim3(256), 0, st, jobs);
   return hipGetLastError();
 }
 

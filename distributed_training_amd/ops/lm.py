@@ -147,6 +147,36 @@ def attention_packed(qkv: torch.Tensor, n_head: int, n_kv_head: int, causal: boo
 
 
 # ------------------------------------------------------------------ norms
+# gamma / beta gradients of the norms, deferred like the weight gradients (see _DEFER): the norm-backward
+# kernel leaves its per-workgroup partials and the column sums of every queued norm are finished by ONE
+# launch at the next flush (csrc/lm_ops.hip colsum_batch_kernel) instead of one ~5 us launch per norm
+# (25 per GPT-2 step).  Entries: (fp32 partials [nblk, C], an alias of the flat-gradient slice [C]).
+_NORM_DEFER: list = []
+
+
+def _defer_ok(p: Optional[torch.Tensor]) -> bool:
+    return p is None or getattr(p, "_dta_gdest", None) is None or bool(getattr(p, "_dta_defer_ok", False))
+
+
+def _norm_backward(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
+                   rms: bool, dres: Optional[torch.Tensor], pw: torch.Tensor, pb: Optional[torch.Tensor],
+                   need_w: bool, need_b: bool) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """dx and the gamma / beta gradients (into their flat-gradient slices when allowed); with both slices
+    available and deferral on, the gamma / beta column sums are queued for the batched flush."""
+    cw = _grad_dest(pw) if need_w else None
+    cb = _grad_dest(pb) if (not rms and need_b) else None
+    if (_group_threshold() and os.environ.get("DTA_NORM_DEFER", "1") != "0" and cw is not None
+            and (rms or not need_b or cb is not None) and _defer_ok(pw)
+            and (rms or _defer_ok(pb)) and cw.is_contiguous() and (cb is None or cb.is_contiguous())):
+        dx, dwp, dbp = native().norm_bwd(dy2, x2, w, mean, rstd, rms, -1, dres, None, None, True)
+        _NORM_DEFER.append((dwp, cw.view(-1)))  # (aliases, never the tensors returned to autograd)
+        if cb is not None:
+            _NORM_DEFER.append((dbp, cb.view(-1)))
+        _queue_end_join()
+        return dx, cw, cb
+    return tuple(native().norm_bwd(dy2, x2, w, mean, rstd, rms, -1, dres, cw, cb))
+
+
 class _Norm(Function):
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool, eps: float) -> torch.Tensor:
@@ -162,10 +192,9 @@ class _Norm(Function):
     def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
         x2, w, mean, rstd = ctx.saved_tensors
         pw, pb = ctx.params
-        dx, dw, db = native().norm_bwd(dy.reshape(x2.shape).contiguous(), x2, w.contiguous(), mean, rstd, ctx.rms,
-                                       -1, None, _grad_dest(pw) if ctx.needs_input_grad[1] else None,
-                                       _grad_dest(pb) if not ctx.rms and ctx.needs_input_grad[2] else None)
-        return dx.view(ctx.shape), dw, (None if ctx.rms else db), None, None
+        dx, dw, db = _norm_backward(dy.reshape(x2.shape).contiguous(), x2, w.contiguous(), mean, rstd, ctx.rms, None,
+                                    pw, pb, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        return dx.view(ctx.shape), (dw if ctx.needs_input_grad[1] else None), (None if ctx.rms else db), None, None
 
 
 class _AddNorm(Function):
@@ -194,11 +223,10 @@ class _AddNorm(Function):
             return g_x, g_x, None, None, None, None
         pw, pb = ctx.params
         dres = None if g_x is None else g_x.reshape(xsum.shape).contiguous()
-        dx, dw, db = native().norm_bwd(g_y.reshape(xsum.shape).contiguous(), xsum, w.contiguous(), mean, rstd,
-                                       ctx.rms, -1, dres, _grad_dest(pw) if ctx.needs_input_grad[2] else None,
-                                       _grad_dest(pb) if not ctx.rms and ctx.needs_input_grad[3] else None)
+        dx, dw, db = _norm_backward(g_y.reshape(xsum.shape).contiguous(), xsum, w.contiguous(), mean, rstd, ctx.rms,
+                                    dres, pw, pb, ctx.needs_input_grad[2], ctx.needs_input_grad[3])
         dx = dx.view(ctx.shape)
-        return dx, dx, dw, (None if ctx.rms else db), None, None
+        return dx, dx, (dw if ctx.needs_input_grad[2] else None), (None if ctx.rms else db), None, None
 
 
 def add_layer_norm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -562,6 +590,7 @@ def new_forward_generation() -> None:
     # flat-gradient slices as its own (two groups writing one destination in one launch).
     _SIDE_CB[0] = False
     _DEFER.clear()
+    _NORM_DEFER.clear()
     _DEFER_TILES[0] = 0
     _FWD_GEN[0] += 1
     _GEN_USES[0] = 0
@@ -571,6 +600,7 @@ def abandon_step() -> None:
     """A step stopped midway (a failed graph capture): drop what its backward queued."""
     _SIDE_CB[0] = False
     _DEFER.clear()
+    _NORM_DEFER.clear()
     _DEFER_TILES[0] = 0
     _GEN_USES[0] = 0
     _CLOSED_GEN[0] = _FWD_GEN[0]
@@ -641,8 +671,8 @@ FLUSH_LISTENERS: list = []
 
 
 def wgrad_pending() -> bool:
-    """Weight gradients are queued (their flat-buffer slices are not written yet)."""
-    return bool(_DEFER)
+    """Weight (or norm gamma / beta) gradients are queued (their flat-buffer slices are not written yet)."""
+    return bool(_DEFER) or bool(_NORM_DEFER)
 
 
 def _group_threshold() -> int:
@@ -651,22 +681,28 @@ def _group_threshold() -> int:
 
 
 def wgrad_flush() -> None:
-    """Launch the queued weight gradients (grouped, at most gemm64_group_max() per launch)."""
-    if not _DEFER:
+    """Launch the queued weight gradients (grouped, at most gemm64_group_max() per launch) and the queued
+    norm gamma / beta column sums (one batched launch)."""
+    if not _DEFER and not _NORM_DEFER:
         return
-    items = list(_DEFER)
-    _DEFER.clear()
-    _DEFER_TILES[0] = 0
     C = native()
-    # csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; every queued reduction is a multiple of
-    # 64 tokens, _weight_grad).  csrc/gemm_w4.hip's grouped kernel (impl 2) measured slower on every
-    # weight-gradient shape (profiles/gemm_w4_vs_k64_hipblaslt.txt) and has no bias gradients.
-    gmax = C.gemm64_group_max()
-    for i in range(0, len(items), gmax):
-        part = items[i:i + gmax]
-        C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
-                           [it[3] for it in part], -1, 1)
-    GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
+    if _DEFER:
+        items = list(_DEFER)
+        _DEFER.clear()
+        _DEFER_TILES[0] = 0
+        # csrc/gemm_k64.hip's grouped kernel (64-deep two-phase loop; every queued reduction is a multiple of
+        # 64 tokens, _weight_grad).  csrc/gemm_w4.hip's grouped kernel (impl 2) measured slower on every
+        # weight-gradient shape (profiles/gemm_w4_vs_k64_hipblaslt.txt) and has no bias gradients.
+        gmax = C.gemm64_group_max()
+        for i in range(0, len(items), gmax):
+            part = items[i:i + gmax]
+            C.gemm_wgrad_group([it[0] for it in part], [it[1] for it in part], [it[2] for it in part],
+                               [it[3] for it in part], -1, 1)
+        GEMM_STATS["group_launches"] += (len(items) + gmax - 1) // gmax
+    if _NORM_DEFER:
+        jobs = list(_NORM_DEFER)
+        _NORM_DEFER.clear()
+        C.colsum_batch([j[0] for j in jobs], [j[1] for j in jobs], -1)
     for fn in list(FLUSH_LISTENERS):
         fn()
 
