@@ -299,3 +299,37 @@ def test_chunked_head_ce_under_engines(arch, strategy, monkeypatch):
     for s in range(2):
         for a, b in zip(g0[s], g1[s]):
             assert ((a - b).norm() / (a.norm() + 1e-12)).item() < 2e-2
+
+
+@pytest.mark.parametrize("strategy", ["ddp", "fsdp"])
+def test_deferred_norm_grads_bitwise(strategy, monkeypatch):
+    """The norms' gamma / beta gradients finished by the batched column-sum launch at the flush
+    (ops/lm.py _NORM_DEFER) are bit-identical to the per-norm launch (DTA_NORM_DEFER=0), under the engine
+    whose flat-gradient slices make the deferral possible."""
+    import copy
+
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.ops import lm
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+
+    dev = _dev()
+    torch.manual_seed(4)
+    base = GPT2(GPT2Config(n_layer=2, n_head=4, n_embd=256, vocab_size=1024, block_size=128))
+    idx = torch.randint(0, 1024, (2, 129), device=dev)
+    grads = []
+    for defer in ("1", "0"):
+        monkeypatch.setenv("DTA_NORM_DEFER", defer)
+        m = copy.deepcopy(base).to(dev)
+        if strategy == "ddp":
+            w = DistributedDataParallel(m, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+        else:
+            w = FullyShardedDataParallel(m, device=dev, wrap_policy=lm_wrap_policy(m), param_dtype=torch.bfloat16)
+        w.zero_grad(set_to_none=True)
+        w(idx[:, :-1], idx[:, 1:]).backward()
+        torch.cuda.synchronize()
+        assert not lm._NORM_DEFER  # flushed by the end of the backward
+        grads.append([p.grad.clone() for p in w.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
