@@ -170,6 +170,7 @@ def _norm_backward(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, mean: t
             and (rms or _defer_ok(pb)) and cw.is_contiguous() and (cb is None or cb.is_contiguous())):
         dx, dwp, dbp = native().norm_bwd(dy2, x2, w, mean, rstd, rms, -1, dres, None, None, True)
         _NORM_DEFER.append((dwp, cw.view(-1)))  # (aliases, never the tensors returned to autograd)
+        GEMM_STATS["deferred_norm"] += 1
         if cb is not None:
             _NORM_DEFER.append((dbp, cb.view(-1)))
         _queue_end_join()
@@ -264,7 +265,7 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tenso
 
 # ------------------------------------------------------------------ GEMM dispatch
 _GEMM_CHOICE: Dict[tuple, int] = {}  # (kind, M, N, K) -> dta tile id (1..3) or 0 = hipBLASLt
-GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "deferred_wgrad": 0, "group_launches": 0}
+GEMM_STATS: Dict[str, int] = {"dta": 0, "torch": 0, "deferred_wgrad": 0, "group_launches": 0, "deferred_norm": 0}
 
 
 def _time_us(fns: Dict[int, Callable[[], object]], rounds: int = 5, reps: int = 4) -> Dict[int, float]:

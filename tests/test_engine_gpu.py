@@ -321,6 +321,7 @@ def test_deferred_norm_grads_bitwise(strategy, monkeypatch):
     grads = []
     for defer in ("1", "0"):
         monkeypatch.setenv("DTA_NORM_DEFER", defer)
+        n0 = lm.GEMM_STATS["deferred_norm"]
         m = copy.deepcopy(base).to(dev)
         if strategy == "ddp":
             w = DistributedDataParallel(m, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
@@ -330,6 +331,7 @@ def test_deferred_norm_grads_bitwise(strategy, monkeypatch):
         w(idx[:, :-1], idx[:, 1:]).backward()
         torch.cuda.synchronize()
         assert not lm._NORM_DEFER  # flushed by the end of the backward
+        assert (lm.GEMM_STATS["deferred_norm"] > n0) == (defer == "1")  # the deferred path did run
         grads.append([p.grad.clone() for p in w.parameters()])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
