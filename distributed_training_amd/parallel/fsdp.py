@@ -296,9 +296,10 @@ class _Unit:
         full.grad = None
         self._dest = None
         self._claimed = set()
-        if own.world_size > 1 and own._defer_wgrad and _lm().wgrad_pending():
-            # weight gradients of this unit (or an earlier one) still queued for a grouped launch
-            # (ops/lm.py _DEFER): reduce-scattered right after that launch (_launch_waiting)
+        if (own.world_size > 1 or own.rep is not None) and own._defer_wgrad and _lm().wgrad_pending():
+            # weight (or norm) gradients of this unit (or an earlier one) still queued for a grouped launch
+            # (ops/lm.py _DEFER / _NORM_DEFER): reduce-scattered -- or, one rank per shard group under HSDP,
+            # replica-all-reduced -- right after that launch (_launch_waiting)
             own._rs_waiting.append((self, g))
         else:
             self._launch_rs(g)
