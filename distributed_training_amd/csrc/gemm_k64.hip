@@ -129,19 +129,36 @@ __device__ __forceinline__ bf16x8 frag_mn(const char* img, int i0, int kk, int l
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BM, int BN, int WC, bool AT, bool BT>
+// WR x WC waves (WR = 2 but for the 192-wide tiles' 4 x 2 grid: a 96-column half over 2 wave columns)
+template <int BM, int BN, int WC, bool AT, bool BT, int WR = 2>
 struct Cfg {
-  static constexpr int NW = 2 * WC, NTHR = 64 * NW;
+  static constexpr int NW = WR * WC, NTHR = 64 * NW;
   static constexpr int HA = BM / 2, HB = BN / 2;                  // half-tile rows / columns
   static constexpr int A_HALF = HA * BK * 2, B_HALF = HB * BK * 2;  // bytes
   static constexpr int LA = A_HALF / (NTHR * 16), LB = B_HALF / (NTHR * 16);  // DMA per thread per half
+  // BJ: a B half is not a whole number of 1 KiB pieces per wave (BN 192 over 8 waves: 12 pieces): both
+  // halves go as ONE 24-piece image (they are always staged together in the two-phase loop)
+  static constexpr bool BJ = B_HALF % (NTHR * 16) != 0;
+  static constexpr int LB2 = 2 * B_HALF / (NTHR * 16);             // B pieces per thread per K-tile
   static constexpr int BUF = 2 * A_HALF + 2 * B_HALF;
-  static constexpr int MTH = HA / 32, NTH = HB / (16 * WC);       // fragments per wave per half
+  static constexpr int MTH = HA / (16 * WR), NTH = HB / (16 * WC);  // fragments per wave per half
   static constexpr int RBA = 2 * HA, RBB = 2 * HB;                 // M/N-major image row bytes
-  static_assert(LA >= 1 && LB >= 1 && MTH >= 1 && NTH >= 1, "tile too small for the workgroup");
+  static constexpr int CPR = BN / 8;                               // 16-B chunks per row of a bf16 C tile image
+  static_assert(LA >= 1 && LB2 >= 2 && MTH >= 1 && NTH >= 1, "tile too small for the workgroup");
+  static_assert(A_HALF % (NTHR * 16) == 0 && (2 * B_HALF) % (NTHR * 16) == 0, "whole DMA pieces per wave");
+  static_assert(HA % (16 * WR) == 0 && HB % (16 * WC) == 0, "whole fragments per wave");
   static_assert(!AT || RBA == 256 || RBA == 128, "M-major A: BM 256 or 128");
   static_assert(!BT || RBB == 256 || RBB == 128, "N-major B: BN 256 or 128");
+  static_assert(!BJ || !BT, "joint B staging: K-major B only");
 };
+
+// chunk swizzle of a C tile image row (CPR chunks): the row index mod CPR for the power-of-two widths, its
+// low three bits for CPR = 24 (an XOR below 8 keeps a chunk inside its group of 8: a permutation of [0, 24))
+template <int CPR>
+__device__ __forceinline__ int cswz(int row) {
+  if constexpr ((CPR & (CPR - 1)) == 0) return row % CPR;
+  else return row & 7;
+}
 
 // STG (one bf16 output): the epilogue goes through the LDS as a whole BM x BN bf16 tile image (in the LDS
 // the K loop used: the image is at most its size) and leaves as whole 2 BN-byte rows -- instead of one 8-B
@@ -150,19 +167,24 @@ struct Cfg {
 // 59.2 -> 44.8 us.
 // DSW: the EPI_DSWIGLU instantiation (a compile-time form: its two-round epilogue in the shared body cost
 // every other kernel registers -- 256 VGPRs and scratch spills at the 256 x 256 tile)
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false, bool DSW = false>
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false, bool DSW = false,
+          int WR = 2>
 __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   static_assert(!DSW || STG, "the SwiGLU-backward epilogue is LDS-staged only");
   static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
-  static_assert(!STG || BM * BN * 2 <= 2 * Cfg<BM, BN, WC, AT, BT>::BUF, "staged epilogue: the tile image fits the LDS");
-  using C = Cfg<BM, BN, WC, AT, BT>;
-  constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
-  constexpr bool STAG = WC == 4;  // two waves per SIMD: stagger the halves
+  static_assert(!STG || BM * BN * 2 <= 2 * Cfg<BM, BN, WC, AT, BT, WR>::BUF, "staged epilogue: the tile image fits the LDS");
+  using C = Cfg<BM, BN, WC, AT, BT, WR>;
+  constexpr int HA = C::HA, HB = C::HB, LA = C::LA, LB = C::LB, LB2 = C::LB2, MTH = C::MTH, NTH = C::NTH, NW = C::NW;
+  constexpr bool BJ = C::BJ;
+  static_assert(!BJ || PH == 2, "joint B staging: two-phase loop only");
+  constexpr bool STAG = NW == 8;  // two waves per SIMD: stagger the halves (waves 4-7 one barrier behind)
+  static_assert(!STAG || WC == 4 || WR == 4, "stagger groups: waves 0-3 / 4-7");
   __shared__ __attribute__((aligned(1024))) char lds[2 * C::BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WC, wc = wave % WC;
+  const bool lag = wave >= NW / 2;  // (STAG) the lagging wave group
 
   // ---- tile (t: this problem's tile index, XCD-remapped by the caller) ----
   const int per_group = kGroupM * g.tiles_n;
@@ -173,8 +195,11 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 
   // ---- per-lane DMA sources of K-tile 0 (half h: rows / columns [h * H, (h+1) * H)) ----
   // half index: 0 top, 1 bottom, 2 left, 3 right; LDS: buffer b at b * BUF, [top|bottom|left|right]
+  // B DMA groups: the two halves, or (BJ) one group of both halves' rows as one image (the halves are
+  // contiguous in the LDS and 96 rows is a multiple of the swizzle's 8, so a piece's rows need no split)
+  constexpr int NBH = BJ ? 1 : 2, LBG = BJ ? LB2 : LB;
   const bf16* srcA[2][LA];
-  const bf16* srcB[2][LB];
+  const bf16* srcB[NBH][LBG];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -189,8 +214,11 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
         srcA[h][j] = g.a + (int64_t)k * g.lda + m0 + h * HA + 8 * ch;
       }
     }
+  }
 #pragma unroll
-    for (int j = 0; j < LB; ++j) {
+  for (int h = 0; h < NBH; ++h) {
+#pragma unroll
+    for (int j = 0; j < LBG; ++j) {
       const int i = j * NW + wave;
       if constexpr (!BT) {
         const int r = 8 * i + (lane >> 3), c = (lane & 7) ^ (r & 7);
@@ -208,14 +236,17 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   // takes this form only when every operand byte lies within 4 GiB of its base
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.a), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(g.b), 0, 0x7fffffff, 0x00020000);
-  unsigned voA[2][LA], voB[2][LB];
+  unsigned voA[2][LA], voB[NBH][LBG];
   if constexpr (BUF) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
       for (int j = 0; j < LA; ++j) voA[h][j] = (unsigned)((srcA[h][j] - g.a) * 2);
+    }
 #pragma unroll
-      for (int j = 0; j < LB; ++j) voB[h][j] = (unsigned)((srcB[h][j] - g.b) * 2);
+    for (int h = 0; h < NBH; ++h) {
+#pragma unroll
+      for (int j = 0; j < LBG; ++j) voB[h][j] = (unsigned)((srcB[h][j] - g.b) * 2);
     }
   }
   const unsigned lds0 = lds_addr(lds);
@@ -244,16 +275,17 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
       for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
     }
   };
-  auto dma_b = [&](int h, int kt) {
+  auto dma_b = [&](int h, int kt) {  // (BJ: h = 0 stages both halves, h = 1 nothing)
+    if (BJ && h) return;
     const int ks = min(kt, nk - 1);
     char* dst = lds + boff(h, kt & 1);
     if constexpr (BUF) {
       const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + boff(h, kt & 1);
 #pragma unroll
-      for (int j = 0; j < LB; ++j) bglds16(rsB, voB[h][j], so, d0 + (j * NW + wave) * 1024);
+      for (int j = 0; j < LBG; ++j) bglds16(rsB, voB[BJ ? 0 : h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
 #pragma unroll
-      for (int j = 0; j < LB; ++j) glds16(srcB[h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
+      for (int j = 0; j < LBG; ++j) glds16(srcB[BJ ? 0 : h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
     }
   };
 
@@ -264,7 +296,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     for (int jj = 0; jj < MTH; ++jj)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const int r0 = wr * (HA / 2) + 16 * jj;
+        const int r0 = wr * (HA / WR) + 16 * jj;
         if constexpr (!AT) af[jj][kk] = frag_k(img, r0, kk, lane);
         else af[jj][kk] = frag_mn<C::RBA>(img, r0, kk, lane);
       }
@@ -335,7 +367,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   vm_wait<2 * LA + LB>();
   bar();
   if constexpr (STAG) {
-    if (wr == 1) bar();
+    if (lag) bar();
   }
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -387,10 +419,10 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   dma_a(0, 1);
   dma_b(0, 1);
   dma_b(1, 1);
-  vm_wait<2 * LA + 2 * LB>();
+  vm_wait<2 * LA + LB2>();
   bar();
   if constexpr (STAG) {
-    if (wr == 1) bar();
+    if (lag) bar();
   }
 #ifdef DTA_K64_STAMP
   unsigned long long seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -406,7 +438,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     dma_a(1, kt2 + 1);
     K64_STAMP(0);
     lgkm0();
-    vm_wait<2 * LA + 2 * LB>();  // bottom (t)
+    vm_wait<2 * LA + LB2>();  // bottom (t)
     K64_STAMP(1);
     bar();
     K64_STAMP(2);
@@ -422,7 +454,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     dma_b(1, kt2 + 2);
     K64_STAMP(5);
     lgkm0();
-    vm_wait<2 * LA + 2 * LB>();  // top, left, right (t+1)
+    vm_wait<2 * LA + LB2>();  // top, left, right (t+1)
     K64_STAMP(6);
     bar();
     K64_STAMP(7);
@@ -451,13 +483,13 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   }
   vm_wait<0>();  // the tail's dummy DMAs land before the workgroup's LDS is released
   if constexpr (STAG) {
-    if (wr == 0) bar();  // equal barrier counts for both halves
+    if (!lag) bar();  // equal barrier counts for both halves
   }
 
   if constexpr (CS) {
     if (do_cs && wc < MTH && (lane >> 4) == 0) {  // (the four columns of accb are equal)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) g.db[m0 + h * HA + wr * (HA / 2) + 16 * wc + lane] = f2bf(accb[h][0]);
+      for (int h = 0; h < 2; ++h) g.db[m0 + h * HA + wr * (HA / WR) + 16 * wc + lane] = f2bf(accb[h][0]);
     }
   }
   // ---- epilogue: lane holds row m, columns n .. n+3 of each (i, j) fragment ----
@@ -468,7 +500,15 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     // (GPT-2 fc2 input gradient x gelu'(h): 78.1 -> 67.8 us).  The GELU dual store stages the rounded h and
     // computes gelu(h) from each row chunk as it leaves (one pass: through the LDS twice it measured 76.8 vs
     // 69.2 us per fragment, scripts/bench_fused_epi.py).
-    constexpr int RB = 2 * BN, CPR = BN / 8, RPI = 64 / CPR;  // row bytes, chunks per row, rows per store
+    // row bytes, chunks per row; each wave moves a contiguous run of the image's chunks, 64 per instruction
+    // (whole rows for the power-of-two widths; CPR = 24 rows straddle instructions)
+    constexpr int RB = 2 * BN, CPR = C::CPR, NIT = BM * CPR / (64 * NW);
+    static_assert(BM * CPR % (64 * NW) == 0, "whole 64-chunk stores per wave");
+    auto rowc = [&](int r, int& row, int& c) __attribute__((always_inline)) {
+      const int q = wave * (BM * CPR / NW) + 64 * r + lane;
+      row = q / CPR;
+      c = q % CPR;
+    };
     if constexpr (DSW) {
       // Two rounds through the tile image (it holds one bf16 tile): the a tile comes in with whole-row loads,
       // each lane turns its four values into db = g a s (in place) and keeps t = g s (1 + a (1 - s)) in its
@@ -477,10 +517,11 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
       // and read fewer here, and g is not rounded to bf16 first.)
       auto stage = [&](const bf16* src) {
 #pragma unroll
-        for (int r = 0; r < BM / (RPI * NW); ++r) {
-          const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+        for (int r = 0; r < NIT; ++r) {
+          int row, c;
+          rowc(r, row, c);
           const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (int64_t)(m0 + row) * g.ldr + n0 + 8 * c);
-          *reinterpret_cast<bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR))) = v;
+          *reinterpret_cast<bf16x8*>(lds + row * RB + 16 * (c ^ cswz<CPR>(row))) = v;
           if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // (4 rows in flight: the t values stay live)
         }
         lgkm0();
@@ -490,18 +531,19 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
         lgkm0();
         bar();
 #pragma unroll
-        for (int r = 0; r < BM / (RPI * NW); ++r) {
-          const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+        for (int r = 0; r < NIT; ++r) {
+          int row, c;
+          rowc(r, row, c);
           *reinterpret_cast<bf16x8*>(dst + (int64_t)(m0 + row) * g.ldc + n0 + 8 * c) =
-              *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
+              *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ cswz<CPR>(row)));
           if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);
         }
       };
       auto frag_px = [&](int i, int j) {
         const int nh = i / NTH, ii = i % NTH, mh = j / MTH, jj = j % MTH;
         const int nl = nh * HB + wc * (HB / WC) + 16 * ii + 4 * (lane >> 4);
-        const int ml = mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
-        return reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ (ml % CPR)) + 8 * ((nl >> 2) & 1));
+        const int ml = mh * HA + wr * (HA / WR) + 16 * jj + (lane & 15);
+        return reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ cswz<CPR>(ml)) + 8 * ((nl >> 2) & 1));
       };
       const float al = alpha_of(g);
       bar();  // every wave's last fragment reads and DMA are done: the LDS is free
@@ -545,10 +587,11 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     bar();  // every wave's last fragment reads and DMA are done: the LDS is free
     if (has_res) {
 #pragma unroll
-      for (int r = 0; r < BM / (RPI * NW); ++r) {
-        const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
+      for (int r = 0; r < NIT; ++r) {
+        int row, c;
+        rowc(r, row, c);
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(g.res + (int64_t)(m0 + row) * g.ldr + n0 + 8 * c);
-        *reinterpret_cast<bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR))) = v;
+        *reinterpret_cast<bf16x8*>(lds + row * RB + 16 * (c ^ cswz<CPR>(row))) = v;
       }
       lgkm0();
       bar();
@@ -562,17 +605,18 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 #pragma unroll
       for (int j = 0; j < 2 * MTH; ++j) {
         const int mh = j / MTH, jj = j % MTH;
-        const int ml = mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
-        bf16x4* px = reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ (ml % CPR)) + 8 * ((nl >> 2) & 1));
+        const int ml = mh * HA + wr * (HA / WR) + 16 * jj + (lane & 15);
+        bf16x4* px = reinterpret_cast<bf16x4*>(lds + ml * RB + 16 * ((nl >> 3) ^ cswz<CPR>(ml)) + 8 * ((nl >> 2) & 1));
         *px = has_res ? val4_res(g, acc[i][j], bv, *px) : val4(g, m0 + ml, n0 + nl, acc[i][j], bv, 0);
       }
     }
     lgkm0();
     bar();
 #pragma unroll
-    for (int r = 0; r < BM / (RPI * NW); ++r) {
-      const int row = wave * (BM / NW) + RPI * r + lane / CPR, c = lane % CPR;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ (row % CPR)));
+    for (int r = 0; r < NIT; ++r) {
+      int row, c;
+      rowc(r, row, c);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * RB + 16 * (c ^ cswz<CPR>(row)));
 #if defined(DTA_K64_EPI_DIAG) && DTA_K64_EPI_DIAG == 1
       if (g.alpha == -1234.5f)  // diagnostic build (scripts/k64_epi_diag.hip): stores skipped, values live
 #endif
@@ -599,16 +643,17 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
 #pragma unroll
     for (int j = 0; j < 2 * MTH; ++j) {
       const int mh = j / MTH, jj = j % MTH;
-      const int m = m0 + mh * HA + wr * (HA / 2) + 16 * jj + (lane & 15);
+      const int m = m0 + mh * HA + wr * (HA / WR) + 16 * jj + (lane & 15);
       store4(g, m, n, acc[i][j], bv);
     }
   }
 }
 
 
-template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false, bool DSW = false>
-__global__ void __launch_bounds__(128 * WC) gemm_k64_kernel(Args g) {
-  k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false, bool DSW = false, int WR = 2>
+// (the 4-wave 128 x 192 tile held to 256 VGPRs: two workgroups per CU -- it took 272 otherwise)
+__global__ void __launch_bounds__(64 * WR * WC, BN == 192 ? 2 : 1) gemm_k64_kernel(Args g) {
+  k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW, WR>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
 // Grouped weight gradients (on this kernel's 64-deep
@@ -664,6 +709,19 @@ static hipError_t launch_l(const Args& g, bool at, bool bt, int ph, bool stg, hi
   return launch<BM, BN, WC, true, false, BUF>(g, ph, stg, st);
 }
 
+// the 192-wide tiles (GPT-2's N = 768 / 2304 / 3072 / 50304 in whole tile columns): K-major A and B (the
+// forward layout), two-phase loop, buffer-descriptor DMA only
+template <int BM, int WC, int WR>
+static hipError_t launch_192(const Args& g, bool at, bool bt, bool buf, bool stg, hipStream_t st) {
+  if (at || bt || !buf || g.epi == EPI_DSWIGLU) return hipErrorInvalidValue;
+  const dim3 grid(g.tiles_m * g.tiles_n), blk(64 * WR * WC);
+  if (stg)
+    hipLaunchKernelGGL((gemm_k64_kernel<BM, 192, WC, false, false, 2, true, true, false, WR>), grid, blk, 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_k64_kernel<BM, 192, WC, false, false, 2, true, false, false, WR>), grid, blk, 0, st, g);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WC>
 static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, bool buf, bool stg, hipStream_t st) {
   return buf ? launch_l<BM, BN, WC, true>(g, at, bt, ph, stg, st) : launch_l<BM, BN, WC, false>(g, at, bt, ph, stg, st);
@@ -682,8 +740,11 @@ constexpr int kW4 = 9;
 constexpr int kW4S = 10;  // the same with the LDS-staged epilogue (whole 256-B row pieces per store)
 constexpr int kFlatDma = 32;
 constexpr int kNoStg = 128;  // tile-id bit: the per-fragment epilogue even where the staged one applies (A/B)
-__host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 ? 128 : 256; }
-__host__ __device__ constexpr int tile_bn(int t) { return t == 2 || t == 3 ? 128 : 256; }
+// 192-wide tiles (two-phase loop, K-major A and B only): 11 = 256 x 192 (8 waves, 4 x 2), 12 = 128 x 192
+// (4 waves, 2 x 2; two workgroups per CU)
+constexpr int kT192 = 11, kT192S = 12;
+__host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 || t == kT192S ? 128 : 256; }
+__host__ __device__ constexpr int tile_bn(int t) { return t == kT192 || t == kT192S ? 192 : (t == 2 || t == 3 ? 128 : 256); }
 
 }  // namespace k64
 }  // namespace dta
@@ -705,6 +766,7 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
     return t ? (t | bits) : 0;
   }
   auto fits = [&](int t) { return M % k64::tile_bm(t) == 0 && N % k64::tile_bn(t) == 0; };
+  if (tile == k64::kT192 || tile == k64::kT192S) return fits(tile) ? tile : 0;
   if (tile) {
     const int base = tile > k64::kTiles ? tile - k64::kTiles : tile;
     return (tile >= 1 && tile <= 2 * k64::kTiles && fits(base)) ? tile : 0;
@@ -807,6 +869,12 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
 #ifdef DTA_K64_STAMP
   g.stamps = dta_k64_stamp_buf;
 #endif
+  if (tile == k64::kT192 || tile == k64::kT192S) {
+    g.tiles_m = M / k64::tile_bm(tile);
+    g.tiles_n = N / 192;
+    return tile == k64::kT192 ? k64::launch_192<256, 2, 4>(g, a_t, b_t, buf, stg, st)
+                              : k64::launch_192<128, 2, 2>(g, a_t, b_t, buf, stg, st);
+  }
   // K-loop phases per 64-deep stage: 4, or 2 for the ids past kTiles
   const int ph = tile > k64::kTiles ? 2 : 4;
   if (tile > k64::kTiles) tile -= k64::kTiles;

@@ -378,15 +378,21 @@ K64 = 10
 # tiles with the two-phase K loop (3-11 % faster than their four-phase forms 1 / 2 / 4 at every
 # GPT-2 and Llama shape: profiles/gemm_k64_vs_hipblaslt.txt), 3 / 7 = 128x128 in both forms
 K64_TILES = (10, 5, 6, 3, 7, 8)  # 10: csrc/gemm_w4.hip (4 waves, 256 x 256; staged epilogue where one bf16 output)
+# 192-wide tiles, K-major A and B only (the forward layout): 11 = 256 x 192 (8 waves), 12 = 128 x 192 (4 waves,
+# two workgroups per CU) -- GPT-2's N = 768 / 2304 / 3072 / 50304 in whole tile columns, so the qkv forward is
+# 768 tiles (3 rounds of 256 CUs) instead of 288 / 576 (1.1 / 2.3 rounds) at the 256- / 128-wide tiles
+K64_TILES_KMAJOR = (11, 12)
 # a hand-written candidate wins a shape when it is at most this much slower than the library (1.0: the
 # faster one; a 2 % preference measured 0.25 ms/step slower on the GPT-2 DDP step, same-box A/B)
 _PREFER_DTA = 1.0
 
 
-def gemm_candidates(M: int, N: int, K: int) -> list:
-    """Hand-written GEMM implementations that cover an M x N x K problem (ids as in _GEMM_CHOICE)."""
+def gemm_candidates(M: int, N: int, K: int, a_t: bool = False, b_t: bool = False) -> list:
+    """Hand-written GEMM implementations that cover an M x N x K problem in the given operand layout
+    (ids as in _GEMM_CHOICE)."""
     C = native()
-    return [K64 + t for t in K64_TILES if C.gemm64_tile(M, N, K, t)]
+    tiles = K64_TILES + (K64_TILES_KMAJOR if not (a_t or b_t) else ())
+    return [K64 + t for t in tiles if C.gemm64_tile(M, N, K, t)]
 
 
 def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]], prefer: float = _PREFER_DTA) -> int:
@@ -495,7 +501,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
     impl = 0
     if _gemm_ok(a, b, bias, out):
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in gemm_candidates(M, N, K):
+        for t in gemm_candidates(M, N, K, a_t, b_t):
             cands[t] = (lambda t=t: _run_gemm(t, a, b, a_t, b_t, out, alpha, bias, scale_dev))
         impl = _pick(kind + ("b" if bias is not None else ""), M, N, K, cands)
     if impl:
@@ -525,7 +531,7 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     impl = 0
     if _gemm_ok(x2, w, b) and N % 8 == 0:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in K64_TILES:
+        for t in K64_TILES + K64_TILES_KMAJOR:
             if C.gemm64_tile(M, N, K, t):
                 cands[K64 + t] = (lambda t=t: run_k64(t))
         # the dual store must win by 15 %: its two output streams cost more inside the step than in
@@ -810,7 +816,7 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     impl = 0
     if ok:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in gemm_candidates(M, N, K):
+        for t in gemm_candidates(M, N, K, False, True):
             cands[t] = (lambda t=t: run(t))
         impl = _pick("dgelu", M, N, K, cands)
     if impl:

@@ -119,6 +119,8 @@ def main():
     if args.merge:
         with open(args.merge) as f:
             base = json.load(f)["entries"]
+        for k, e in entries.items():  # same-box in-step A/B overrides stay with their key
+            e.update({f: v for f, v in base.get(k, {}).items() if f.startswith("in_step_")})
         base.update(entries)
         entries = base
     props = torch.cuda.get_device_properties(0)

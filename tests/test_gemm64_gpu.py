@@ -310,3 +310,83 @@ def test_gemm64_swiglu_backward_epilogue(tile, M, N, K):
     with pytest.raises(RuntimeError):
         C.gemm64(dy, w, False, True, None, None, False, 1.0, torch.zeros(N, dtype=torch.bfloat16, device="cuda"),
                  64, ab, tile)
+
+
+# ---- the 192-wide tiles (11 = 256 x 192, 8 waves in a 4 x 2 grid with the B halves staged as one image;
+# 12 = 128 x 192, 4 waves): K-major A and B only (the forward layout)
+TILES_192 = {11: (256, 192), 12: (128, 192)}
+
+
+@pytest.mark.parametrize("tile", [11, 12])
+def test_gemm64_192_exact_small_integers(tile):
+    """Exact small-integer products through both epilogues (fp32 per-fragment, bf16 staged with its CPR = 24
+    chunk map, and the staged form forced off), pipelines shorter than the DMA look-ahead and many tiles."""
+    from distributed_training_amd.ops import native
+
+    bm, bn = TILES_192[tile]
+    gen = torch.Generator().manual_seed(tile)
+    for M, N, K in ((2 * bm, 3 * bn, 64), (bm, bn, 128), (3 * bm, 2 * bn, 640), (8 * bm, 4 * bn, 192)):
+        a = torch.randint(-3, 4, (M, K), generator=gen).float()
+        b = torch.randint(-3, 4, (N, K), generator=gen).float()
+        want = a @ b.t()
+        got, = native().gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), out_f32=True, tile=tile)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), want), (tile, M, N, K)
+        a01 = a.clamp(-1, 1) * (torch.rand(a.shape, generator=gen) < 0.25)
+        want = a01 @ b.clamp(-1, 1).t()
+        for t in (tile, tile | 128):
+            got, = native().gemm64(a01.bfloat16().cuda(), b.clamp(-1, 1).bfloat16().cuda(), tile=t)
+            torch.cuda.synchronize()
+            assert torch.equal(got.float().cpu(), want), (t, M, N, K)
+
+
+@pytest.mark.parametrize("tile", [11, 12])
+def test_gemm64_192_epilogues_and_layouts(tile):
+    """Bias, GELU dual store, + residual, alpha: staged bit-identical to per-fragment and close to fp32;
+    the transposed layouts are refused loudly (no silent fallback)."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    gen = torch.Generator().manual_seed(40 + tile)
+    M, N, K = 1024, 2304, 384
+    x = torch.randn(M, K, generator=gen).bfloat16().cuda()
+    w = (torch.randn(N, K, generator=gen) * 0.1).bfloat16().cuda()
+    bias = torch.randn(N, generator=gen).bfloat16().cuda()
+    res = torch.randn(M, N, generator=gen).bfloat16().cuda()
+    ref = x.float() @ w.float().t()
+    outs = []
+    for t in (tile, tile | 128):
+        h, act = C.gemm64(x, w, bias=bias, epi=2, out2=torch.empty(M, N, dtype=torch.bfloat16, device="cuda"), tile=t)
+        r, = C.gemm64(x, w, alpha=0.5, bias=bias, epi=32, res=res, tile=t)
+        outs.append((h, act, r))
+    torch.cuda.synchronize()
+    for u, v in zip(*outs):
+        assert torch.equal(u, v), tile
+    h, act, r = outs[0]
+    _close(h, ref + bias.float(), K)
+    torch.testing.assert_close(act.float(), F.gelu(h.float(), approximate="tanh"), rtol=1.6e-2, atol=1e-2)
+    _close(r, 0.5 * ref + bias.float() + res.float(), K)
+    for a_t, b_t in ((False, True), (True, False), (True, True)):
+        a = x.t().contiguous() if a_t else x
+        b = w.t().contiguous() if b_t else w
+        with pytest.raises(RuntimeError):
+            C.gemm64(a, b, a_t, b_t, tile=tile)
+            torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("tile", [11, 12, 11 | 128])
+@pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (8192, 3072, 768), (8192, 768, 3072)])
+def test_gemm64_192_busy_chip(tile, M, N, K):
+    """GPT-2-shaped problems at full occupancy (the staggered 8-wave loop's waits under real DMA latency;
+    the 4-wave tile at two workgroups per CU): random operands, three launches, against fp32."""
+    from distributed_training_amd.ops import native
+
+    gen = torch.Generator(device="cuda").manual_seed(tile + M + N + K)
+    a = torch.randn(M, K, generator=gen, device="cuda").bfloat16()
+    b = (torch.randn(N, K, generator=gen, device="cuda") * 0.02).bfloat16()
+    want = a.float() @ b.float().t()
+    scale = want.abs().max().item()
+    for _ in range(3):
+        got, = native().gemm64(a, b, tile=tile)
+        err = (got.float() - want).abs().max().item() / scale
+        assert err < 8e-3, (tile, err)
