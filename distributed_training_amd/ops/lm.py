@@ -1249,10 +1249,12 @@ class _ChunkedLinearCrossEntropy(Function):
 
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int,
-                chunk: int) -> torch.Tensor:
+                chunk: int, grad: bool) -> torch.Tensor:
         x2 = x.reshape(-1, x.shape[-1])
         T, V = x2.shape[0], w.shape[0]
-        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        # grad: autograd records this call (needs_input_grad is set from requires_grad even under no_grad --
+        # an evaluation forward must neither compute nor write gradients, least of all into an engine's slice)
+        need_dx, need_dw = grad and ctx.needs_input_grad[0], grad and ctx.needs_input_grad[1]
         count = (target != ignore_index).sum().clamp_min(1).float()
         loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
         buf = torch.empty(min(chunk, T), V, dtype=x.dtype, device=x.device)
@@ -1298,7 +1300,7 @@ class _ChunkedLinearCrossEntropy(Function):
         if dw is not None:
             dest = None if ctx.dw_final else _grad_dest(ctx.wparam)
             dw = torch.mul(dw, s, out=dest) if dest is not None else dw.mul_(s)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 HEAD_CE_CHUNK = int(os.environ.get("DTA_HEAD_CE_CHUNK", "0"))
@@ -1321,7 +1323,7 @@ def linear_cross_entropy(x: torch.Tensor, w: torch.Tensor, target: torch.Tensor,
         chunk = HEAD_CE_CHUNK if chunk is None else chunk
         t = target.reshape(-1).contiguous()
         if chunk and chunk % 8 == 0 and t.numel() > chunk:
-            return _ChunkedLinearCrossEntropy.apply(x, w, t, ignore_index, int(chunk))
+            return _ChunkedLinearCrossEntropy.apply(x, w, t, ignore_index, int(chunk), torch.is_grad_enabled())
         return _LinearCrossEntropy.apply(x, w, t, ignore_index)
     logits = F.linear(x, w).reshape(-1, w.shape[0])
     return F.cross_entropy(logits.float(), target.reshape(-1), ignore_index=ignore_index)

@@ -338,6 +338,25 @@ def test_chunked_head_ce_peak_memory():
     assert _rel(grads[1][0], grads[0][0]) < 1e-2 and _rel(grads[1][1], grads[0][1]) < 1e-2
 
 
+def test_chunked_head_ce_no_grad_forward_writes_no_gradient():
+    """An evaluation forward (torch.no_grad) of the row-blocked head + CE computes the loss only: the
+    weight-gradient destination hook an engine attaches (``_dta_gdest_fwd``) is never asked for a slice
+    -- ``needs_input_grad`` alone is still True under no_grad -- and the loss equals the one-block form's."""
+    torch.manual_seed(9)
+    T, C, V = 600, 256, 1000
+    x = (0.5 * torch.randn(T, C, device=DEV)).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (T,), device=DEV)
+    asked = []
+    w._dta_gdest_fwd = lambda: asked.append(1)
+    with torch.no_grad():
+        loss = lm.linear_cross_entropy(x, w, t, chunk=128)
+        ref = lm.linear_cross_entropy(x, w, t, chunk=0)
+    assert not asked and not loss.requires_grad
+    assert abs(loss.item() - ref.item()) < 1e-3 * abs(ref.item())
+    del w._dta_gdest_fwd
+
+
 def test_linear_cross_entropy_scale_in_epilogue(monkeypatch):
     """The hand-written head GEMMs (DTA_GEMM=dta) fold the loss-gradient scale grad / count, a device
     scalar, into their epilogues (gemm64 alpha_dev) -- no separate scaling pass -- and match fp32."""
