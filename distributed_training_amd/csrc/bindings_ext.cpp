@@ -41,8 +41,9 @@ hipError_t dta_gemm_k64_wgrad_group(int, const void* const*, const int64_t*, con
                                     void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
                                     hipStream_t);
 int dta_gemm_k64_tile(int, int, int, int);
+int dta_gemm_k64_sk_plan(int, int, int, int, int*, int*);
 hipError_t dta_gemm_k64(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, void*, int64_t, float*,
-                        int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t, const float*);
+                        int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t, const float*, float*, int*);
 size_t dta_linear_step_lds_bytes(int, int, int, int);
 int dta_linear_step_supported(int, int, int, int);
 
@@ -206,7 +207,7 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
                                     c10::optional<torch::Tensor> out, c10::optional<torch::Tensor> out2,
                                     bool out_f32, double alpha, c10::optional<torch::Tensor> bias, int64_t epi,
                                     c10::optional<torch::Tensor> res, int64_t tile, int64_t stream,
-                                    c10::optional<torch::Tensor> alpha_dev) {
+                                    c10::optional<torch::Tensor> alpha_dev, c10::optional<torch::Tensor> sk_cnt) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm64: GPU tensors");
   TORCH_CHECK(a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16, "gemm64: bf16 operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm64: 2-D, unit inner stride");
@@ -260,10 +261,30 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
                 "gemm64: alpha_dev must be a one-element fp32 GPU tensor");
     ad = alpha_dev->data_ptr<float>();
   }
+  // stream-K ids: fp32 slabs for the cut tiles (from the caching allocator, on this stream) and the caller's
+  // arrival counters (int32 [>= tiles], zero; the kernel leaves them zero)
+  float* skw = nullptr;
+  int* skc = nullptr;
+  torch::Tensor ws;
+  if (tile & 64) {
+    int grid = 0, span = 0;
+    const int tiles = dta_gemm_k64_sk_plan((int)M, (int)N, (int)K, (int)tile, &grid, &span);
+    TORCH_CHECK(tiles > 0, "gemm64: not a stream-K tile for this shape");
+    TORCH_CHECK(sk_cnt && sk_cnt->defined() && sk_cnt->is_cuda() && sk_cnt->scalar_type() == torch::kInt32 &&
+                    sk_cnt->is_contiguous() && sk_cnt->numel() >= tiles && sk_cnt->device() == a.device(),
+                "gemm64: stream-K needs sk_cnt, int32 zeros [>= tiles] on the operands' device");
+    const int base = (int)(tile & ~(64 | 128));
+    const int tb = base > 4 && base <= 8 ? base - 4 : base;
+    const int64_t bm = (tb == 3 || tb == 4 || tb == 12) ? 128 : 256;
+    const int64_t bn = (tb == 11 || tb == 12) ? 192 : ((tb == 2 || tb == 3) ? 128 : 256);
+    ws = torch::empty({(int64_t)grid * 2 * bm * bn}, a.options().dtype(torch::kFloat32));
+    skw = ws.data_ptr<float>();
+    skc = sk_cnt->data_ptr<int>();
+  }
   ok(dta_gemm_k64(a.data_ptr(), a.stride(0), a_t, b.data_ptr(), b.stride(0), b_t, out_f32 ? nullptr : c.data_ptr(),
                   c.stride(0), two ? c2.data_ptr() : nullptr, two ? c2.stride(0) : 0,
                   out_f32 ? c.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, (float)alpha, bp, (int)epi, rp, ldr,
-                  (int)tile, stream_of(stream), ad),
+                  (int)tile, stream_of(stream), ad, skw, skc),
      "gemm64");
   if (two) return {c, c2};
   return {c};
@@ -284,7 +305,12 @@ void dta_register_ext(pybind11::module_& m) {
   m.def("gemm64", &gemm_k64, py::arg("a"), py::arg("b"), py::arg("a_t") = false, py::arg("b_t") = false,
         py::arg("out") = py::none(), py::arg("out2") = py::none(), py::arg("out_f32") = false, py::arg("alpha") = 1.0,
         py::arg("bias") = py::none(), py::arg("epi") = 0, py::arg("res") = py::none(), py::arg("tile") = 0,
-        py::arg("stream") = -1, py::arg("alpha_dev") = py::none());
+        py::arg("stream") = -1, py::arg("alpha_dev") = py::none(), py::arg("sk_cnt") = py::none());
+  m.def("gemm64_sk_plan", [](int M, int N, int K, int tile) {
+          int grid = 0, span = 0;
+          const int tiles = dta_gemm_k64_sk_plan(M, N, K, tile, &grid, &span);
+          return std::vector<int>{tiles, grid, span};
+        }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile"));
   m.def("gemm64_tile", [](int M, int N, int K, int tile) { return dta_gemm_k64_tile(M, N, K, tile); },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile") = 0);
   m.def("linear_step_supported", [](int I, int C, int B, bool mom) { return dta_linear_step_supported(I, C, B, mom) != 0; });

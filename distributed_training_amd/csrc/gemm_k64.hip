@@ -70,12 +70,14 @@
 #include "common.h"
 #include "gemm_epi.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
 namespace dta {
 namespace k64 {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #ifdef DTA_K64_STAMP
 // s_memtime with its lgkmcnt(0) in ONE statement (cdna_hip_programming.md "In-kernel stamps"); the
@@ -160,6 +162,22 @@ __device__ __forceinline__ int cswz(int row) {
   else return row & 7;
 }
 
+// Stream-K (SK): the grid's G workgroups split the problem's tiles x K-tiles "units" into equal runs of
+// `span` >= ceil(nk / 2) units, so every CU gets the same work whatever the tile count (GPT-2's N = 768
+// input gradients are 192 tiles of 256 x 128 for 256 CUs; Llama's qkv weight gradient 384 of 256 x 256).
+// A tile whose K range is cut between workgroups (at most three, by the span bound) is finished by the
+// LAST of them to arrive: each contributor stores its fp32 accumulators write-through (sc1, 16 B) into its
+// own slab, drains them (vmcnt(0) in every wave), and one lane adds to the tile's counter (agent scope);
+// the workgroup whose add returns n - 1 reads the other slabs with sc1 loads, sums the parts in K order
+// (((p0 + p1) + p2): the same bits whoever arrives last -- fp32 addition commutes) and runs the normal
+// epilogue, then re-zeroes the counter (zeroed once at allocation; cdna_hip_programming.md split-K
+// in-launch reduction, the sc1 form).  No workgroup ever waits for another.
+struct SkArgs {
+  float* ws;         // [G][2][BM * BN] fp32 slabs: a workgroup's first (slot 0) and last (slot 1) segment
+  int* cnt;          // [tiles] arrival counters, zero between launches
+  int span;          // units (K-tiles) per workgroup
+};
+
 // STG (one bf16 output): the epilogue goes through the LDS as a whole BM x BN bf16 tile image (in the LDS
 // the K loop used: the image is at most its size) and leaves as whole 2 BN-byte rows -- instead of one 8-B
 // store per lane per fragment (16 rows x 32 B per instruction).  Measured (scripts/bench_w4.py, 256 x 256):
@@ -168,8 +186,10 @@ __device__ __forceinline__ int cswz(int row) {
 // DSW: the EPI_DSWIGLU instantiation (a compile-time form: its two-round epilogue in the shared body cost
 // every other kernel registers -- 256 VGPRs and scratch spills at the 256 x 256 tile)
 template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool CS, bool STG = false, bool DSW = false,
-          int WR = 2>
-__device__ __forceinline__ void k64_body(const Args& g, const int t) {
+          int WR = 2, bool SK = false>
+__device__ __forceinline__ void k64_body(const Args& g, const int t, const int kb = 0, const int ke = 0,
+                                         const SkArgs* sk = nullptr, const int wsk = 0, const int slot = 0) {
+  static_assert(!SK || (PH == 2 && !CS && !DSW), "stream-K: two-phase loop, plain / fused epilogues");
   static_assert(!DSW || STG, "the SwiGLU-backward epilogue is LDS-staged only");
   static_assert(!CS || (PH == 2 && AT), "bias-gradient column sums: two-phase loop, M-major A (weight gradients)");
   static_assert(!STG || BM * BN * 2 <= 2 * Cfg<BM, BN, WC, AT, BT, WR>::BUF, "staged epilogue: the tile image fits the LDS");
@@ -191,7 +211,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   const int grp = t / per_group, in_g = t - grp * per_group;
   const int gm0 = grp * kGroupM, gh = min(kGroupM, g.tiles_m - gm0);
   const int m0 = (gm0 + in_g % gh) * BM, n0 = (in_g / gh) * BN;
-  const int nk = g.K / BK;
+  const int nk_all = g.K / BK;
+  // SK: this workgroup's K-tiles [kb, ke) of the tile (the DMA offsets start at kb); else all of them
+  const int kofs = SK ? kb : 0, nk = SK ? ke - kb : nk_all;
 
   // ---- per-lane DMA sources of K-tile 0 (half h: rows / columns [h * H, (h+1) * H)) ----
   // half index: 0 top, 1 bottom, 2 left, 3 right; LDS: buffer b at b * BUF, [top|bottom|left|right]
@@ -264,7 +286,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
     return ILV ? 4 * C::A_HALF + (2 * h + par) * C::B_HALF : par * C::BUF + 2 * C::A_HALF + h * C::B_HALF;
   };
   auto dma_a = [&](int h, int kt) {  // A half h of K-tile kt (past the end: the last K-tile, never read)
-    const int ks = min(kt, nk - 1);
+    const int ks = kofs + min(kt, nk - 1);
     char* dst = lds + aoff(h, kt & 1);
     if constexpr (BUF) {
       const unsigned so = (unsigned)(ks * stepA * 2), d0 = lds0 + aoff(h, kt & 1);
@@ -277,7 +299,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   };
   auto dma_b = [&](int h, int kt) {  // (BJ: h = 0 stages both halves, h = 1 nothing)
     if (BJ && h) return;
-    const int ks = min(kt, nk - 1);
+    const int ks = kofs + min(kt, nk - 1);
     char* dst = lds + boff(h, kt & 1);
     if constexpr (BUF) {
       const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + boff(h, kt & 1);
@@ -485,6 +507,59 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t) {
   if constexpr (STAG) {
     if (!lag) bar();  // equal barrier counts for both halves
   }
+  if constexpr (SK) {
+    if (nk != nk_all) {  // a cut tile: publish this part; the last contributor to arrive finishes the tile
+      constexpr int NQ = 4 * NTH * MTH, NT = 64 * NW;  // f32x4 accumulators per lane, threads
+      constexpr unsigned SLAB = (unsigned)BM * BN * 4;
+      const int64_t u0 = (int64_t)t * nk_all;
+      const int lo = (int)(u0 / sk->span), hi = (int)((u0 + nk_all - 1) / sk->span);
+      auto slab = [&](int w, int sl) __attribute__((always_inline)) {
+        return __builtin_amdgcn_make_buffer_rsrc(sk->ws + ((int64_t)w * 2 + sl) * (SLAB / 4), 0, SLAB, 0x00020000);
+      };
+      {
+        const __amdgpu_buffer_rsrc_t own = slab(wsk, slot);
+#pragma unroll
+        for (int i = 0; i < 2 * NTH; ++i)
+#pragma unroll
+          for (int j = 0; j < 2 * MTH; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), own,
+                                                   (unsigned)(((i * 2 * MTH + j) * NT + tid) * 16), 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(lds);  // (the one LDS array: the K loop is done with it)
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(sk->cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == hi - lo;
+        if (last) __hip_atomic_store(sk->cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
+      }
+      __syncthreads();
+      const bool last = *flag != 0;
+      __syncthreads();  // every wave has read the flag before the epilogue reuses the LDS
+      if (!last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (keeps the slab loads below the ticket)
+      // the tile = the contributors' parts summed in K order, ((p_lo + ...) + p_hi), every part (this one too,
+      // stored above) read back from its slab: the same bits whoever arrives last, one part of each fragment
+      // row in flight at a time (the accumulators plus one row of parts fit the registers)
+      auto slot_of = [&](int c) __attribute__((always_inline)) { return ((int64_t)c * sk->span) / nk_all == t ? 0 : 1; };
+      for (int c = lo; c <= hi; ++c) {
+        const __amdgpu_buffer_rsrc_t r = slab(c, slot_of(c));
+#pragma unroll
+        for (int i = 0; i < 2 * NTH; ++i) {
+          f32x4 pa[2 * MTH];
+#pragma unroll
+          for (int j = 0; j < 2 * MTH; ++j)
+            pa[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  r, (unsigned)(((i * 2 * MTH + j) * NT + tid) * 16), 0, 16));
+#pragma unroll
+          for (int j = 0; j < 2 * MTH; ++j) acc[i][j] = c == lo ? pa[j] : acc[i][j] + pa[j];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      static_assert(NQ == 4 * NTH * MTH, "");
+    }
+  }
 
   if constexpr (CS) {
     if (do_cs && wc < MTH && (lane >> 4) == 0) {  // (the four columns of accb are equal)
@@ -656,6 +731,24 @@ __global__ void __launch_bounds__(64 * WR * WC, BN == 192 ? 2 : 1) gemm_k64_kern
   k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW, WR>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
+// Stream-K form (SkArgs): workgroup w (XCD-remapped: consecutive runs share an XCD's L2) walks the units
+// [w span, (w + 1) span) of the tile-major (tile, K-tile) order, one body call per tile segment
+template <int BM, int BN, int WC, bool AT, bool BT, bool STG, int WR = 2>
+__global__ void __launch_bounds__(64 * WR * WC, BN == 192 ? 2 : 1) gemm_k64_sk_kernel(Args g, SkArgs s) {
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int nk = g.K / BK;
+  const int64_t units = (int64_t)g.tiles_m * g.tiles_n * nk;
+  const int64_t u1 = min(units, (int64_t)(w + 1) * s.span);
+  bool first = true;
+  for (int64_t u = (int64_t)w * s.span; u < u1; first = false) {
+    const int t = (int)(u / nk), kb = (int)(u - (int64_t)t * nk);
+    const int ke = (int)min<int64_t>(nk, kb + (u1 - u));
+    if (!first) __syncthreads();  // the previous segment's epilogue is done with the LDS
+    k64_body<BM, BN, WC, AT, BT, 2, true, false, STG, false, WR, true>(g, t, kb, ke, &s, w, first ? 0 : 1);
+    u += ke - kb;
+  }
+}
+
 // Grouped weight gradients (on this kernel's 64-deep
 // two-phase loop): dW_i = A_i^T B_i for several problems in ONE launch of 256 x 256 tiles over the
 // full token reduction, the bias gradients from the same MFMA pipe (CS); the tiles of all problems
@@ -722,6 +815,27 @@ static hipError_t launch_192(const Args& g, bool at, bool bt, bool buf, bool stg
   return hipGetLastError();
 }
 
+template <int BM, int BN, int WC, int WR = 2>
+static hipError_t launch_sk(const Args& g, const SkArgs& s, int grid, bool at, bool bt, bool stg, hipStream_t st) {
+  const dim3 gd(grid), blk(64 * WR * WC);
+#define DTA_SK_L(AT_, BT_)                                                                                        \
+  do {                                                                                                           \
+    if (stg) hipLaunchKernelGGL((gemm_k64_sk_kernel<BM, BN, WC, AT_, BT_, true, WR>), gd, blk, 0, st, g, s);    \
+    else hipLaunchKernelGGL((gemm_k64_sk_kernel<BM, BN, WC, AT_, BT_, false, WR>), gd, blk, 0, st, g, s);       \
+  } while (0)
+  if constexpr (BN == 192) {  // K-major operands only
+    if (at || bt) return hipErrorInvalidValue;
+    DTA_SK_L(false, false);
+  } else {
+    if (!at && !bt) DTA_SK_L(false, false);
+    else if (!at && bt) DTA_SK_L(false, true);
+    else if (at && bt) DTA_SK_L(true, true);
+    else return hipErrorInvalidValue;  // (the TT layout: no stream-K instantiation)
+  }
+#undef DTA_SK_L
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WC>
 static hipError_t launch_t(const Args& g, bool at, bool bt, int ph, bool buf, bool stg, hipStream_t st) {
   return buf ? launch_l<BM, BN, WC, true>(g, at, bt, ph, stg, st) : launch_l<BM, BN, WC, false>(g, at, bt, ph, stg, st);
@@ -743,6 +857,11 @@ constexpr int kNoStg = 128;  // tile-id bit: the per-fragment epilogue even wher
 // 192-wide tiles (two-phase loop, K-major A and B only): 11 = 256 x 192 (8 waves, 4 x 2), 12 = 128 x 192
 // (4 waves, 2 x 2; two workgroups per CU)
 constexpr int kT192 = 11, kT192S = 12;
+// tile-id bit: the stream-K form of a two-phase tile (5-8, 11, 12; buffer DMA), see SkArgs
+constexpr int kSK = 64;
+__host__ __device__ constexpr bool sk_base(int t) { return (t >= 5 && t <= 8) || t == kT192 || t == kT192S; }
+// resident workgroups per CU of each two-phase tile (LDS: 128 / 96 / 64 / 96 / 112 / 80 KB; VGPRs)
+__host__ __device__ constexpr int sk_per_cu(int t) { return t == 7 || t == kT192S ? 2 : 1; }
 __host__ __device__ constexpr int tile_bm(int t) { return t == 3 || t == 4 || t == kT192S ? 128 : 256; }
 __host__ __device__ constexpr int tile_bn(int t) { return t == kT192 || t == kT192S ? 192 : (t == 2 || t == 3 ? 128 : 256); }
 
@@ -767,6 +886,11 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   }
   auto fits = [&](int t) { return M % k64::tile_bm(t) == 0 && N % k64::tile_bn(t) == 0; };
   if (tile == k64::kT192 || tile == k64::kT192S) return fits(tile) ? tile : 0;
+  if (tile & k64::kSK) {  // stream-K: a two-phase tile (optionally with the per-fragment epilogue bit)
+    const int base = tile & ~(k64::kSK | k64::kNoStg);
+    const int tb = base > k64::kTiles && base <= 2 * k64::kTiles ? base - k64::kTiles : base;
+    return k64::sk_base(base) && fits(tb) ? tile : 0;
+  }
   if (tile) {
     const int base = tile > k64::kTiles ? tile - k64::kTiles : tile;
     return (tile >= 1 && tile <= 2 * k64::kTiles && fits(base)) ? tile : 0;
@@ -790,6 +914,30 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
   return best && best != 3 ? best + k64::kTiles : best;
 }
 
+// Stream-K plan of a tile id with the kSK bit: the grid (resident workgroups of the tile on this device, or
+// fewer where a run would drop below half a tile's K-tiles) and each workgroup's run of K-tile units; returns
+// the tile count (the arrival counters the call needs), 0 if the id is not a stream-K id for the shape
+int dta_gemm_k64_sk_plan(int M, int N, int K, int tile, int* grid, int* span) {
+  if (!(tile & k64::kSK) || !dta_gemm_k64_tile(M, N, K, tile)) return 0;
+  const int base = tile & ~(k64::kSK | k64::kNoStg);
+  const int tb = base > k64::kTiles && base <= 2 * k64::kTiles ? base - k64::kTiles : base;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t pr;
+    ncu = hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 256;
+  }
+  const int tiles = (M / k64::tile_bm(tb)) * (N / k64::tile_bn(tb));
+  const int nk = K / k64::BK;
+  const int64_t units = (int64_t)tiles * nk;
+  const int64_t g0 = (int64_t)ncu * k64::sk_per_cu(base);
+  int64_t sp = (units + g0 - 1) / g0;
+  sp = std::max<int64_t>(sp, (nk + 1) / 2);  // at most three workgroups share a tile
+  *span = (int)sp;
+  *grid = (int)((units + sp - 1) / sp);
+  return tiles;
+}
+
 #ifdef DTA_K64_STAMP
 unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k64_stamps.hip)
 #endif
@@ -799,7 +947,12 @@ unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k
 hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int64_t ldb, bool b_t, void* c,
                         int64_t ldc, void* c2, int64_t ldc2, float* c32, int M, int N, int K, float alpha,
                         const void* bias, int epi, const void* res, int64_t ldr, int tile, hipStream_t st,
-                        const float* alpha_dev) {
+                        const float* alpha_dev, float* sk_ws, int* sk_cnt) {
+  int sk_grid = 0, sk_span = 0;
+  if (tile & k64::kSK) {
+    if (!dta_gemm_k64_sk_plan(M, N, K, tile, &sk_grid, &sk_span) || !sk_ws || !sk_cnt || epi == k64::EPI_DSWIGLU)
+      return hipErrorInvalidValue;
+  }
   tile = dta_gemm_k64_tile(M, N, K, tile);
   if (!tile || (!c && !c32)) return hipErrorInvalidValue;
   if (epi == k64::EPI_DSWIGLU && (bias || c32 || !res || c2)) return hipErrorInvalidValue;
@@ -869,6 +1022,22 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
 #ifdef DTA_K64_STAMP
   g.stamps = dta_k64_stamp_buf;
 #endif
+  if (tile & k64::kSK) {
+    if (!buf) return hipErrorInvalidValue;  // (buffer-descriptor DMA only)
+    const int base = tile & ~k64::kSK;
+    const int tb = base > k64::kTiles && base <= 2 * k64::kTiles ? base - k64::kTiles : base;
+    g.tiles_m = M / k64::tile_bm(tb);
+    g.tiles_n = N / k64::tile_bn(tb);
+    const k64::SkArgs s{sk_ws, sk_cnt, sk_span};
+    switch (base) {
+      case 5: return k64::launch_sk<256, 256, 4>(g, s, sk_grid, a_t, b_t, stg, st);
+      case 6: return k64::launch_sk<256, 128, 4>(g, s, sk_grid, a_t, b_t, stg, st);
+      case 7: return k64::launch_sk<128, 128, 2>(g, s, sk_grid, a_t, b_t, stg, st);
+      case 8: return k64::launch_sk<128, 256, 4>(g, s, sk_grid, a_t, b_t, stg, st);
+      case k64::kT192: return k64::launch_sk<256, 192, 2, 4>(g, s, sk_grid, a_t, b_t, stg, st);
+      default: return k64::launch_sk<128, 192, 2, 2>(g, s, sk_grid, a_t, b_t, stg, st);
+    }
+  }
   if (tile == k64::kT192 || tile == k64::kT192S) {
     g.tiles_m = M / k64::tile_bm(tile);
     g.tiles_n = N / 192;

@@ -387,12 +387,28 @@ K64_TILES_KMAJOR = (11, 12)
 _PREFER_DTA = 1.0
 
 
-def gemm_candidates(M: int, N: int, K: int, a_t: bool = False, b_t: bool = False) -> list:
+def gemm_candidates(M: int, N: int, K: int, a_t: bool = False, b_t: bool = False, sk: bool = True) -> list:
     """Hand-written GEMM implementations that cover an M x N x K problem in the given operand layout
-    (ids as in _GEMM_CHOICE)."""
+    (ids as in _GEMM_CHOICE; ``sk``: with the stream-K forms where they can help).  Memoised per shape."""
+    key = (M, N, K, bool(a_t), bool(b_t), bool(sk))
+    c = _CANDS.get(key)
+    if c is None:
+        c = _CANDS[key] = _gemm_candidates(M, N, K, a_t, b_t, sk)
+    return c
+
+
+_CANDS: Dict[tuple, list] = {}
+
+
+def _gemm_candidates(M: int, N: int, K: int, a_t: bool, b_t: bool, sk: bool) -> list:
     C = native()
-    tiles = K64_TILES + (K64_TILES_KMAJOR if not (a_t or b_t) else ())
-    return [K64 + t for t in tiles if C.gemm64_tile(M, N, K, t)]
+    kmaj = not (a_t or b_t)
+    tiles = K64_TILES + (K64_TILES_KMAJOR if kmaj else ())
+    out = [K64 + t for t in tiles if C.gemm64_tile(M, N, K, t)]
+    if sk and not (a_t and not b_t):
+        out += [K64 + (t | SK_BIT) for t in _SK_TILES + (_SK_TILES_KMAJOR if kmaj else ())
+                if C.gemm64_tile(M, N, K, t | SK_BIT) and _sk_useful(M, N, K, t)]
+    return out
 
 
 def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], object]], prefer: float = _PREFER_DTA) -> int:
@@ -446,6 +462,8 @@ def _pick(kind: str, M: int, N: int, K: int, cands: Dict[int, Callable[[], objec
 
             logging.getLogger(__name__).info("GEMM %s %dx%dx%d not in the tracked table: timed in-run -> %s",
                                              kind, M, N, K, _impl_name(c))
+    if c and (c - K64) & SK_BIT and _sk_cnt(torch.device("cuda", torch.cuda.current_device())) is None:
+        c = K64 + ((c - K64) & ~SK_BIT)  # (no counters yet, inside a graph capture: the tile's plain form)
     _GEMM_CHOICE[key] = c
     GEMM_PICK_SOURCE[key] = src
     if mode == "auto":
@@ -458,13 +476,60 @@ def _capturing() -> bool:
 
 
 def _impl_name(c: int) -> str:
-    return "hipblaslt" if not c else f"k64/t{c - K64}"
+    if not c:
+        return "hipblaslt"
+    t = c - K64
+    return f"k64/t{t & ~SK_BIT}sk" if t & SK_BIT else f"k64/t{t}"
+
+
+# ---- stream-K forms of the two-phase tiles (csrc/gemm_k64.hip SkArgs): tile id | SK_BIT.  The grid is the
+# tile's resident workgroups and each takes an equal run of (tile, K-tile) units, so a shape whose tile count
+# leaves part of the chip idle in its last round (GPT-2's N = 768 input gradients: 192 tiles of 256 x 128 on
+# 256 CUs; Llama's qkv weight gradient: 384 of 256 x 256) keeps every CU busy; a tile cut between workgroups
+# is finished by the last to arrive, the parts summed in K order (deterministic).
+SK_BIT = 64
+_SK_TILES = (5, 6, 7, 8)            # any layout but TT
+_SK_TILES_KMAJOR = (11, 12)         # K-major A and B
+_SK_CNT: Dict[int, torch.Tensor] = {}  # per device: the arrival counters (zero between launches)
+_SK_CNT_LEN = 1 << 17
+
+
+def _sk_cnt(dev: torch.device) -> Optional[torch.Tensor]:
+    """The device's stream-K arrival counters (allocated zeroed on first use outside graph capture; the kernel
+    leaves them zero).  GEMMs of one device run on one stream at a time (the compute stream, or the capture
+    stream while a step graph is recorded), so one buffer per device serves them all."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    c = _SK_CNT.get(idx)
+    if c is None and not _capturing():
+        c = _SK_CNT[idx] = torch.zeros(_SK_CNT_LEN, dtype=torch.int32, device=dev)
+    return c
+
+
+def _sk_useful(M: int, N: int, K: int, t: int) -> bool:
+    """A stream-K candidate where the plain tile's last round would leave >= 10 % of the slots idle and the
+    reduction is deep (K >= 8192): every cut tile costs an fp32 slab per part (128-256 KB, written and read
+    back at the end of a workgroup's run), which the shallow shapes do not earn back -- GPT-2's K = 768-3072
+    input gradients measured 30-60 % slower in stream-K form, its K = 8192 weight gradients and K = 50304
+    LM-head input gradient faster (profiles/gemm_table_sk_r5t.jsonl)."""
+    if K < 8192:
+        return False
+    tiles, grid, _span = native().gemm64_sk_plan(M, N, K, t | SK_BIT)
+    if tiles <= 0 or tiles > _SK_CNT_LEN:
+        return False
+    slots = 256 * (2 if t in (7, 12) else 1)
+    rounds = -(-tiles // slots)
+    return tiles < 0.9 * rounds * slots
+
+
+def _cnt_for(impl: int, x: torch.Tensor) -> Optional[torch.Tensor]:
+    return _sk_cnt(x.device) if (impl - K64) & SK_BIT else None
 
 
 def _run_gemm(impl: int, a: torch.Tensor, b: torch.Tensor, a_t: bool, b_t: bool, out: Optional[torch.Tensor] = None,
               alpha: float = 1.0, bias: Optional[torch.Tensor] = None,
               alpha_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
-    return native().gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64, -1, alpha_dev)[0]
+    return native().gemm64(a, b, a_t, b_t, out, None, False, alpha, bias, 0, None, impl - K64, -1, alpha_dev,
+                           _cnt_for(impl, a))[0]
 
 
 def _gemm_ok(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -526,14 +591,14 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
 
     def run_k64(t: int) -> Tuple[torch.Tensor, ...]:
         h = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
-        return tuple(C.gemm64(x2, w, False, False, h, torch.empty_like(h), False, 1.0, b, 2, None, t))
+        return tuple(C.gemm64(x2, w, False, False, h, torch.empty_like(h), False, 1.0, b, 2, None, t, -1, None,
+                              _cnt_for(K64 + t, x2)))
 
     impl = 0
     if _gemm_ok(x2, w, b) and N % 8 == 0:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in K64_TILES + K64_TILES_KMAJOR:
-            if C.gemm64_tile(M, N, K, t):
-                cands[K64 + t] = (lambda t=t: run_k64(t))
+        for c in gemm_candidates(M, N, K):
+            cands[c] = (lambda t=c - K64: run_k64(t))
         # the dual store must win by 15 %: its two output streams cost more inside the step than in
         # the back-to-back timing (GPT-2 fc: per-fragment 85.8 us in-step vs 69-76 timed, staged 78-82
         # vs 64.8; hipBLASLt + GELU kernel 47.1 + 23.1 us in-step -- profiles/gpt2_ddp_1gpu_kernels_r4.txt,
@@ -808,7 +873,8 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
           and h2.data_ptr() % 16 == 0 and N % 8 == 0)
 
     def run(impl: int) -> torch.Tensor:
-        return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64)[0]
+        return C.gemm64(dy2, w, False, True, None, None, False, 1.0, None, 16, h2, impl - K64, -1, None,
+                        _cnt_for(impl, dy2))[0]
 
     def run_torch() -> torch.Tensor:
         return C.gelu_bwd(torch.mm(dy2, w), h2, -1)

@@ -390,3 +390,114 @@ def test_gemm64_192_busy_chip(tile, M, N, K):
         got, = native().gemm64(a, b, tile=tile)
         err = (got.float() - want).abs().max().item() / scale
         assert err < 8e-3, (tile, err)
+
+
+# ---- stream-K forms (tile id | 64): equal runs of (tile, K-tile) units per workgroup; a cut tile is summed
+# by its last-arriving contributor in K order (deterministic), counters left zero
+SK = 64
+SK_TILES = {5: (256, 256), 6: (256, 128), 7: (128, 128), 8: (128, 256), 11: (256, 192), 12: (128, 192)}
+SK_LAYOUTS = [(False, False), (False, True), (True, True)]
+
+
+def _sk_cnt():
+    from distributed_training_amd.ops import lm
+
+    return lm._sk_cnt(torch.device("cuda", torch.cuda.current_device()))
+
+
+@pytest.mark.parametrize("tile", [5, 6, 7, 8, 11, 12])
+@pytest.mark.parametrize("a_t,b_t", SK_LAYOUTS)
+def test_gemm64_stream_k_exact(a_t, b_t, tile):
+    """Small integers (exact in fp32 whatever the summation order) through the stream-K form at tile counts and
+    K depths that cut tiles into two and three parts (span = ceil(nk / 2) when the tiles are few), fp32 and
+    staged bf16 outputs; the arrival counters are zero afterwards."""
+    from distributed_training_amd.ops import native
+
+    if tile in (11, 12) and (a_t or b_t):
+        pytest.skip("192-wide tiles: K-major operands only")
+    C = native()
+    bm, bn = SK_TILES[tile]
+    cnt = _sk_cnt()
+    gen = torch.Generator().manual_seed(100 + tile + 2 * a_t + b_t)
+    for M, N, K in ((3 * bm, 5 * bn, 448), (bm, 2 * bn, 64 * 9), (2 * bm, 3 * bn, 64 * 48), (bm, bn, 64)):
+        tiles, grid, span = C.gemm64_sk_plan(M, N, K, tile | SK)
+        assert tiles == (M // bm) * (N // bn) and span >= (K // 64 + 1) // 2
+        a = torch.randint(-3, 4, (K, M) if a_t else (M, K), generator=gen).float()
+        b = torch.randint(-3, 4, (K, N) if b_t else (N, K), generator=gen).float()
+        want = (a.t() if a_t else a) @ (b if b_t else b.t())
+        got, = C.gemm64(a.bfloat16().cuda(), b.bfloat16().cuda(), a_t, b_t, out_f32=True, tile=tile | SK, sk_cnt=cnt)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), want), (tile, a_t, b_t, M, N, K)
+        a01 = a.clamp(-1, 1) * (torch.rand(a.shape, generator=gen) < 0.25)
+        want = (a01.t() if a_t else a01) @ (b.clamp(-1, 1) if b_t else b.clamp(-1, 1).t())
+        for t in (tile | SK, tile | SK | 128):
+            got, = C.gemm64(a01.bfloat16().cuda(), b.clamp(-1, 1).bfloat16().cuda(), a_t, b_t, tile=t, sk_cnt=cnt)
+            torch.cuda.synchronize()
+            assert torch.equal(got.float().cpu(), want), (t, a_t, b_t, M, N, K)
+    assert int(cnt.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("tile", [6, 7, 12])
+def test_gemm64_stream_k_epilogues_deterministic(tile):
+    """The fused epilogues through the stream-K form (bias, GELU dual store, + residual; x gelu'(res) in the
+    input-gradient layout) match the plain tile's to bf16 rounding and repeat bit-identically."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    cnt = _sk_cnt()
+    gen = torch.Generator().manual_seed(60 + tile)
+    M, N, K = 1024, 768 if tile != 12 else 1536, 64 * 30
+    x = torch.randn(M, K, generator=gen).bfloat16().cuda()
+    w = (torch.randn(N, K, generator=gen) * 0.05).bfloat16().cuda()
+    wn = (torch.randn(K, N, generator=gen) * 0.05).bfloat16().cuda()
+    bias = torch.randn(N, generator=gen).bfloat16().cuda()
+    res = torch.randn(M, N, generator=gen).bfloat16().cuda()
+
+    def run(t):
+        h, act = C.gemm64(x, w, bias=bias, epi=2, out2=torch.empty(M, N, dtype=torch.bfloat16, device="cuda"),
+                          tile=t, sk_cnt=cnt)
+        r, = C.gemm64(x, w, alpha=0.5, bias=bias, epi=32, res=res, tile=t, sk_cnt=cnt)
+        outs = [h, act, r]
+        if tile != 12:
+            d, = C.gemm64(x, wn, False, True, epi=16, res=res, tile=t, sk_cnt=cnt)
+            outs.append(d)
+        return outs
+
+    plain, sk1, sk2 = run(tile), run(tile | SK), run(tile | SK)
+    torch.cuda.synchronize()
+    for u, v in zip(sk1, sk2):
+        assert torch.equal(u, v), tile
+    for u, v in zip(sk1, plain):
+        torch.testing.assert_close(u.float(), v.float(), rtol=2e-2, atol=2e-2)
+    assert int(cnt.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("tile,a_t,b_t,M,N,K", [
+    (6, False, True, 8192, 768, 3072),     # GPT-2 input gradients (192 tiles of 256 x 128)
+    (7, False, True, 8192, 768, 2304),
+    (12, False, False, 8192, 768, 3072),   # GPT-2 fc2 forward
+    (5, True, True, 6144, 4096, 8192),     # Llama qkv weight gradient (384 tiles of 256 x 256)
+    (6, False, False, 8192, 768, 768),
+])
+def test_gemm64_stream_k_busy_chip(tile, a_t, b_t, M, N, K):
+    """Full-chip stream-K launches at the shapes it is for, random operands against fp32, three launches
+    bit-identical (the cut tiles' parts are summed in K order whoever arrives last)."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    cnt = _sk_cnt()
+    gen = torch.Generator(device="cuda").manual_seed(tile + M + N + K)
+    a = torch.randn((K, M) if a_t else (M, K), generator=gen, device="cuda").bfloat16()
+    b = (torch.randn((K, N) if b_t else (N, K), generator=gen, device="cuda") * 0.02).bfloat16()
+    want = (a.float().t() if a_t else a.float()) @ (b.float() if b_t else b.float().t())
+    scale = want.abs().max().item()
+    first = None
+    for _ in range(3):
+        got, = C.gemm64(a, b, a_t, b_t, tile=tile | SK, sk_cnt=cnt)
+        err = (got.float() - want).abs().max().item() / scale
+        assert err < 8e-3, (tile, err)
+        if first is None:
+            first = got.clone()
+        else:
+            assert torch.equal(got, first), tile
+    assert int(cnt.abs().sum().item()) == 0

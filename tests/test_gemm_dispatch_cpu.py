@@ -26,7 +26,8 @@ def _fresh(monkeypatch, table_on=True):
 def test_table_is_valid_and_covers_the_lm_steps():
     doc = json.load(open(lm.TABLE_PATH))
     assert "gfx950" in doc["arch"] and doc["rounds"] >= 9
-    valid = {0} | {lm.K64 + t for t in lm.K64_TILES + lm.K64_TILES_KMAJOR}
+    base = lm.K64_TILES + lm.K64_TILES_KMAJOR
+    valid = {0} | {lm.K64 + t for t in base} | {lm.K64 + (t | lm.SK_BIT) for t in lm._SK_TILES + lm._SK_TILES_KMAJOR}
     kinds = set()
     for key, e in doc["entries"].items():
         kind, dims = key.rsplit(" ", 1)
