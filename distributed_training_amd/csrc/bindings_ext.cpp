@@ -41,7 +41,7 @@ hipError_t dta_gemm_k64_wgrad_group(int, const void* const*, const int64_t*, con
                                     void* const*, const int64_t*, const int*, const int*, const int*, void* const*,
                                     hipStream_t);
 int dta_gemm_k64_tile(int, int, int, int);
-int dta_gemm_k64_sk_plan(int, int, int, int, int*, int*);
+int dta_gemm_k64_sk_plan(int, int, int, int, int*, int*, int64_t*);
 hipError_t dta_gemm_k64(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, void*, int64_t, float*,
                         int, int, int, float, const void*, int, const void*, int64_t, int, hipStream_t, const float*, float*, int*);
 size_t dta_linear_step_lds_bytes(int, int, int, int);
@@ -268,16 +268,13 @@ std::vector<torch::Tensor> gemm_k64(torch::Tensor a, torch::Tensor b, bool a_t, 
   torch::Tensor ws;
   if (tile & 64) {
     int grid = 0, span = 0;
-    const int tiles = dta_gemm_k64_sk_plan((int)M, (int)N, (int)K, (int)tile, &grid, &span);
+    int64_t wsf = 0;
+    const int tiles = dta_gemm_k64_sk_plan((int)M, (int)N, (int)K, (int)tile, &grid, &span, &wsf);
     TORCH_CHECK(tiles > 0, "gemm64: not a stream-K tile for this shape");
     TORCH_CHECK(sk_cnt && sk_cnt->defined() && sk_cnt->is_cuda() && sk_cnt->scalar_type() == torch::kInt32 &&
                     sk_cnt->is_contiguous() && sk_cnt->numel() >= tiles && sk_cnt->device() == a.device(),
                 "gemm64: stream-K needs sk_cnt, int32 zeros [>= tiles] on the operands' device");
-    const int base = (int)(tile & ~(64 | 128));
-    const int tb = base > 4 && base <= 8 ? base - 4 : base;
-    const int64_t bm = (tb == 3 || tb == 4 || tb == 12) ? 128 : 256;
-    const int64_t bn = (tb == 11 || tb == 12) ? 192 : ((tb == 2 || tb == 3) ? 128 : 256);
-    ws = torch::empty({(int64_t)grid * 2 * bm * bn}, a.options().dtype(torch::kFloat32));
+    ws = torch::empty({wsf}, a.options().dtype(torch::kFloat32));
     skw = ws.data_ptr<float>();
     skc = sk_cnt->data_ptr<int>();
   }
@@ -308,7 +305,7 @@ void dta_register_ext(pybind11::module_& m) {
         py::arg("stream") = -1, py::arg("alpha_dev") = py::none(), py::arg("sk_cnt") = py::none());
   m.def("gemm64_sk_plan", [](int M, int N, int K, int tile) {
           int grid = 0, span = 0;
-          const int tiles = dta_gemm_k64_sk_plan(M, N, K, tile, &grid, &span);
+          const int tiles = dta_gemm_k64_sk_plan(M, N, K, tile, &grid, &span, nullptr);
           return std::vector<int>{tiles, grid, span};
         }, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile"));
   m.def("gemm64_tile", [](int M, int N, int K, int tile) { return dta_gemm_k64_tile(M, N, K, tile); },

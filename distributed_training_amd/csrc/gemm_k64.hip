@@ -916,8 +916,9 @@ int dta_gemm_k64_tile(int M, int N, int K, int tile) {
 
 // Stream-K plan of a tile id with the kSK bit: the grid (resident workgroups of the tile on this device, or
 // fewer where a run would drop below half a tile's K-tiles) and each workgroup's run of K-tile units; returns
-// the tile count (the arrival counters the call needs), 0 if the id is not a stream-K id for the shape
-int dta_gemm_k64_sk_plan(int M, int N, int K, int tile, int* grid, int* span) {
+// the tile count (the arrival counters the call needs), 0 if the id is not a stream-K id for the shape;
+// ws_floats: the fp32 slab space the launch needs (grid x 2 slabs of BM x BN)
+int dta_gemm_k64_sk_plan(int M, int N, int K, int tile, int* grid, int* span, int64_t* ws_floats) {
   if (!(tile & k64::kSK) || !dta_gemm_k64_tile(M, N, K, tile)) return 0;
   const int base = tile & ~(k64::kSK | k64::kNoStg);
   const int tb = base > k64::kTiles && base <= 2 * k64::kTiles ? base - k64::kTiles : base;
@@ -935,6 +936,7 @@ int dta_gemm_k64_sk_plan(int M, int N, int K, int tile, int* grid, int* span) {
   sp = std::max<int64_t>(sp, (nk + 1) / 2);  // at most three workgroups share a tile
   *span = (int)sp;
   *grid = (int)((units + sp - 1) / sp);
+  if (ws_floats) *ws_floats = (int64_t)*grid * 2 * k64::tile_bm(tb) * k64::tile_bn(tb);
   return tiles;
 }
 
@@ -950,7 +952,8 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
                         const float* alpha_dev, float* sk_ws, int* sk_cnt) {
   int sk_grid = 0, sk_span = 0;
   if (tile & k64::kSK) {
-    if (!dta_gemm_k64_sk_plan(M, N, K, tile, &sk_grid, &sk_span) || !sk_ws || !sk_cnt || epi == k64::EPI_DSWIGLU)
+    if (!dta_gemm_k64_sk_plan(M, N, K, tile, &sk_grid, &sk_span, nullptr) || !sk_ws || !sk_cnt ||
+        epi == k64::EPI_DSWIGLU)
       return hipErrorInvalidValue;
   }
   tile = dta_gemm_k64_tile(M, N, K, tile);
