@@ -349,6 +349,31 @@ def _gfx950() -> bool:
         return False
 
 
+# ---- the library GEMMs' own solution choice: PyTorch TunableOp results measured on MI355X
+# (ops/tunableop_mi355x.csv; hipBLASLt / rocBLAS solutions searched per shape, scripts/gpu_r5v.sh) for the GEMMs the
+# table leaves on the library -- GPT-2's c_fc forward, LM-head forward and input gradient take solutions other
+# than the heuristic's: step 10.30 / 10.29 -> 10.17 / 10.22 ms same box (profiles/tunableop_ab_r5v.jsonl).  Read
+# only (tuning off, nothing written); a file whose validators (torch / HIP / hipBLASLt / rocBLAS versions, arch)
+# do not match this install is ignored by torch.  DTA_TUNABLEOP=0, or PYTORCH_TUNABLEOP_* set by the user: left
+# alone.
+TUNABLEOP_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_mi355x.csv")
+_TUNABLEOP_SET = [False]
+
+
+def _library_tuning() -> None:
+    if _TUNABLEOP_SET[0]:
+        return
+    _TUNABLEOP_SET[0] = True
+    if (os.environ.get("DTA_TUNABLEOP", "1") == "0" or any(k.startswith("PYTORCH_TUNABLEOP") for k in os.environ)
+            or not os.path.exists(TUNABLEOP_PATH) or not torch.cuda.is_available()):
+        return
+    import torch.cuda.tunable as tunable
+
+    tunable.set_filename(TUNABLEOP_PATH, False)
+    tunable.tuning_enable(False)
+    tunable.enable(True)
+
+
 def gemm_table() -> Dict[tuple, int]:
     """The tracked table as {(kind, M, N, K): impl id} ({} off gfx950 or with DTA_GEMM_TABLE=0).  An entry's
     ``in_step_pick`` (with its ``in_step_evidence``: same-box step A/B runs) overrides the isolated-timing
@@ -359,6 +384,7 @@ def gemm_table() -> Dict[tuple, int]:
         if os.environ.get("DTA_GEMM_TABLE", "1") != "0" and os.path.exists(TABLE_PATH) and _gfx950():
             import json
 
+            _library_tuning()
             with open(TABLE_PATH) as f:
                 for k, v in json.load(f)["entries"].items():
                     kind, dims = k.rsplit(" ", 1)
