@@ -7,6 +7,7 @@
 //   for d in 0 1 2; do hipcc -O3 --offload-arch=gfx950 -DDTA_K64_EPI_DIAG=$d -I distributed_training_amd/csrc \
 //       scripts/k64_epi_diag.hip -o /tmp/k64_epi_$d; done; /tmp/k64_epi_0
 #include "../distributed_training_amd/csrc/gemm_k64.hip"
+#include "../distributed_training_amd/csrc/gemm_k64_sk.hip"
 
 #include <algorithm>
 #include <cstdio>

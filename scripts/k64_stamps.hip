@@ -6,6 +6,7 @@
 //   hipcc -O3 --offload-arch=gfx950 -DDTA_K64_STAMP -I distributed_training_amd/csrc \
 //         scripts/k64_stamps.hip -o /tmp/k64_stamps && /tmp/k64_stamps M N K layout tile
 #include "../distributed_training_amd/csrc/gemm_k64.hip"
+#include "../distributed_training_amd/csrc/gemm_k64_sk.hip"
 
 #include <cstdio>
 #include <vector>
