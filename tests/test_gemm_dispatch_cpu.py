@@ -107,3 +107,25 @@ def test_in_step_override_wins(monkeypatch, tmp_path):
     table = lm.gemm_table()
     assert table[("dgrad", 8192, 768, 3072)] == lm.K64 + 6
     assert table[("fwd", 64, 64, 64)] == 0
+
+
+def test_candidate_sets_respect_layouts_and_stream_k_rules():
+    """The 192-wide tiles are offered for K-major operands only; stream-K forms only where the plain tile's
+    last round leaves >= 10 % of the chip idle and the reduction is deep (K >= 8192), never for the TT layout;
+    the stream-K plan keeps every tile within three workgroups (span >= ceil(nk / 2)) and covers all units."""
+    from distributed_training_amd.ops import native
+
+    C = native()
+    names = lambda *a: {lm._impl_name(c) for c in lm.gemm_candidates(*a)}  # noqa: E731
+    nt = names(8192, 2304, 768, False, False)
+    assert {"k64/t11", "k64/t12"} <= nt and not any(n.endswith("sk") for n in nt)  # K = 768: no stream-K
+    assert not ({"k64/t11", "k64/t12"} & names(8192, 2304, 768, False, True))
+    deep = names(768, 3072, 8192, True, True)  # GPT-2 weight gradient: 36 tiles of 256 x 256
+    assert "k64/t5sk" in deep and not any(n.startswith("k64/t11") or n.startswith("k64/t12") for n in deep)
+    assert not any(n.endswith("sk") for n in names(768, 3072, 8192, True, False))  # TT: no stream-K
+    assert not any(n.endswith("sk") for n in names(8192, 4096, 4096, False, False))  # 512 tiles: 2 full rounds
+    for M, N, K, t in ((8192, 768, 3072, 6), (6144, 4096, 8192, 5), (8192, 768, 50304 // 64 * 64, 5), (256, 384, 448, 12)):
+        tiles, grid, span = C.gemm64_sk_plan(M, N, K, t | lm.SK_BIT)
+        nk = K // 64
+        assert tiles > 0 and span >= (nk + 1) // 2 and grid * span >= tiles * nk > (grid - 1) * span, (M, N, K, t)
+    assert C.gemm64_sk_plan(8192, 768, 3072, 3 | lm.SK_BIT)[0] == 0  # four-phase / non-stream-K base tile
