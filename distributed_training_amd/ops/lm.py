@@ -413,14 +413,27 @@ K64_TILES_KMAJOR = (11, 12)
 _PREFER_DTA = 1.0
 
 
-def gemm_candidates(M: int, N: int, K: int, a_t: bool = False, b_t: bool = False, sk: bool = True) -> list:
+def gemm_candidates(M: int, N: int, K: int, a_t: bool = False, b_t: bool = False, sk: bool = True,
+                    big: bool = False) -> list:
     """Hand-written GEMM implementations that cover an M x N x K problem in the given operand layout
-    (ids as in _GEMM_CHOICE; ``sk``: with the stream-K forms where they can help).  Memoised per shape."""
-    key = (M, N, K, bool(a_t), bool(b_t), bool(sk))
+    (ids as in _GEMM_CHOICE; ``sk``: with the stream-K forms where they can help; ``big``: an operand spans
+    2 GiB or more, past the buffer descriptors' 32-bit offsets -- the tiles that DMA only through descriptors,
+    the 192-wide, the stream-K forms and W4, are left out).  Memoised per shape."""
+    key = (M, N, K, bool(a_t), bool(b_t), bool(sk), bool(big))
     c = _CANDS.get(key)
     if c is None:
-        c = _CANDS[key] = _gemm_candidates(M, N, K, a_t, b_t, sk)
+        c = _CANDS[key] = _gemm_candidates(M, N, K, a_t, b_t, sk and not big)
+        if big:  # (csrc/gemm_w4.hip too: descriptor DMA only)
+            c = _CANDS[key] = [x for x in c if x - K64 not in K64_TILES_KMAJOR + (10,)]
     return c
+
+
+def _big(*ts: Optional[torch.Tensor]) -> bool:
+    """Some operand's bytes reach past 2 GiB from its base (csrc/gemm_k64.hip: descriptor DMA off)."""
+    for t in ts:
+        if t is not None and t.numel() and 2 * ((t.shape[0] - 1) * t.stride(0) + t.shape[-1]) >= 0x7FFFFFFF:
+            return True
+    return False
 
 
 _CANDS: Dict[tuple, list] = {}
@@ -592,7 +605,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
     impl = 0
     if _gemm_ok(a, b, bias, out):
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in gemm_candidates(M, N, K, a_t, b_t):
+        for t in gemm_candidates(M, N, K, a_t, b_t, big=_big(a, b)):
             cands[t] = (lambda t=t: _run_gemm(t, a, b, a_t, b_t, out, alpha, bias, scale_dev))
         impl = _pick(kind + ("b" if bias is not None else ""), M, N, K, cands)
     if impl:
@@ -623,7 +636,7 @@ def gemm_gelu_dual(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor])
     impl = 0
     if _gemm_ok(x2, w, b) and N % 8 == 0:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for c in gemm_candidates(M, N, K):
+        for c in gemm_candidates(M, N, K, big=_big(x2, w)):
             cands[c] = (lambda t=c - K64: run_k64(t))
         # the dual store must win by 15 %: its two output streams cost more inside the step than in
         # the back-to-back timing (GPT-2 fc: per-fragment 85.8 us in-step vs 69-76 timed, staged 78-82
@@ -908,7 +921,7 @@ def _dgelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, h2: torch.Tensor) -> torch.
     impl = 0
     if ok:
         cands: Dict[int, Callable[[], object]] = {0: run_torch}
-        for t in gemm_candidates(M, N, K, False, True):
+        for t in gemm_candidates(M, N, K, False, True, big=_big(dy2, w)):
             cands[t] = (lambda t=t: run(t))
         impl = _pick("dgelu", M, N, K, cands)
     if impl:

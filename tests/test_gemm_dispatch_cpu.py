@@ -129,3 +129,15 @@ def test_candidate_sets_respect_layouts_and_stream_k_rules():
         nk = K // 64
         assert tiles > 0 and span >= (nk + 1) // 2 and grid * span >= tiles * nk > (grid - 1) * span, (M, N, K, t)
     assert C.gemm64_sk_plan(8192, 768, 3072, 3 | lm.SK_BIT)[0] == 0  # four-phase / non-stream-K base tile
+
+
+def test_big_operands_leave_out_descriptor_only_tiles():
+    """An operand spanning >= 2 GiB (GPT-2 at B = 32: the [32768, 50304] logit gradient) takes no candidate that
+    DMAs only through 32-bit buffer descriptors (192-wide, stream-K, W4): they would refuse the launch."""
+    base = {lm._impl_name(c) for c in lm.gemm_candidates(32768, 768, 50304, False, True)}
+    big = {lm._impl_name(c) for c in lm.gemm_candidates(32768, 768, 50304, False, True, big=True)}
+    assert any(n.endswith("sk") for n in base) and "k64/t10" in base
+    assert big and not any(n.endswith("sk") or n in ("k64/t10", "k64/t11", "k64/t12") for n in big)
+    x = torch.empty(0, dtype=torch.bfloat16)
+    assert not lm._big(x) and lm._big(torch.empty(32768, 50304, dtype=torch.bfloat16, device="meta"))
+    assert not lm._big(torch.empty(8192, 50304, dtype=torch.bfloat16, device="meta"))
