@@ -36,14 +36,15 @@ def _r(*shape, scale=1.0):
     return ((torch.rand(*shape, device=DEV) * 2 - 1) * scale).to(torch.bfloat16)
 
 
-def collect_keys():
+def collect_keys(gpt2_batches=(8,)):
     from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
     from distributed_training_amd.models.llama import Llama, LlamaConfig
 
     os.environ["DTA_GEMM"] = "torch"
     keys = set()
-    for build, B, S in ((lambda: GPT2(GPT2Config(n_layer=1)), 8, 1024),
-                        (lambda: Llama(LlamaConfig(n_layer=1)), 1, 8192)):
+    runs = [(lambda: GPT2(GPT2Config(n_layer=1)), b, 1024) for b in gpt2_batches]
+    runs.append((lambda: Llama(LlamaConfig(n_layer=1)), 1, 8192))
+    for build, B, S in runs:
         torch.manual_seed(0)
         m = build().to(DEV).to(torch.bfloat16)
         idx = torch.randint(0, m.vocab_size, (B, S + 1), device=DEV)
@@ -109,11 +110,17 @@ def main():
     ap.add_argument("--check", default="")
     ap.add_argument("--only", default="", help="comma-separated kinds to measure (default: every key)")
     ap.add_argument("--merge", default="", help="table whose entries the measured ones are added to / replace")
+    ap.add_argument("--gpt2-batches", default="8", help="GPT-2 batch sizes (x 1024 tokens) whose GEMM keys to collect")
+    ap.add_argument("--new-only", action="store_true", help="measure only keys missing from the --merge table")
     args = ap.parse_args()
-    keys = collect_keys()
+    keys = collect_keys(tuple(int(b) for b in args.gpt2_batches.split(",")))
     if args.only:
         kinds = set(args.only.split(","))
         keys = [k for k in keys if k[0] in kinds]
+    if args.new_only and args.merge:
+        with open(args.merge) as f:
+            have = json.load(f)["entries"]
+        keys = [k for k in keys if f"{k[0]} {k[1]}x{k[2]}x{k[3]}" not in have]
     print(f"[gemm_table] {len(keys)} keys", flush=True)
     entries = measure(keys)
     if args.merge:
