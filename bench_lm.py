@@ -196,10 +196,14 @@ def main() -> None:
         prof.pop()
 
     graphed = None
-    # DDP: any world size (its bucket collectives are captured too); FSDP: one rank, where every unit
-    # aliases its shard (nothing is freed or re-allocated between units, so the step is capturable)
-    graph_ok = args.strategy == "ddp" or (ws == 1 and getattr(wrapped, "graph_capturable", lambda: False)())
-    if args.impl == "native" and graph_ok and not args.no_graph:
+    policy = (False, "torch baseline")
+    if args.impl == "native":
+        # the Trainer's policy (engine/step_graph.py capture_policy): engine state capturable, and at
+        # world size > 1 every collective on the IPC data plane (RCCL in a graph: DTA_GRAPH_RCCL=1)
+        from distributed_training_amd.engine.step_graph import capture_policy
+
+        policy = capture_policy(wrapped)
+    if args.impl == "native" and policy[0] and not args.no_graph:
         # the whole step (zero_grad, forward, backward with the bucket hooks, AdamW) as ONE hipGraph;
         # its construction runs 3 eager warm-up steps and the capture (untimed, before the warm-up below)
         from distributed_training_amd.engine.step_graph import GraphedStep
@@ -238,8 +242,14 @@ def main() -> None:
         step()
     barrier()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     for _ in range(args.steps):
         step()
+    # host cost of the step: the wall time until the last step is ENQUEUED (no sync inside the step, so
+    # this is below the GPU time unless the host is the bottleneck) and the CPU time of every thread
+    # (autograd's device thread included) -- eager vs graphed (--no-graph) is this difference
+    t_enq = time.perf_counter() - t0
+    c_enq = time.process_time() - c0
     barrier()
     el = time.perf_counter() - t0
     peak_mem = torch.cuda.max_memory_allocated(dev)
@@ -274,6 +284,8 @@ def main() -> None:
            "higher_is_better": True, "scaling": "weak", "dtype": "bf16", "data": "synthetic tokens",
            "samples_per_s": round(args.batch * ws * args.steps / el, 2), "mfu": round(mfu, 4),
            "params_M": round(n_params / 1e6, 1), "peak_mem_GB": round(peak_mem / 1e9, 2),
+           "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
+           "host_cpu_ms_per_step": round(c_enq / args.steps * 1e3, 3),
            "final_loss": float(state["loss"].item()),
            "fsdp_units": (len(wrapped.units) if args.impl == "native" and args.strategy == "fsdp" else None),
            "comm": ("none: one rank (DDP skips the all-reduce, FSDP runs NO_SHARD)" if ws == 1 else
@@ -287,6 +299,11 @@ def main() -> None:
         # which implementation each projection GEMM shape runs (measured per shape, DTA_GEMM=auto)
         out["optimizer_in_backward"] = bool(overlap_opt)
         out["step_graph"] = graphed is not None
+        out["capture_policy"] = policy[1]
+        if args.strategy == "ddp":
+            out["bucket_caps"] = {"first_MiB": round(wrapped.bucket_bytes[0] / 2 ** 20, 2),
+                                  "cap_MiB": round(wrapped.bucket_bytes[1] / 2 ** 20, 2),
+                                  "buckets": len(wrapped.buckets), "source": wrapped.bucket_caps_source}
         out["head_ce_chunk"] = _lm.HEAD_CE_CHUNK
         routes = getattr(getattr(wrapped, "comm", None), "routes", None)
         if routes is not None:

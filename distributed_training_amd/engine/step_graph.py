@@ -17,11 +17,16 @@ What makes the native step capturable:
   the same overwrites), and the fused optimizers keep their step count on the device;
 * the per-shape GEMM choice (``ops/lm.py`` ``_pick``, which times candidates with a
   synchronize) is made during the eager warm-up steps, before capture.
-The bucket collectives of the DDP engine are captured too (RCCL and the IPC push
-kernels are graph-capturable; tests/test_ipc_gpu.py replays a captured multi-rank
-step against the eager one).  The FSDP engine at one rank too (every unit aliases its
-shard: ``FullyShardedDataParallel.graph_capturable``); at several ranks it frees and
-re-allocates unit storage between units, so it keeps the eager step.
+The collectives of the step are captured too.  Whether a step may be captured is ONE
+policy, :func:`capture_policy`, shared by the Trainer (engine/trainer.py) and
+``bench_lm.py``: the engine's host state must be capturable (DDP: always on the GPU;
+FSDP: at one rank every unit aliases its shard, at several every unit gathers into a
+fixed buffer -- parallel/fsdp.py ``_GatherRing``), and at world size > 1 every
+collective of the step must route to the IPC push data plane, whose kernels keep their
+epoch counters on the device (graph replays advance them) and whose captured multi-rank
+DDP and FSDP replays are tested bit-identical to the eager steps (tests/test_ipc_gpu.py).
+A collective routed to RCCL keeps the step eager unless ``DTA_GRAPH_RCCL=1`` opts in:
+RCCL inside a replayed graph at world size > 1 has not been run on a multi-GPU node.
 
 Host logic that the replay skips is redone around it:
 * the communicator's error poll of the engine's end-of-backward finalize (a peer
@@ -39,11 +44,62 @@ batch into them (device-to-device) before the replay.
 from __future__ import annotations
 
 import logging
-from typing import Any, Callable, Optional, Sequence
+import os
+from typing import Any, Callable, Optional, Sequence, Tuple
 
 import torch
 
 logger = logging.getLogger(__name__)
+
+
+def _plane(comm: Any, op: str, dtype: torch.dtype, nbytes: int) -> str:
+    """The data plane a collective goes to: ``"ipc"`` (capturable push kernels), ``"rccl"``, or
+    ``"host"`` (torch / gloo process-group calls: not capturable)."""
+    from ..parallel.comm import RcclComm
+    from ..parallel.ipc import IpcComm
+    from ..parallel.routed import RoutedComm
+
+    if isinstance(comm, RoutedComm):
+        return _plane(comm.fast if comm.route_of(op, dtype, nbytes) == "fast" else comm.primary, op, dtype, nbytes)
+    if isinstance(comm, IpcComm):
+        return "ipc"
+    if isinstance(comm, RcclComm):
+        return "rccl"
+    return "host"
+
+
+def capture_policy(engine: Any) -> Tuple[bool, str]:
+    """May ``engine``'s whole training step be captured as one hipGraph?  ``(ok, reason)``.
+
+    * the engine's per-step host state must allow it (``graph_capturable()``: DDP on the GPU; FSDP
+      aliasing its shards at one rank or gathering into fixed buffers at several);
+    * at one rank no collective runs;
+    * at several, every collective the step issues (``step_messages()``) must route to the IPC data
+      plane -- or to RCCL with ``DTA_GRAPH_RCCL=1`` (RCCL replayed inside a graph at world size > 1 is
+      not verified on a multi-GPU node, so it is an explicit opt-in); process-group (gloo / torch)
+      calls never are.
+    Reference: the eager step of src/distributed_trainer.py:160-165 under the DDP / FSDP wraps of
+    src/dist_strategy/ddp_strategy.py:18-21 and fsdp_strategy.py:20-26."""
+    cap = getattr(engine, "graph_capturable", None)
+    if cap is None or not cap():
+        return False, "engine state not capturable"
+    ws = int(getattr(engine, "world_size", 1))
+    if ws <= 1:
+        return True, "one rank: no collective"
+    msgs = getattr(engine, "step_messages", None)
+    comm = getattr(engine, "comm", None)
+    if msgs is None or comm is None:
+        return False, "collectives unknown"
+    planes = {_plane(comm, op, dt, n) for op, dt, n in msgs()}
+    if getattr(engine, "rep", None) is not None:
+        planes.add(_plane(engine.rep, "all_reduce", torch.float32, 1 << 30))
+    if planes <= {"ipc"}:
+        return True, "every collective on the IPC data plane"
+    if "host" in planes:
+        return False, "collectives on the process group (not capturable)"
+    if os.environ.get("DTA_GRAPH_RCCL", "0") == "1":
+        return True, "RCCL collectives captured (DTA_GRAPH_RCCL=1)"
+    return False, "collectives routed to RCCL (set DTA_GRAPH_RCCL=1 to capture them)"
 
 
 def _agree_all_ok(engine: Any, ok: bool, device: torch.device) -> bool:

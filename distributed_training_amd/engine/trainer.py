@@ -209,39 +209,20 @@ class Trainer:
     # ------------------------------------------------------------------ loop
     def _graph_eligible(self, source: torch.Tensor, targets: torch.Tensor) -> bool:
         from ..ops.optim import FusedAdamW, FusedSGD
+        from .step_graph import capture_policy
 
         c = self.config
         # only the fused optimizers keep their step count on the device (torch's AdamW keeps it on the
         # host and cannot be captured)
-        capturable = (isinstance(self._strategy, DDPStrategy) and hasattr(self.model, "flat")) or \
-            getattr(self.model, "graph_capturable", lambda: False)()
-        return (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip and capturable
+        if not (c.step_graph and self.env.is_gpu and source.is_cuda and not c.grad_clip
                 and isinstance(self.optimizer, (FusedSGD, FusedAdamW))
-                and not c.desync_check_every and getattr(self, "_graphed", None) is not False
-                and not self._buckets_on_rccl())
-
-    def _buckets_on_rccl(self) -> bool:
-        """A multi-rank DDP step whose bucket all-reduces (any of them) go to RCCL is not captured:
-        replaying RCCL inside a hipGraph at world size > 1 has not been verified on a multi-GPU
-        node (the multi-rank replay parity test runs the IPC data plane on a shared GPU,
-        tests/test_ipc_gpu.py) -- the eager step is used there until it is."""
-        if self.env.world_size <= 1:
+                and not c.desync_check_every and getattr(self, "_graphed", None) is not False):
             return False
-        from ..parallel.comm import RcclComm
-        from ..parallel.routed import RoutedComm
-
-        comm = getattr(self.model, "comm", None)
-        if isinstance(comm, RcclComm):
-            return True
-        if isinstance(comm, RoutedComm):
-            fl = getattr(self.model, "flat", None)
-            buckets = getattr(self.model, "buckets", None)
-            if fl is None or buckets is None:
-                return True
-            esz = fl.grad.element_size()
-            return any(comm.route_of("all_reduce", fl.grad.dtype, (b.end - b.start) * esz) == "primary"
-                       for b in buckets)
-        return False
+        if getattr(self, "_policy", None) is None:
+            self._policy = capture_policy(self.model)  # (the one policy bench_lm.py applies too)
+            if not self._policy[0]:
+                logger.info(f"step graph not used: {self._policy[1]}")
+        return self._policy[0]
 
     def _run_batch(self, source: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         if self._graph_eligible(source, targets):

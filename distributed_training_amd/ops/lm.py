@@ -155,7 +155,8 @@ _NORM_DEFER: list = []
 
 
 def _defer_ok(p: Optional[torch.Tensor]) -> bool:
-    return p is None or getattr(p, "_dta_gdest", None) is None or bool(getattr(p, "_dta_defer_ok", False))
+    gd = getattr(p, "_dta_gdest", None) if p is not None else None
+    return gd is None or bool(getattr(gd, "defer_ok", False))
 
 
 def _norm_backward(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
@@ -165,8 +166,11 @@ def _norm_backward(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, mean: t
     available and deferral on, the gamma / beta column sums are queued for the batched flush."""
     cw = _grad_dest(pw) if need_w else None
     cb = _grad_dest(pb) if (not rms and need_b) else None
+    # deferred only for a gamma (beta) used ONCE in this backward (ADVICE r5): a second use would get no
+    # slice (_grad_dest) and autograd would sum the returned slice before the batched flush wrote it
     if (_group_threshold() and os.environ.get("DTA_NORM_DEFER", "1") != "0" and cw is not None
-            and (rms or not need_b or cb is not None) and _defer_ok(pw)
+            and (rms or not need_b or cb is not None) and _defer_ok(pw) and _single_use(pw)
+            and (rms or not need_b or _single_use(pb))
             and (rms or _defer_ok(pb)) and cw.is_contiguous() and (cb is None or cb.is_contiguous())):
         dx, dwp, dbp = native().norm_bwd(dy2, x2, w, mean, rstd, rms, -1, dres, None, None, True)
         _NORM_DEFER.append((dwp, cw.view(-1)))  # (aliases, never the tensors returned to autograd)
@@ -178,6 +182,14 @@ def _norm_backward(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, mean: t
     return tuple(native().norm_bwd(dy2, x2, w, mean, rstd, rms, -1, dres, cw, cb))
 
 
+def _count_norm_uses(ctx: Any, w: torch.Tensor, b: Optional[torch.Tensor], iw: int) -> None:
+    """A norm's gamma / beta count as weight uses (``_single_use``) like a Linear's weight."""
+    if ctx.needs_input_grad[iw]:
+        _count_use(w)
+    if b is not None and ctx.needs_input_grad[iw + 1]:
+        _count_use(b)
+
+
 class _Norm(Function):
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, rms: bool, eps: float) -> torch.Tensor:
@@ -187,6 +199,7 @@ class _Norm(Function):
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.rms, ctx.shape = rms, shape
         ctx.params = (w, b)  # their .grad decides a direct write into the flat gradient (_grad_dest)
+        _count_norm_uses(ctx, w, b, 1)
         return y.view(shape)
 
     @staticmethod
@@ -212,6 +225,7 @@ class _AddNorm(Function):
         ctx.save_for_backward(xsum, w, mean, rstd)
         ctx.rms, ctx.shape = rms, shape
         ctx.params = (w, b)
+        _count_norm_uses(ctx, w, b, 2)
         # an unused output (the final norm's residual stream) gets no zero-filled gradient: no
         # [tokens, C] fill and no zero residual read by the norm-backward kernel
         ctx.set_materialize_grads(False)
@@ -350,7 +364,7 @@ def _gfx950() -> bool:
 
 
 # ---- the library GEMMs' own solution choice: PyTorch TunableOp results measured on MI355X
-# (ops/tunableop_mi355x.csv; hipBLASLt / rocBLAS solutions searched per shape, scripts/gpu_r5v.sh) for the GEMMs the
+# (ops/tunableop_mi355x.csv; hipBLASLt / rocBLAS solutions searched per shape: profiles/tunableop_ab_r5v.jsonl) for the GEMMs the
 # table leaves on the library -- GPT-2's c_fc forward, LM-head forward and input gradient take solutions other
 # than the heuristic's: step 10.30 / 10.29 -> 10.17 / 10.22 ms same box (profiles/tunableop_ab_r5v.jsonl).  Read
 # only (tuning off, nothing written); a file whose validators (torch / HIP / hipBLASLt / rocBLAS versions, arch)
@@ -544,6 +558,21 @@ def _sk_cnt(dev: torch.device) -> Optional[torch.Tensor]:
     return c
 
 
+_NUM_CUS: Dict[int, int] = {}
+
+
+def _num_cus() -> int:
+    """Compute units of the current device (256 on a whole MI355X; fewer in a CU-partition mode) --
+    what ``dta_gemm_k64_sk_plan`` sizes the stream-K grid from."""
+    if not torch.cuda.is_available():  # (CPU: the dispatch rules are unit-tested with a stand-in kernel library)
+        return 256
+    idx = torch.cuda.current_device()
+    n = _NUM_CUS.get(idx)
+    if n is None:
+        n = _NUM_CUS[idx] = int(torch.cuda.get_device_properties(idx).multi_processor_count)
+    return n
+
+
 def _sk_useful(M: int, N: int, K: int, t: int) -> bool:
     """A stream-K candidate where the plain tile's last round would leave >= 10 % of the slots idle and the
     reduction is deep (K >= 8192): every cut tile costs an fp32 slab per part (128-256 KB, written and read
@@ -555,7 +584,7 @@ def _sk_useful(M: int, N: int, K: int, t: int) -> bool:
     tiles, grid, _span = native().gemm64_sk_plan(M, N, K, t | SK_BIT)
     if tiles <= 0 or tiles > _SK_CNT_LEN:
         return False
-    slots = 256 * (2 if t in (7, 12) else 1)
+    slots = _num_cus() * (2 if t in (7, 12) else 1)  # (the kernel's plan sizes its grid from the same count)
     rounds = -(-tiles // slots)
     return tiles < 0.9 * rounds * slots
 
@@ -772,7 +801,7 @@ def _queue_end_join() -> None:
 # token reduction -- no split, no slabs, bias gradients from the same MFMA pipe
 # (csrc/gemm_k64.hip gemm_k64_group_kernel).  The queue is flushed before every DDP bucket
 # launch and at the end of the backward (same stream: no further synchronisation); under the
-# FSDP engine (unit pieces, ``_dta_defer_ok``) a unit's reduce-scatter waits for the flush that
+# FSDP engine (unit pieces, ``_Piece.defer_ok``) a unit's reduce-scatter waits for the flush that
 # writes its pieces (parallel/fsdp.py ``_launch_waiting``).
 _DEFER: list = []
 _DEFER_TILES = [0]
@@ -839,7 +868,7 @@ def _weight_grad(dy2: torch.Tensor, x2: torch.Tensor, with_bias: bool = False, w
     if thr and M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1 \
             and (M // 256) * (N // 256) <= _DEFER_MAX_TILES and x2.stride(0) % 8 == 0 \
             and cw is not None and (cb is not None or not with_bias) \
-            and (getattr(w, "_dta_gdest", None) is None or getattr(w, "_dta_defer_ok", False)) \
+            and _defer_ok(w) \
             and _single_use(w) and cw.stride(0) % 8 == 0 \
             and cw.data_ptr() % 16 == 0 and (cb is None or cb.data_ptr() % 16 == 0):
         # deferred: computed by a grouped launch at the next flush (see _DEFER).  The queue
@@ -1219,14 +1248,10 @@ def _claimed_slice(p: torch.Tensor) -> Optional[torch.Tensor]:
     wrote its gradient there (:func:`_grad_dest` claimed it; autograd has not accumulated
     yet): a further contribution can be added into it in place."""
     gd = getattr(p, "_dta_gdest", None)
-    if gd is not None:  # FSDP unit view: its piece of the unit's gradient buffer (parallel/fsdp.py piece_dest)
-        unit = getattr(getattr(gd, "func", None), "__self__", None)
-        e = getattr(gd, "args", (None,))[0]
-        if unit is None or not getattr(unit, "in_backward", False) or e not in getattr(unit, "_claimed", ()):
-            return None
-        o, n = unit.offsets[e], unit.numels[e]
-        d = unit.grad_buffer()[o:o + n].view(unit.shapes[e])
-        return d if d.dtype == p.dtype else None
+    if gd is not None:  # FSDP unit view: its piece of the unit's gradient buffer (parallel/fsdp.py _Piece)
+        cs = getattr(gd, "claimed_slice", None)
+        d = cs() if cs is not None else None
+        return d if d is not None and d.dtype == p.dtype else None
     tag = getattr(p, "_dta_flat", None)
     if tag is None or p.grad is not None:
         return None
@@ -1368,12 +1393,17 @@ class _ChunkedLinearCrossEntropy(Function):
         if need_dw:
             # the weight gradient straight into the engine's gradient slice when it is final already in
             # the forward (DDP after zero_grad(set_to_none); FSDP at one rank): no [V, C] buffer of its own
-            f = getattr(w, "_dta_gdest_fwd", None)
-            dw = f() if f is not None else (_grad_dest(w) if getattr(w, "_dta_gdest", None) is None else None)
+            gd = getattr(w, "_dta_gdest", None)
+            f = getattr(w, "_dta_gdest_fwd", None) or getattr(gd, "forward_dest", None)
+            dw = f() if f is not None else (_grad_dest(w) if gd is None else None)
             dw_final = dw is not None
             if dw is None:
                 dw = torch.empty_like(w)
         C = native()
+        # (several blocks: dW accumulates in bf16 -- hipBLASLt's beta = 1 adds each block's fp32 product to the
+        # running sum and rounds once per block, so the result carries up to T / chunk bf16 roundings instead of
+        # one.  An fp32 [V, C] running sum would round once but costs 4 V C bytes -- at Llama-3 8B as much as the
+        # logits the row blocks save; the drift is bounded by test_chunked_head_ce_dw_drift_many_blocks.)
         for i, r0 in enumerate(range(0, T, chunk)):
             r1 = min(T, r0 + chunk)
             lg = buf[:r1 - r0]
@@ -1397,6 +1427,11 @@ class _ChunkedLinearCrossEntropy(Function):
 
     @staticmethod
     def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
+        if getattr(ctx, "consumed", False):
+            # the gradients were formed in the forward and handed over by the first backward
+            raise RuntimeError("the chunked LM head + CE (head_ce_chunk) supports one backward per forward "
+                               "(retain_graph=True and a second backward are not supported)")
+        ctx.consumed = True
         s = (g.float() / ctx.count).reshape(())
         dx, dw = ctx.dx, ctx.dw
         ctx.dx = ctx.dw = None

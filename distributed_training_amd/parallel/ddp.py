@@ -49,7 +49,7 @@ from torch.autograd import Variable
 
 from ..utils import profiling as prof
 from .comm import Communicator, TorchComm
-from .flat import FlatParamGroup, build_flat_group, plan_buckets, xgmi_bucket_caps
+from .flat import FlatParamGroup, bucket_caps_for, build_flat_group, plan_buckets
 
 logger = logging.getLogger(__name__)
 
@@ -76,10 +76,14 @@ class DistributedDataParallel(nn.Module):
         esize = torch.empty((), dtype=param_dtype).element_size()
         grad_bytes = sum(p.numel() for _, p in named) * esize
         if bucket_cap_mb in (None, "auto"):
-            first_b, cap_b = xgmi_bucket_caps(self.world_size, grad_bytes)
+            # measured: the α/β fit of the communicator's wrap-time all-reduce timings (RoutedComm),
+            # else the assumed xGMI constants (parallel/flat.py bucket_caps_for)
+            first_b, cap_b, self.bucket_caps_source = bucket_caps_for(self.comm, self.world_size, grad_bytes,
+                                                                      param_dtype)
         else:
             cap_b = int(float(bucket_cap_mb) * MiB)
             first_b = MiB  # torch's dist._DEFAULT_FIRST_BUCKET_BYTES (also for first_bucket_mb="auto")
+            self.bucket_caps_source = "configured"
         if first_bucket_mb not in (None, "auto"):
             first_b = int(float(first_bucket_mb) * MiB)
         self.bucket_bytes = (first_b, cap_b)
@@ -354,6 +358,17 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self.require_sync = old
+
+    def graph_capturable(self) -> bool:
+        """The engine's per-step host logic only enqueues work on persistent buffers (bucket slices of
+        the flat gradient, events), so the step can be captured as one hipGraph on the GPU -- whether
+        its collectives may be is engine/step_graph.py ``capture_policy``'s call."""
+        return bool(self.flat.grad.is_cuda)
+
+    def step_messages(self) -> List[Tuple[str, torch.dtype, int]]:
+        """The collectives one training step issues: ``(op, dtype, bytes)`` per bucket all-reduce."""
+        esz = self.flat.grad.element_size()
+        return [("all_reduce", self.flat.grad.dtype, (b.end - b.start) * esz) for b in self.buckets]
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         self.flat.zero_grad(set_to_none)

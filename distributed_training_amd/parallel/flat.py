@@ -19,6 +19,7 @@ Trainer wraps the model) -- keeps working.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -271,6 +272,55 @@ def xgmi_bucket_caps(world_size: int, grad_bytes: int, min_buckets: int = 6) -> 
     cap = int(min(64 * MiB, max(4 * MiB, cap)))
     first = max(1 * MiB, cap // 16)
     return first, cap
+
+
+def fit_alpha_beta(points: Sequence[Tuple[float, float]]) -> Optional[Tuple[float, float]]:
+    """Least-squares fit of ``t = alpha + S / beta`` over measured ``(S bytes, t seconds)`` points:
+    ``(alpha seconds, beta bytes/s of message size)``, or None when the points do not give a positive
+    slope (noise, too few sizes).  ``alpha`` is clamped at >= 0."""
+    pts = [(float(s), float(t)) for s, t in points if s > 0 and t > 0 and math.isfinite(t)]
+    if len({s for s, _ in pts}) < 2:
+        return None
+    n = len(pts)
+    ms = sum(s for s, _ in pts) / n
+    mt = sum(t for _, t in pts) / n
+    var = sum((s - ms) ** 2 for s, _ in pts)
+    slope = sum((s - ms) * (t - mt) for s, t in pts) / var
+    if slope <= 0:
+        return None
+    alpha = max(0.0, mt - slope * ms)
+    return alpha, 1.0 / slope
+
+
+def measured_bucket_caps(grad_bytes: int, alpha: float, beta: float, min_buckets: int = 6) -> Tuple[int, int]:
+    """(first_cap_bytes, cap_bytes) from a MEASURED all-reduce cost ``t(S) = alpha + S / beta`` (the
+    α/β fit of the routed communicator's wrap-time calibration, :meth:`.routed.RoutedComm.alpha_beta`):
+    the same rule as :func:`xgmi_bucket_caps` -- a steady bucket whose fixed cost is <= 10 % of its
+    transfer time (``S >= 10 alpha beta``), but >= ``min_buckets`` buckets per backward for overlap,
+    clamped to [4, 64] MiB; a first bucket of cap / 16 (>= 1 MiB)."""
+    MiB = 1 << 20
+    cap = min(10.0 * alpha * beta, grad_bytes / max(1, min_buckets))
+    cap = int(min(64 * MiB, max(4 * MiB, cap)))
+    first = max(1 * MiB, cap // 16)
+    return first, cap
+
+
+def bucket_caps_for(comm: Any, world_size: int, grad_bytes: int, dtype: Any) -> Tuple[int, int, str]:
+    """DDP's ``bucket_cap_mb="auto"``: measured caps when the communicator timed its all-reduce at wrap
+    (``alpha_beta``), else the assumed xGMI constants (the no-calibration fallback).  Returns
+    ``(first_cap_bytes, cap_bytes, source)``."""
+    ab = None
+    fn = getattr(comm, "alpha_beta", None) if world_size > 1 else None
+    if fn is not None:
+        try:
+            ab = fn("all_reduce", dtype)
+        except Exception:  # noqa: BLE001 - a communicator without usable timings: the model
+            ab = None
+    if ab is not None:
+        first, cap = measured_bucket_caps(grad_bytes, *ab)
+        return first, cap, f"measured: alpha {ab[0] * 1e6:.1f} us, beta {ab[1] / 1e9:.1f} GB/s"
+    first, cap = xgmi_bucket_caps(world_size, grad_bytes)
+    return first, cap, "xgmi model (assumed constants)"
 
 
 def build_flat_group(params_with_names: Sequence[Tuple[str, torch.nn.Parameter]], device: torch.device,

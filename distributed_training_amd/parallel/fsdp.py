@@ -39,7 +39,6 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
-import functools
 import os
 import logging
 from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Set, Tuple, Type, Union
@@ -110,17 +109,94 @@ class _SplitInto(torch.autograd.Function):
     def backward(ctx: Any, *grads: Any) -> Tuple[Optional[torch.Tensor], None]:
         u = ctx.unit
         dest = u.grad_buffer()
-        pos = 0
-        for size, g in zip(u._split_sizes, grads):
-            sl = dest[pos:pos + size]
+        base, es = dest.data_ptr(), dest.element_size()
+        # (host cost: a piece written in place -- the common case -- is recognised by its address,
+        # without building a slice of the buffer for it)
+        for pos, size, g in zip(u._split_offs, u._split_sizes, grads):
             if g is None:
-                sl.zero_()
-            elif g.data_ptr() != sl.data_ptr():
-                sl.copy_(g.reshape(-1))
-            pos += size
+                dest[pos:pos + size].zero_()
+            elif g.data_ptr() != base + pos * es:
+                dest[pos:pos + size].copy_(g.reshape(-1))
         # a fresh view (its own TensorImpl, referenced only here) so AccumulateGrad
         # adopts it as full.grad instead of cloning it
         return dest.view(-1), None
+
+
+class _Piece:
+    """Parameter ``e`` of a unit as the native ops see it (``view._dta_gdest``, ops/lm.py): called, the
+    slice of the unit's gradient buffer its backward may write (:meth:`_Unit.piece_dest`);
+    ``forward_dest()`` the same for an op that forms the gradient in its forward; ``defer_ok`` whether
+    its weight gradient may join a grouped launch.  One object per parameter, made once at wrap: the
+    per-forward view setup only attaches it (host cost of the eager step)."""
+
+    __slots__ = ("unit", "e")
+
+    def __init__(self, unit: "_Unit", e: int) -> None:
+        self.unit, self.e = unit, e
+
+    def __call__(self) -> Optional[torch.Tensor]:
+        return self.unit.piece_dest(self.e)
+
+    def forward_dest(self) -> Optional[torch.Tensor]:
+        return self.unit.piece_dest_forward(self.e)
+
+    @property
+    def defer_ok(self) -> bool:
+        return bool(self.unit.owner._defer_wgrad)
+
+    def claimed_slice(self) -> Optional[torch.Tensor]:
+        """This backward's slice of the parameter when another use already claimed (and wrote) it."""
+        u, e = self.unit, self.e
+        if not u.in_backward or e not in u._claimed:
+            return None
+        o, n = u.offsets[e], u.numels[e]
+        return u.grad_buffer()[o:o + n].view(u.shapes[e])
+
+
+class _GatherRing:
+    """Preallocated, FIXED gather buffers of the units at world size > 1 (capture-safe FULL_SHARD).
+
+    Instead of allocating a unit's full-parameter storage before its all-gather and freeing it after
+    use (storage ``resize_``: different addresses from step to step, allocator calls inside the step),
+    unit ``u`` gathers into slot ``pos(u) mod R`` of ``R`` buffers sized for the largest unit, where
+    ``pos`` is its place in the forward order.  In flight at once are the unit being computed and the
+    one prefetched (forward: next, backward: previous), and the output unit kept from the forward into
+    the backward: R = 3 slots always separate them.  The root unit (gathered through the whole
+    forward and backward) has a buffer of its own.  Slot reuse is ordered by the comm stream waiting on
+    the compute stream when the next occupant's all-gather is enqueued -- issued after every kernel
+    reading the previous occupant.  The addresses are the same every step, so the step (all-gathers and
+    reduce-scatters on the IPC data plane included) can be captured once and replayed as a hipGraph
+    (engine/step_graph.py).  Memory: R x the largest unit (Llama-3 8B at 8 ranks: 3 x 1.05 GB of bf16)."""
+
+    def __init__(self, owner: "FullyShardedDataParallel", slots: int) -> None:
+        self.owner = owner
+        self.n = max(2, int(slots))
+        units = [u for u in owner.units if not u.is_root]
+        mx = max((u.total for u in units), default=0)
+        dt, dev = owner.param_dtype, owner.device
+        self.bufs = [torch.empty(mx, dtype=dt, device=dev) for _ in range(self.n if units else 0)]
+        self.holder: List[Optional["_Unit"]] = [None] * len(self.bufs)
+        for u in owner.units:
+            u.ring = self
+            if u.is_root:
+                u.fixed = torch.empty(u.total, dtype=dt, device=dev)
+
+    def claim(self, u: "_Unit") -> torch.Tensor:
+        if u.fixed is not None:
+            return u.fixed
+        if u.slot is None:
+            order = self.owner._fwd_order
+            if u not in order:  # (a unit gathered outside the recorded forward: a buffer of its own)
+                u.fixed = torch.empty(u.total, dtype=self.owner.param_dtype, device=self.owner.device)
+                return u.fixed
+            u.slot = order.index(u) % self.n
+        k = u.slot
+        h = self.holder[k]
+        if h is not None and h is not u:
+            h.wait()  # (its gather is complete before the slot is rewritten; never pending here)
+            h.gathered = False
+        self.holder[k] = u
+        return self.bufs[k][:u.total]
 
 
 class _Unit:
@@ -152,6 +228,12 @@ class _Unit:
             pos = o + n
         if self.total > pos:
             self._split_sizes.append(self.total - pos)
+        self._split_offs = [sum(self._split_sizes[:i]) for i in range(len(self._split_sizes))]
+        self._pieces = [_Piece(self, e) for e in range(len(entries))]
+        self._targets: Optional[List[List[Tuple[Dict[str, Any], str]]]] = None  # set_views' attribute slots
+        self.ring: Optional[_GatherRing] = None  # fixed gather buffers (world size > 1, see _GatherRing)
+        self.slot: Optional[int] = None
+        self.fixed: Optional[torch.Tensor] = None
         dt = owner.param_dtype
         self.full = torch.zeros(self.total, dtype=dt, device=owner.device).requires_grad_(True)
         self._nbytes = self.full.untyped_storage().nbytes()
@@ -182,7 +264,7 @@ class _Unit:
             st.resize_(self._nbytes)
 
     def free(self) -> None:
-        if self.alias:  # the storage is the shard's: never released here
+        if self.alias or self.ring is not None:  # the shard's storage / a fixed buffer: never released here
             self.gathered = False
             return
         self.full.untyped_storage().resize_(0)
@@ -210,7 +292,12 @@ class _Unit:
                 self.full.data = src
             self.gathered = True
             return
-        self._alloc()
+        if self.ring is not None:
+            buf = self.ring.claim(self)
+            if self.full.data_ptr() != buf.data_ptr():
+                self.full.data = buf
+        else:
+            self._alloc()
         if self.owner.world_size == 1:  # (CPU offload at one rank) the shard is the whole unit
             self.full.data.copy_(self.shard_source())
             self.gathered = True
@@ -233,15 +320,30 @@ class _Unit:
         included), so backward builds the unit's flat gradient with a single
         concatenation -- per-slice views would each allocate a zero-filled
         full-size gradient and add it in (O(params x unit size) traffic)."""
-        aliases = self.owner._aliases
         pieces = _SplitInto.apply(self.full, self)
-        for e, ((mod, attr, name, _), k, shp) in enumerate(zip(self.entries, self._piece_index, self.shapes)):
+        targets = self._targets if self._targets is not None else self._build_targets()
+        for piece, k, shp, tg in zip(self._pieces, self._piece_index, self.shapes, targets):
             view = pieces[k].view(shp)
-            view._dta_gdest = functools.partial(self.piece_dest, e)
-            view._dta_gdest_fwd = functools.partial(self.piece_dest_forward, e)
-            view._dta_defer_ok = self.owner._defer_wgrad  # its weight gradient may join a grouped launch
-            for m2, a2, _ in aliases.get(name, [(mod, attr, name)]):  # tied weights: every owner
-                setattr(m2, a2, view)
+            view._dta_gdest = piece  # (ops/lm.py: its gradient slice, deferral -- see _Piece)
+            for d, a in tg:  # tied weights: every owner
+                d[a] = view
+
+    def _build_targets(self) -> List[List[Tuple[Dict[str, Any], str]]]:
+        """Where each parameter's view goes: the owning modules' instance dicts.  The wrap removed the
+        parameters from ``_parameters`` (they are plain tensor attributes since), so a direct
+        ``__dict__`` store is what ``nn.Module.__setattr__`` would do, at a fraction of its host cost
+        (it runs once per parameter per forward)."""
+        aliases = self.owner._aliases
+        out = []
+        for mod, attr, name, _ in self.entries:
+            tg = []
+            for m2, a2, _n in aliases.get(name, [(mod, attr, name)]):
+                if a2 in m2._parameters or a2 in m2._buffers or a2 in m2._modules:
+                    raise RuntimeError(f"FSDP: {name} is still registered on its module")
+                tg.append((m2.__dict__, a2))
+            out.append(tg)
+        self._targets = out
+        return out
 
     # ---------------------------------------------------------- gradient destination
     def grad_buffer(self) -> torch.Tensor:
@@ -341,7 +443,8 @@ class FullyShardedDataParallel(nn.Module):
                  device: Optional[torch.device] = None, wrap_policy: WrapPolicy = None,
                  param_dtype: torch.dtype = torch.float32, reshard_after_forward: bool = True,
                  prefetch: bool = True, sync_module_states: bool = True, cpu_offload: bool = False,
-                 reduce_dtype: Optional[torch.dtype] = None, replicate_comm: Optional[Communicator] = None) -> None:
+                 reduce_dtype: Optional[torch.dtype] = None, replicate_comm: Optional[Communicator] = None,
+                 gather_ring: Optional[int] = None) -> None:
         super().__init__()
         self.cpu_offload = bool(cpu_offload)
         if self.cpu_offload and param_dtype != torch.float32:
@@ -479,6 +582,12 @@ class FullyShardedDataParallel(nn.Module):
                 if b.numel():
                     self.rep.broadcast(b.data, src=0)
 
+        # fixed gather buffers at world size > 1 (_GatherRing; gather_ring / DTA_FSDP_GATHER_RING = 0: the
+        # allocate-and-free storage of every unit instead, not capturable)
+        ring = int(os.environ.get("DTA_FSDP_GATHER_RING", "3")) if gather_ring is None else int(gather_ring)
+        self._ring: Optional[_GatherRing] = None
+        if ring > 0 and self.world_size > 1 and not self.cpu_offload:
+            self._ring = _GatherRing(self, ring)
         prepare = getattr(self.comm, "prepare", None)
         if prepare is not None and self.world_size > 1:
             # size-routed data planes (parallel/routed.py): the route of every unit's all-gather and
@@ -793,14 +902,31 @@ class FullyShardedDataParallel(nn.Module):
             torch.cuda.current_stream(self.device).synchronize()  # host gradients complete before a CPU step
         for u in self.units:  # any unit not used in backward: drop its gathered copy
             u.in_backward = False
+            u.wait()  # (a prefetch nothing consumed: ordered here, so a captured step has no unjoined work)
             if u.gathered and (not u.is_root or self.reshard_root_after_backward):
                 u.free()
 
     def graph_capturable(self) -> bool:
         """The whole step can be captured as one hipGraph (engine/step_graph.py): at one rank without
-        CPU offload every unit aliases its shard, so no storage is freed or re-allocated between
-        units and no collective runs -- the replay repeats the same kernels on the same buffers."""
-        return self.world_size == 1 and self.rep is None and not self.cpu_offload and all(u.alias for u in self.units)
+        CPU offload every unit aliases its shard; at several, every unit gathers into a fixed buffer
+        (_GatherRing) -- either way no storage is freed or re-allocated between units and the replay
+        repeats the same kernels and collectives on the same buffers.  (Whether the collectives may be
+        captured -- the data plane they route to -- is engine/step_graph.py ``capture_policy``'s call.)"""
+        if self.cpu_offload or self.rep is not None:
+            return False
+        if self.world_size == 1:
+            return all(u.alias for u in self.units)
+        return self._ring is not None
+
+    def step_messages(self) -> List[Tuple[str, torch.dtype, int]]:
+        """The collectives one training step issues: per unit its all-gather(s) and reduce-scatter."""
+        pe = torch.empty((), dtype=self.param_dtype).element_size()
+        re_ = torch.empty((), dtype=self.reduce_dtype).element_size()
+        out: List[Tuple[str, torch.dtype, int]] = []
+        for u in self.units:
+            out.append(("all_gather", self.param_dtype, u.total * pe))
+            out.append(("reduce_scatter", self.reduce_dtype, u.total * re_))
+        return out
 
     def _mark_grads_fresh(self) -> None:
         self._grad_fresh = True

@@ -143,6 +143,23 @@ class RoutedComm(Communicator):
             added.append(size)
         return added
 
+    def alpha_beta(self, op: str = "all_reduce", dtype: torch.dtype = torch.bfloat16) -> Optional[Tuple[float, float]]:
+        """``(alpha s, beta B/s)`` of ``t(S) = alpha + S / beta`` fitted over the calibration's timings of
+        (op, dtype) -- per size class the time of the route the class takes (the MAX over the ranks, so
+        every rank fits the same numbers and derives the same DDP bucket plan).  None without timings.
+        parallel/flat.py ``bucket_caps_for`` sizes DDP's buckets from it."""
+        from .flat import fit_alpha_beta
+
+        routes = self.table.get((op, dtype))
+        if routes is None:
+            return None
+        pts = []
+        for s, r in zip(self.sizes, routes):
+            t = self.timings.get(f"{op} {str(dtype).replace('torch.', '')} {s // MiB}MiB")
+            if t is not None:
+                pts.append((s, (t[1] if r == "fast" else t[0]) * 1e-6))
+        return fit_alpha_beta(pts)
+
     def routes(self) -> Dict[str, str]:
         """``"all_reduce bf16 <=4MiB" -> "ipc" | "rccl"`` for the log / bench JSON."""
         out = {}

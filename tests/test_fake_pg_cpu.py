@@ -113,3 +113,55 @@ def test_ddp_buckets_sized_for_xgmi_and_padded():
     ids = [i for b in ddp.buckets for i in b.param_ids]
     assert ids == list(range(len(ddp.flat.params)))
     assert ddp.flat.names[0] == "11.bias"  # reverse registration order: last layer's grads fill bucket 0
+
+
+def test_ddp_bucket_caps_from_measured_allreduce_times():
+    """bucket_cap_mb="auto" with a calibrated communicator: the caps come from the α/β fit of the
+    all-reduce timings the routed communicator measured at wrap, not from the
+    assumed xGMI constants -- pinned here with a fixed fake timing table."""
+    import torch.nn as nn
+
+    from distributed_training_amd.parallel.comm import Communicator
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+    from distributed_training_amd.parallel.flat import fit_alpha_beta, measured_bucket_caps
+    from distributed_training_amd.parallel.routed import MiB, SIZES, RoutedComm
+
+    class Plane(Communicator):
+        def __init__(self, name):
+            self.name, self.rank, self.world_size, self.device = name, 0, 8, torch.device("cpu")
+
+        def all_reduce(self, t, op="sum", async_op=False):
+            return None
+
+        def broadcast(self, t, src=0, async_op=False):
+            return None
+
+    # t(S) = 25 us + S / 120 GB/s on RCCL; the IPC plane wins the 1 MiB class only (8 us + S / 60 GB/s)
+    alpha, beta = 25e-6, 120e9
+    table = {("all_reduce", torch.bfloat16): ["fast", "primary", "primary", "primary"]}
+    comm = RoutedComm(Plane("rccl"), Plane("ipc"), table=table)
+    for s in SIZES:
+        comm.timings[f"all_reduce bfloat16 {s // MiB}MiB"] = (round((alpha + s / beta) * 1e6, 1),
+                                                              round((8e-6 + s / 60e9) * 1e6, 1))
+    a, b = comm.alpha_beta("all_reduce", torch.bfloat16)
+    # the fit runs over the ROUTED times: the 1 MiB point is the IPC plane's
+    want = fit_alpha_beta([(s, ((8e-6 + s / 60e9) if i == 0 else (alpha + s / beta))) for i, s in enumerate(SIZES)])
+    assert abs(a - want[0]) < 1e-7 and abs(b / want[1] - 1) < 1e-3
+    assert fit_alpha_beta([(MiB, 30e-6), (4 * MiB, 60e-6)]) == pytest.approx((20e-6, 3 * MiB / 30e-6))
+    assert fit_alpha_beta([(MiB, 30e-6), (4 * MiB, 20e-6)]) is None  # no positive slope: the model
+
+    model = nn.Sequential(*[nn.Linear(1024, 1024) for _ in range(24)])  # 100.7 MB of bf16 gradients
+    ddp = DistributedDataParallel(model, comm=comm, device=torch.device("cpu"), bucket_cap_mb="auto",
+                                  param_dtype=torch.bfloat16, init_sync=False)
+    grad_bytes = sum(p.numel() for p in model.parameters()) * 2
+    assert ddp.bucket_bytes == measured_bucket_caps(grad_bytes, a, b)
+    assert ddp.bucket_caps_source.startswith("measured")
+    first, cap = ddp.bucket_bytes
+    # 10 alpha beta ~ 30 MB > grad / 6 ~ 16.8 MB: the overlap rule (>= 6 buckets) sets the cap
+    assert cap == int(min(10 * a * b, grad_bytes / 6)) and first == max(MiB, cap // 16)
+    # a plain communicator (no timings): the xGMI model
+    from distributed_training_amd.parallel.flat import xgmi_bucket_caps
+
+    ddp2 = DistributedDataParallel(model, comm=Plane("rccl"), device=torch.device("cpu"), bucket_cap_mb="auto",
+                                   param_dtype=torch.bfloat16, init_sync=False)
+    assert ddp2.bucket_bytes == xgmi_bucket_caps(8, grad_bytes) and ddp2.bucket_caps_source.startswith("xgmi")

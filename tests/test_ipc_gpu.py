@@ -668,3 +668,83 @@ def _hsdp_worker(rank, ws, shard_size):
 @pytest.mark.parametrize("ws,shard_size", [(2, 1), (4, 2), (8, 4)])  # (2, 1): one rank per shard group
 def test_hybrid_shard_shared_gpu(ws, shard_size):
     run_gloo(_hsdp_worker, ws, shard_size)
+
+
+def _fsdp_graph_multirank_worker(rank, ws, arch):
+    """FULL_SHARD at world size > 1 in a capture-safe form -- every unit gathers
+    into a FIXED buffer (parallel/fsdp.py _GatherRing) instead of allocating and freeing its storage --
+    so the whole step (per-unit IPC all-gathers with prefetch, reduce-scatters, deferred grouped weight
+    gradients, fused AdamW) is captured ONCE per rank and replayed.  Three runs on the same batches:
+    eager with the allocate-and-free storage (gather_ring=0), eager with the ring, and the replayed
+    graph: losses and fp32 master shards bit-identical across all three, replicas consistent across
+    ranks, and the capture policy (engine/step_graph.py) says yes for the IPC data plane."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.engine.step_graph import GraphedStep, capture_policy
+    from distributed_training_amd.models.gpt2 import GPT2, GPT2Config
+    from distributed_training_amd.models.llama import Llama, LlamaConfig
+    from distributed_training_amd.ops.optim import FusedAdamW
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel, lm_wrap_policy
+    from distributed_training_amd.parallel.ipc import IpcComm
+
+    dev = _shared()
+    g = torch.Generator(device="cpu").manual_seed(60 + rank)  # different batches per rank
+    data = [torch.randint(0, 1024, (2, 129), generator=g).to(dev) for _ in range(5)]
+    seq = [data[0]] * 3 + data[1:]  # GraphedStep's 3 warm-up steps train on the static batch
+
+    def build():
+        torch.manual_seed(0)
+        if arch == "gpt2":
+            return GPT2(GPT2Config(n_layer=3, n_head=4, n_embd=256, vocab_size=1024, block_size=256)).to(dev)
+        return Llama(LlamaConfig(n_layer=3, n_head=4, n_kv_head=2, n_embd=256, ffn_hidden=512, vocab_size=1024,
+                                 block_size=256)).to(dev)
+
+    out = []
+    # one communicator for the three runs (an IPC buffer freed and re-allocated in one process can come back
+    # at the same address, whose dmabuf export the driver then refuses)
+    comm = IpcComm(rank, ws, dev, tag=f"fsdpg_{arch}")
+    for mode in ("resize", "ring", "graph"):
+        model = build()
+        w = FullyShardedDataParallel(model, comm=comm, device=dev, wrap_policy=lm_wrap_policy(model),
+                                     param_dtype=torch.bfloat16, gather_ring=0 if mode == "resize" else 3)
+        assert (w._ring is None) == (mode == "resize")
+        ok, why = capture_policy(w)
+        assert ok == (mode != "resize"), why
+        opt = FusedAdamW(w.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+
+        def step(xb):
+            opt.zero_grad(set_to_none=True)
+            loss = w(xb[:, :-1], xb[:, 1:])
+            loss.backward()
+            opt.step()
+            return loss
+
+        losses = []
+        if mode == "graph":
+            gs = GraphedStep(step, [data[0].clone()], warmup=3, engine=w)
+            assert gs.ok, gs.error
+            for xb in seq[3:]:
+                losses.append(gs(xb).float().clone())
+        else:
+            for xb in seq:
+                losses.append(step(xb).float().clone())
+                assert not any(u.gathered for u in w.units)
+            losses = losses[3:]
+        torch.cuda.synchronize()
+        comm.poll_errors()
+        out.append((torch.stack(losses).cpu(), w.shards.master.clone()))
+        if mode == "graph":
+            full = torch.cat([v.float().reshape(-1).cpu() for v in w.full_state_dict(rank0_only=False).values()])
+    comm.destroy()
+    for k in (1, 2):
+        assert torch.equal(out[0][0], out[k][0]), (rank, k, out[0][0], out[k][0])
+        assert torch.equal(out[0][1], out[k][1]), (rank, k)
+    parts = _gather_cpu(full)  # the gathered model is the same on every rank
+    assert all(torch.equal(p, parts[0]) for p in parts[1:])
+    dist.barrier()
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("arch", ["gpt2", "llama"])
+def test_fsdp_step_graph_multirank_matches_eager(arch, ws):
+    run_gloo(_fsdp_graph_multirank_worker, ws, arch)

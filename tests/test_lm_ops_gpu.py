@@ -198,6 +198,52 @@ def test_ddp_linear_gradients_written_into_flat_buffer():
         assert all(ddp.flat.grad_is_view(i) for i in range(len(ddp.flat.params)))
 
 
+@pytest.mark.parametrize("fused_add", [False, True])
+def test_ddp_norm_weight_used_twice(fused_add):
+    """A LayerNorm (gamma, beta) applied twice in one backward: the deferred column-sum path
+    (ops/lm.py _NORM_DEFER) must not be taken for it -- the gradient is the sum of both uses,
+    equal to an un-wrapped copy's."""
+    import copy
+
+    from distributed_training_amd.parallel.comm import RcclComm
+    from distributed_training_amd.parallel.ddp import DistributedDataParallel
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = lm.Linear(256, 256)
+            self.ln = torch.nn.LayerNorm(256)
+            self.b = lm.Linear(256, 256)
+
+        def forward(self, x):
+            h = self.a(x)
+            if fused_add:
+                r, h = lm.add_layer_norm(h, x, self.ln.weight, self.ln.bias)
+            else:
+                h = lm.layer_norm(h, self.ln.weight, self.ln.bias)
+            h = self.b(h)
+            return lm.layer_norm(h, self.ln.weight, self.ln.bias)  # second use of gamma / beta
+
+    torch.manual_seed(5)
+    dev = torch.device(DEV, 0)
+    net = Net().to(dev).bfloat16()
+    with torch.no_grad():
+        net.ln.weight.uniform_(0.5, 1.5)
+        net.ln.bias.uniform_(-0.5, 0.5)
+    ref = copy.deepcopy(net)
+    ddp = DistributedDataParallel(net, comm=RcclComm(0, 1, dev), device=dev, param_dtype=torch.bfloat16)
+    x = torch.randn(1024, 256, device=dev).bfloat16()
+    for it in range(3):
+        ddp.zero_grad(set_to_none=True)
+        ddp(x).float().square().mean().backward()
+        for p in ref.parameters():
+            p.grad = None
+        ref(x).float().square().mean().backward()
+        refs = dict(ref.named_parameters())
+        for name, p in net.named_parameters():
+            assert _rel(p.grad, refs[name].grad) < 2e-2, (it, name)
+
+
 def test_llama_tiny_fsdp_trains_on_gpu():
     from distributed_training_amd.models.llama import Block, Llama, LlamaConfig
     from distributed_training_amd.ops.optim import FusedAdamW
@@ -336,6 +382,32 @@ def test_chunked_head_ce_peak_memory():
     saved = peaks[0] - peaks[1]
     assert saved > 0.8 * (T - chunk) * V * 2, (peaks, saved)
     assert _rel(grads[1][0], grads[0][0]) < 1e-2 and _rel(grads[1][1], grads[0][1]) < 1e-2
+
+
+def test_chunked_head_ce_dw_drift_many_blocks():
+    """the row-blocked head accumulates dW in bf16 (one rounding per block, hipBLASLt beta = 1) --
+    pinned with an explicit tolerance at many blocks (T / chunk = 32) against an fp32 reference: within
+    1e-2 norm-relative and within 4x the one-block form's own error (plus a floor).  A second backward
+    through the same graph raises instead of returning no gradients."""
+    torch.manual_seed(11)
+    T, C, V, chunk = 8192, 256, 4096, 256
+    x = (0.5 * torch.randn(T, C, device=DEV)).bfloat16().requires_grad_()
+    w = (0.1 * torch.randn(V, C, device=DEV)).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (T,), device=DEV)
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    torch.nn.functional.cross_entropy(xf @ wf.t(), t).backward()
+    errs = []
+    for ch in (0, chunk):
+        x.grad = w.grad = None
+        lm.linear_cross_entropy(x, w, t, chunk=ch).backward()
+        errs.append((_rel(x.grad, xf.grad), _rel(w.grad, wf.grad)))
+    (ex0, ew0), (ex1, ew1) = errs
+    assert ex1 < 1e-2 and ew1 < 1e-2, errs
+    assert ew1 <= 4 * ew0 + 2e-3, errs
+    loss = lm.linear_cross_entropy(x, w, t, chunk=chunk)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="one backward per forward"):
+        loss.backward()
 
 
 def test_chunked_head_ce_no_grad_forward_writes_no_gradient():

@@ -1,5 +1,6 @@
 """Native DDP / FSDP engines vs torch references, multi-process gloo (CPU)."""
 import copy
+import os
 
 import pytest
 import torch
@@ -691,24 +692,39 @@ def test_hybrid_shard_strategy_from_config():
         FSDPStrategy(False, sharding="hsdp2")
 
 
-def test_step_graph_off_when_buckets_route_to_rccl():
-    """at world size > 1 the whole-step hipGraph is not used when any DDP bucket's
-    all-reduce routes to RCCL (RCCL-in-graph replay unverified on a multi-GPU node); IPC-only routes keep it."""
+def test_capture_policy_routes():
+    """ONE capture policy (engine/step_graph.py capture_policy) for the Trainer and
+    bench_lm.py -- at world size > 1 the whole-step hipGraph is used only when every collective of the
+    step routes to the IPC data plane (RCCL-in-graph replay is unverified on a multi-GPU node: opt-in
+    DTA_GRAPH_RCCL=1); process-group calls never; one rank always (if the engine state allows)."""
     from types import SimpleNamespace
 
-    from distributed_training_amd.engine.trainer import Trainer
-    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.engine.step_graph import capture_policy
+    from distributed_training_amd.parallel.comm import RcclComm, TorchComm
+    from distributed_training_amd.parallel.ipc import IpcComm
     from distributed_training_amd.parallel.routed import MiB, RoutedComm
 
-    rc = RoutedComm(TorchComm(), TorchComm(), sizes=(MiB, 16 * MiB), calibrate=False)
-    buckets = [SimpleNamespace(start=0, end=MiB // 8), SimpleNamespace(start=MiB // 8, end=3 * MiB)]
-    flat = SimpleNamespace(grad=torch.zeros(1, dtype=torch.bfloat16))
-    tr = Trainer.__new__(Trainer)
-    tr.env = SimpleNamespace(world_size=2)
-    tr.model = SimpleNamespace(comm=rc, flat=flat, buckets=buckets)
+    def stub(cls):
+        c = cls.__new__(cls)
+        c.rank, c.world_size, c.device = 0, 2, torch.device("cpu")
+        return c
+
+    rc = RoutedComm(stub(RcclComm), stub(IpcComm), sizes=(MiB, 16 * MiB), calibrate=False)
+    msgs = [("all_reduce", torch.bfloat16, MiB // 4), ("all_reduce", torch.bfloat16, 6 * MiB)]
+    eng = SimpleNamespace(graph_capturable=lambda: True, world_size=2, comm=rc, step_messages=lambda: msgs)
     rc.table[("all_reduce", torch.bfloat16)] = ["fast", "fast"]
-    assert not tr._buckets_on_rccl()
-    rc.table[("all_reduce", torch.bfloat16)] = ["fast", "primary"]  # the 5.8 MB bucket goes to RCCL
-    assert tr._buckets_on_rccl()
-    tr.env = SimpleNamespace(world_size=1)
-    assert not tr._buckets_on_rccl()
+    assert capture_policy(eng)[0]
+    rc.table[("all_reduce", torch.bfloat16)] = ["fast", "primary"]  # the 6 MB bucket goes to RCCL
+    ok, why = capture_policy(eng)
+    assert not ok and "RCCL" in why
+    os.environ["DTA_GRAPH_RCCL"] = "1"
+    try:
+        assert capture_policy(eng)[0]
+    finally:
+        del os.environ["DTA_GRAPH_RCCL"]
+    eng.comm = TorchComm()  # gloo / torch process group: never captured
+    assert not capture_policy(eng)[0]
+    eng.world_size = 1
+    assert capture_policy(eng)[0]
+    eng.graph_capturable = lambda: False  # e.g. FSDP with CPU offload
+    assert not capture_policy(eng)[0]
