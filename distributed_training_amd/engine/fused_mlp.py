@@ -34,6 +34,8 @@ from ..ops import native
 
 logger = logging.getLogger(__name__)
 _TRACE = bool(os.environ.get("DTA_BENCH_TRACE"))
+# single-step launches at the start of the first (warm-up) call; DTA_MLP_WARM_SPLIT (A/B of the warm-up split)
+_WARM_SPLIT = max(1, int(os.environ.get("DTA_MLP_WARM_SPLIT", "1")))
 
 
 def fused_eligible(module: nn.Module, optimizer: Any, loader: Any, loss: str, device: torch.device) -> Optional[str]:
@@ -462,6 +464,7 @@ class FusedMLPProgram:
         # the timed region of a short bench call is a few dozen microseconds)
         _T = [time.perf_counter()] if _TRACE else None
         end = self.launched + n
+        first_call = self.launched == 0
         g = self.opt.param_groups[0]
         hkey = (g["lr"], g.get("momentum", 0.0), g.get("dampening", 0.0), g.get("weight_decay", 0.0),
                 g.get("nesterov", False), g.get("maximize", False))
@@ -472,9 +475,9 @@ class FusedMLPProgram:
             self._ensure(min(2 * self.chunk_steps, self.R - self.steps_per_epoch))
         while self.launched < end:
             k = min(end - self.launched, self.chunk_steps)
-            if self.launched == 0 and n > 1:
-                # the first call (the warm-up) runs its steps as two launches, 1 + rest: on the
-                # gpurun boxes the SECOND launch of the program paid ~14-17 us inside
+            if first_call and self.launched < _WARM_SPLIT and end - self.launched > 1:
+                # the first call (the warm-up) runs its steps as 1 + rest launches (_WARM_SPLIT single-step
+                # launches first): on the gpurun boxes the SECOND launch of the program paid ~14-17 us inside
                 # hipLaunchKernel (the third ~1 us), which otherwise lands on the first timed call.
                 # Warm-up accounting only -- the per-step kernel time is unchanged
                 # (profiles/headline_split_first_launch.txt)
