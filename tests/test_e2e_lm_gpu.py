@@ -66,3 +66,28 @@ def test_lm_step_graph_through_entrypoint_gpu(tmp_path, name, args):
     assert "Loading snapshot" in log2 and "0] Epoch 1 |" not in log2
     resumed = _losses(log2)
     assert resumed[0] < losses[0]
+
+
+@pytest.mark.parametrize("name,args", [
+    ("gpt2_fsdp", TINY_GPT2 + GPU_WIDTH + ["train=gpt2_fsdp", "train.dataset_size=128"]),
+    ("llama_fsdp", TINY_LLAMA + GPU_WIDTH + ["model.ffn_hidden=512", "train=llama3_8b_fsdp", "train.dataset_size=64"]),
+    ("gpt2_ddp", TINY_GPT2 + GPU_WIDTH + ["train=gpt2_ddp", "train.dataset_size=128"]),
+])
+def test_lm_step_graph_two_ranks_through_entrypoint(tmp_path, name, args):
+    """Two ranks sharing the GPU (DTA_SHARED_GPU=1: the IPC data plane, gloo control plane) through the
+    entrypoint: the Trainer's capture policy (engine/step_graph.py) sees every collective on the IPC plane and
+    replays the whole step -- FSDP FULL_SHARD included, its units gathered into the fixed ring buffers
+    (parallel/fsdp.py _GatherRing) -- on both ranks; the loss is finite and falls."""
+    tag = "ws2"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={_port()}", ENTRY, "3", "1000", *args, "train.device=cuda",
+           f"hydra.run.dir={tmp_path}/{tag}", f"train.snapshot_path={tmp_path / 'snap.pt'}"]
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="4", DTA_SHARED_GPU="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    log = (tmp_path / tag / "train.log").read_text()
+    assert "Running with 2 processes total" in log, log[-2000:]
+    assert log.count("whole training step is replayed as one hipGraph") == 2, log[-3000:]
+    assert "step graph disabled" not in log and "step graph not used" not in log
+    losses = _losses(log)  # (both ranks log each epoch: first two lines epoch 0, last two the final epoch)
+    assert len(losses) == 6 and sum(losses[-2:]) < sum(losses[:2]), losses
