@@ -728,3 +728,39 @@ def test_capture_policy_routes():
     assert capture_policy(eng)[0]
     eng.graph_capturable = lambda: False  # e.g. FSDP with CPU offload
     assert not capture_policy(eng)[0]
+
+
+def _fsdp_ring_vs_resize(rank, ws):
+    from distributed_training_amd.ops.optim import FusedSGD
+    from distributed_training_amd.parallel.comm import TorchComm
+    from distributed_training_amd.parallel.fsdp import FullyShardedDataParallel
+
+    finals = []
+    for ring in (0, 3, 2):
+        for raf in (True, False):
+            torch.manual_seed(0)
+            m = CkptNet() if raf else Net()
+            fs = FullyShardedDataParallel(m, TorchComm(), torch.device("cpu"), wrap_policy={Block}, gather_ring=ring,
+                                          reshard_after_forward=raf)
+            assert (fs._ring is None) == (ring == 0) and len(fs.units) >= 3
+            if ring:
+                assert len(fs._ring.bufs) == ring and fs.graph_capturable()
+            opt = FusedSGD(fs.parameters(), lr=0.1, momentum=0.9)
+            for it in range(3):
+                g = torch.Generator().manual_seed(11 + it)
+                X, Y = torch.randn(8 * ws, 20, generator=g), torch.randn(8 * ws, 1, generator=g)
+                opt.zero_grad()
+                F.mse_loss(fs(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+                opt.step()
+                assert not any(u.gathered for u in fs.units if not u.is_root)
+            finals.append((ring, raf, torch.cat([v.reshape(-1) for v in fs.full_state_dict(rank0_only=False).values()])))
+    base = {raf: t for ring, raf, t in finals if ring == 0}
+    for ring, raf, t in finals:
+        assert torch.equal(t, base[raf]), (ring, raf)
+
+
+def test_fsdp_gather_ring_matches_allocate_and_free():
+    """parallel/fsdp.py _GatherRing (fixed gather buffers at world size > 1, 2 or 3 slots) trains bit-identically
+    to the allocate-and-free unit storage, with prefetch, activation checkpointing (re-gathered units) and
+    reshard_after_forward off (units evicted from a shared slot and re-gathered for backward)."""
+    run_gloo(_fsdp_ring_vs_resize, 3)
