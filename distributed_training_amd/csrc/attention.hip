@@ -1078,13 +1078,16 @@ static void fwd_launch(const AttnArgs& a, bool causal, hipStream_t st) {
 }
 
 // 8 waves (256 queries) per workgroup share each K/V tile: measured faster
-// whenever the grid still holds >= 256 (D = 64; GPT-2: 43.6 -> 37.4 us) or
-// >= 1024 (D = 128) such workgroups.
+// whenever the grid still holds >= 1024 such workgroups (D = 128; Llama-3 8B shape 552 -> 526 us).
+// At D = 64 the 8-wave form was faster at GPT-2's 384 workgroups before the forward's software
+// pipeline (round 2: 43.6 -> 37.4 us); at HEAD the 4-wave form is (26.2-27.6 -> 24.3-24.8 us,
+// profiles/attn_forms_r6k.jsonl), so both head dims take the same threshold.
 static int fwd_waves(const AttnArgs& a, int D) {
   const char* force = getenv("DTA_ATTN_FWD_WAVES");  // tests / sweeps: "4" or "8"
   if (force) return atoi(force) == 8 ? 8 : 4;
+  (void)D;
   const int64_t wg8 = (int64_t)((a.S + 255) / 256) * a.B * a.H;
-  return wg8 >= (D == 128 ? 1024 : 256) ? 8 : 4;
+  return wg8 >= 1024 ? 8 : 4;
 }
 
 static int dq_waves(const AttnArgs& a, int D) {

@@ -103,7 +103,9 @@ class _SplitInto(torch.autograd.Function):
     def forward(ctx: Any, full: torch.Tensor, unit: Any) -> Tuple[torch.Tensor, ...]:
         ctx.unit = unit
         ctx.set_materialize_grads(False)
-        return tuple(full.split(unit._split_sizes))
+        # every piece already in its parameter's shape, in ONE native call (shape templates on the meta device):
+        # no per-parameter Python view per forward
+        return tuple(torch._C._nn.unflatten_dense_tensors(full, unit._templates))
 
     @staticmethod
     def backward(ctx: Any, *grads: Any) -> Tuple[Optional[torch.Tensor], None]:
@@ -229,6 +231,8 @@ class _Unit:
         if self.total > pos:
             self._split_sizes.append(self.total - pos)
         self._split_offs = [sum(self._split_sizes[:i]) for i in range(len(self._split_sizes))]
+        shape_of = {k: shp for k, shp in zip(self._piece_index, self.shapes)}
+        self._templates = [torch.empty(shape_of.get(k, (n,)), device="meta") for k, n in enumerate(self._split_sizes)]
         self._pieces = [_Piece(self, e) for e in range(len(entries))]
         self._targets: Optional[List[List[Tuple[Dict[str, Any], str]]]] = None  # set_views' attribute slots
         self.ring: Optional[_GatherRing] = None  # fixed gather buffers (world size > 1, see _GatherRing)
@@ -322,8 +326,8 @@ class _Unit:
         full-size gradient and add it in (O(params x unit size) traffic)."""
         pieces = _SplitInto.apply(self.full, self)
         targets = self._targets if self._targets is not None else self._build_targets()
-        for piece, k, shp, tg in zip(self._pieces, self._piece_index, self.shapes, targets):
-            view = pieces[k].view(shp)
+        for piece, k, tg in zip(self._pieces, self._piece_index, targets):
+            view = pieces[k]
             view._dta_gdest = piece  # (ops/lm.py: its gradient slice, deferral -- see _Piece)
             for d, a in tg:  # tied weights: every owner
                 d[a] = view
