@@ -248,9 +248,12 @@ __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restr
     d[i] = f2bf(s[i]);
 }
 
+#ifndef DTA_OPT_MAX_GRID
+#define DTA_OPT_MAX_GRID 2048
+#endif
 static inline int grid_for(int64_t n_vec) {
   int64_t b = (n_vec + 255) / 256;
-  if (b > 2048) b = 2048;  // 256 CUs x 8 blocks; grid-stride the rest
+  if (b > DTA_OPT_MAX_GRID) b = DTA_OPT_MAX_GRID;  // 256 CUs x 8 blocks; grid-stride the rest
   if (b < 1) b = 1;
   return (int)b;
 }
