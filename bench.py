@@ -107,16 +107,32 @@ def build(args: argparse.Namespace, dev: "torch.device", ws: int) -> Tuple[Any, 
     return ds, model, loader
 
 
+def bench_comm(dev: "torch.device") -> Any:
+    """The step's communicator (``make_comm``: native RCCL at N > 1).  A native communicator that cannot come up
+    on every rank (librccl not loadable, init refused) falls back to torch.distributed's own process group --
+    RCCL through c10d -- so the run still yields its number; the JSON's ``comm`` says which one ran."""
+    import torch.distributed as dist
+
+    from distributed_training_amd.parallel.comm import TorchComm, make_comm
+
+    try:
+        return make_comm(dev)
+    except Exception as e:  # noqa: BLE001 - load / init failures are raised on every rank alike
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            raise
+        print(f"[bench] native communicator unavailable ({e}); torch.distributed used", file=sys.stderr)
+        return TorchComm(device=dev)
+
+
 def run_fused(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runner":
     import torch
 
     from distributed_training_amd.engine.fused_mlp import FusedMLPProgram, fused_eligible
     from distributed_training_amd.ops.optim import FusedSGD
-    from distributed_training_amd.parallel.comm import make_comm
     from distributed_training_amd.parallel.ddp import DistributedDataParallel
 
     ds, model, loader = build(args, dev, ws)
-    comm = make_comm(dev)
+    comm = bench_comm(dev)
     ddp = DistributedDataParallel(model, comm=comm, device=dev)
     opt = FusedSGD(ddp.parameters(), lr=args.lr)
     why = fused_eligible(model, opt, loader, "mse", dev)
@@ -149,7 +165,6 @@ def run_fused_linear(args: argparse.Namespace, dev: "torch.device", ws: int) -> 
     from distributed_training_amd.data.datasets import DeviceDataLoader, MyTrainDataset
     from distributed_training_amd.engine.fused_linear import FusedLinearProgram, linear_eligible
     from distributed_training_amd.ops.optim import FusedSGD
-    from distributed_training_amd.parallel.comm import make_comm
     from distributed_training_amd.parallel.ddp import DistributedDataParallel
     from distributed_training_amd.parallel.sampler import DistributedSampler
 
@@ -158,7 +173,7 @@ def run_fused_linear(args: argparse.Namespace, dev: "torch.device", ws: int) -> 
     model = torch.nn.Linear(20, 1).to(dev)
     rank = int(os.environ.get("RANK", "0"))
     loader = DeviceDataLoader(ds, args.batch, sampler=DistributedSampler(ds, num_replicas=ws, rank=rank), device=dev)
-    comm = make_comm(dev)
+    comm = bench_comm(dev)
     ddp = DistributedDataParallel(model, comm=comm, device=dev)
     opt = FusedSGD(ddp.parameters(), lr=args.lr)
     why = linear_eligible(model, opt, loader, "cross_entropy", dev)
@@ -182,11 +197,10 @@ def run_generic(args: argparse.Namespace, dev: "torch.device", ws: int) -> "Runn
     import torch.nn.functional as F
 
     from distributed_training_amd.ops.optim import FusedSGD
-    from distributed_training_amd.parallel.comm import make_comm
     from distributed_training_amd.parallel.ddp import DistributedDataParallel
 
     ds, model, loader = build(args, dev, ws)
-    comm = make_comm(dev)
+    comm = bench_comm(dev)
     ddp = DistributedDataParallel(model, comm=comm, device=dev)
     opt = FusedSGD(ddp.parameters(), lr=args.lr)
     state = {"it": None, "epoch": 0, "loss": None}
@@ -366,6 +380,8 @@ def main() -> None:
     if getattr(args, "shared_gpu", False):
         out["shared_gpu"] = f"{ws} ranks on {torch.cuda.device_count()} GPU(s): correctness rehearsal, not a scaling number"
     out.update(getattr(finish, "info", {}))
+    if comm is not None and ws > 1:
+        out["comm"] = getattr(comm, "name", type(comm).__name__)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

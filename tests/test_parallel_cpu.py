@@ -764,3 +764,32 @@ def test_fsdp_gather_ring_matches_allocate_and_free():
     to the allocate-and-free unit storage, with prefetch, activation checkpointing (re-gathered units) and
     reshard_after_forward off (units evicted from a shared slot and re-gathered for backward)."""
     run_gloo(_fsdp_ring_vs_resize, 3)
+
+
+def _bench_comm_fallback(rank, ws):
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    from distributed_training_amd.parallel import comm as comm_mod
+
+    def refuse(*a, **k):
+        raise RuntimeError("could not load librccl: test")
+
+    orig = comm_mod.make_comm
+    comm_mod.make_comm = refuse
+    try:
+        c = bench.bench_comm(torch.device("cpu"))
+    finally:
+        comm_mod.make_comm = orig
+    assert c.name == "torch" and c.world_size == ws
+    t = torch.full((3,), float(rank + 1))
+    c.all_reduce(t, op="sum")
+    assert t.tolist() == [float(sum(range(1, ws + 1)))] * 3
+
+
+def test_bench_comm_falls_back_to_torch_distributed():
+    """bench.py at N > 1: a native communicator that cannot come up on the ranks leaves the run on
+    torch.distributed's process group instead of ending it (the JSON's ``comm`` names the one that ran)."""
+    run_gloo(_bench_comm_fallback, 2)
