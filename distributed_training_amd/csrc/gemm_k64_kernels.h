@@ -82,6 +82,20 @@ namespace k64 {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// DTA_K64_DMA_IN_MFMA (diagnostic builds, scripts/k64_dim_probe.hip): the two-phase loop issues each phase's
+// LDS-DMA pieces inside the phase's MFMA cluster (spread between the MFMAs) instead of in its read phase.
+#ifndef DTA_K64_DMA_IN_MFMA
+#define DTA_K64_DMA_IN_MFMA 0
+#endif
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void k64_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    k64_static_for<N, I + 1>(f);
+  }
+}
+
 #ifdef DTA_K64_STAMP
 // s_memtime with its lgkmcnt(0) in ONE statement (cdna_hip_programming.md "In-kernel stamps"); the
 // diagnostic build's run time is never quoted, only the segment shares
@@ -453,6 +467,45 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   unsigned long long seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = stamp_now();
 #endif
+  // DIM (DTA_K64_DMA_IN_MFMA): a phase's DMA pieces go out between the MFMAs of its cluster, after the
+  // phase's first barrier -- later than the read-phase placement, so every restaged half was retired by
+  // every wave's reads even earlier than that form guarantees; the waits then leave one phase's pieces
+  // fewer in flight (S1: the previous S3's top / left / right; S3: the S1 bottom), three barrier
+  // intervals after issue as before
+  constexpr bool DIM = DTA_K64_DMA_IN_MFMA != 0;
+  auto piece_a = [&](int h, int kt, int j) {
+    const int ks = kofs + min(kt, nk - 1);
+    if constexpr (BUF) bglds16(rsA, voA[h][j], (unsigned)(ks * stepA * 2), lds0 + aoff(h, kt & 1) + (j * NW + wave) * 1024);
+    else glds16(srcA[h][j] + ks * stepA, lds + aoff(h, kt & 1) + (j * NW + wave) * 1024);
+  };
+  auto piece_b = [&](int h, int kt, int j) {
+    const int ks = kofs + min(kt, nk - 1);
+    if constexpr (BUF) bglds16(rsB, voB[BJ ? 0 : h][j], (unsigned)(ks * stepB * 2), lds0 + boff(h, kt & 1) + (j * NW + wave) * 1024);
+    else glds16(srcB[BJ ? 0 : h][j] + ks * stepB, lds + boff(h, kt & 1) + (j * NW + wave) * 1024);
+  };
+  // the 2 x (2 NTH MTH) MFMAs of mma(af, bx, mh, nhx) then mma(af, by, mh, nhy), with piece p of NP issued
+  // after MFMA (p + 1) * NM / (NP + 1)
+  auto mma2_dma = [&](const bf16x8 (&bx)[NTH][2], int nhx, const bf16x8 (&by)[NTH][2], int nhy, int mh, auto issue,
+                      auto NPc) __attribute__((always_inline)) {
+    constexpr int NP = decltype(NPc)::value, NM = 4 * NTH * MTH, STEP = NM / (NP + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    k64_static_for<NM>([&](auto mc) {
+      constexpr int m = decltype(mc)::value, half = m / (NM / 2), r = m % (NM / 2);
+      constexpr int kk = r / (NTH * MTH), ii = (r / MTH) % NTH, jj = r % MTH;
+      const bf16x8(&bf)[NTH][2] = half == 0 ? bx : by;
+      const int nh = half == 0 ? nhx : nhy;
+      acc[nh * NTH + ii][mh * MTH + jj] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ii][kk], af[jj][kk], acc[nh * NTH + ii][mh * MTH + jj], 0, 0, 0);
+      if constexpr ((m + 1) % STEP == 0 && (m + 1) / STEP <= NP) {
+        __builtin_amdgcn_sched_barrier(0);
+        issue(std::integral_constant<int, (m + 1) / STEP - 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
   // kt2: kt with its parity as a compile-time constant (P = 0 / 1), so (kt2 & 1) folds into immediates;
   // P = -1: runtime parity (every tile but the buffer-DMA 256 x 256 one)
   auto ktile = [&](const int kt, auto P) {
@@ -460,31 +513,47 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     read_a(af, kt2, 0);
     read_b(b0, kt2, 0);
     read_b(b1, kt2, 1);
-    dma_a(1, kt2 + 1);
+    if constexpr (!DIM) dma_a(1, kt2 + 1);
     K64_STAMP(0);
     lgkm0();
-    vm_wait<2 * LA + LB2>();  // bottom (t)
+    vm_wait<DIM ? LA + LB2 : 2 * LA + LB2>();  // bottom (t)
     K64_STAMP(1);
     bar();
     K64_STAMP(2);
-    mma(af, b0, 0, 0);
-    mma(af, b1, 0, 1);
+    if constexpr (DIM) {
+      mma2_dma(b0, 0, b1, 1, 0, [&](auto pc) { piece_a(1, kt2 + 1, decltype(pc)::value); },
+               std::integral_constant<int, LA>{});
+    } else {
+      mma(af, b0, 0, 0);
+      mma(af, b1, 0, 1);
+    }
     mma_cs(af, 0);
     K64_STAMP(3);
     bar();
     K64_STAMP(4);
     read_a(af, kt2, 1);
-    dma_a(0, kt2 + 2);
-    dma_b(0, kt2 + 2);
-    dma_b(1, kt2 + 2);
+    if constexpr (!DIM) {
+      dma_a(0, kt2 + 2);
+      dma_b(0, kt2 + 2);
+      dma_b(1, kt2 + 2);
+    }
     K64_STAMP(5);
     lgkm0();
-    vm_wait<2 * LA + LB2>();  // top, left, right (t+1)
+    vm_wait<DIM ? LA : 2 * LA + LB2>();  // top, left, right (t+1)
     K64_STAMP(6);
     bar();
     K64_STAMP(7);
-    mma(af, b1, 1, 1);
-    mma(af, b0, 1, 0);
+    if constexpr (DIM) {
+      mma2_dma(b1, 1, b0, 0, 1, [&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        if constexpr (p < LA) piece_a(0, kt2 + 2, p);
+        else if constexpr (BJ) piece_b(0, kt2 + 2, p - LA);
+        else piece_b((p - LA) / LB, kt2 + 2, (p - LA) % LB);
+      }, std::integral_constant<int, LA + LB2>{});
+    } else {
+      mma(af, b1, 1, 1);
+      mma(af, b0, 1, 0);
+    }
     mma_cs(af, 1);
     K64_STAMP(8);
     bar();
