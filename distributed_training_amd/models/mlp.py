@@ -9,7 +9,7 @@ training step has a dedicated fused gfx950 kernel (``ops/mlp_fused.py``).
 """
 from __future__ import annotations
 
-from typing import Any, List, Optional, Sequence, Union
+from typing import Any, List, Sequence, Union
 
 import torch
 import torch.nn as nn
