@@ -31,7 +31,7 @@ struct Args {
   int epi;
   bf16* db;  // weight-gradient groups: the bias gradient db[m] = sum_k A(m, k) (nullptr: none)
   const float* alpha_dev;  // nullptr, or a device scalar multiplying alpha (a loss scale known only on the GPU)
-#ifdef DTA_K64_STAMP
+#if defined(DTA_K64_STAMP) || defined(DTA_K64_TIMELINE)
   unsigned long long* stamps;  // diagnostic build only: per-wave cycle sums of the two-phase loop's segments
 #endif
 };

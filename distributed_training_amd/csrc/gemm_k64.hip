@@ -76,7 +76,7 @@ int dta_gemm_k64_sk_plan(int M, int N, int K, int tile, int* grid, int* span, in
   return tiles;
 }
 
-#ifdef DTA_K64_STAMP
+#if defined(DTA_K64_STAMP) || defined(DTA_K64_TIMELINE)
 unsigned long long* dta_k64_stamp_buf = nullptr;  // diagnostic build (scripts/k64_stamps.hip)
 #endif
 
@@ -158,7 +158,7 @@ hipError_t dta_gemm_k64(const void* a, int64_t lda, bool a_t, const void* b, int
   g.alpha = alpha;
   g.alpha_dev = alpha_dev;
   g.epi = epi;
-#ifdef DTA_K64_STAMP
+#if defined(DTA_K64_STAMP) || defined(DTA_K64_TIMELINE)
   g.stamps = dta_k64_stamp_buf;
 #endif
   if (tile & k64::kSK) {

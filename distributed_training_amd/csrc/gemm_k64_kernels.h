@@ -118,6 +118,27 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   } while (0)
 #endif
 
+#ifdef DTA_K64_TIMELINE
+// diagnostic build (scripts/k64_timeline.hip): per wave, the device real-time clock (100 MHz, one clock for
+// every CU) at kernel entry (0), after the K loop's prologue (1), after the K loop (2) and after the epilogue's
+// stores have drained (3), plus the wave's HW_ID (4) and XCC_ID (5) -- where a tile's time goes outside the loop
+__device__ __forceinline__ unsigned long long k64_rt() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define K64_TL(i, v)                                                                         \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0) g.stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6 + (i)] = (v); \
+  } while (0)
+#else
+#define K64_TL(i, v) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ bf16x4 tr4(const char* lds, int byte_off) {
   typedef short s4 __attribute__((ext_vector_type(4)));
   const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lds + byte_off));
@@ -463,6 +484,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   if constexpr (STAG) {
     if (lag) bar();
   }
+#ifdef DTA_K64_TIMELINE
+  K64_TL(1, k64_rt());
+#endif
 #ifdef DTA_K64_STAMP
   unsigned long long seg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_prev = stamp_now();
@@ -576,6 +600,9 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
 #endif
   }
   vm_wait<0>();  // the tail's dummy DMAs land before the workgroup's LDS is released
+#ifdef DTA_K64_TIMELINE
+  K64_TL(2, k64_rt());
+#endif
   if constexpr (STAG) {
     if (!lag) bar();  // equal barrier counts for both halves
   }
@@ -800,7 +827,21 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
 template <int BM, int BN, int WC, bool AT, bool BT, int PH, bool BUF, bool STG = false, bool DSW = false, int WR = 2>
 // (the 4-wave 128 x 192 tile held to 256 VGPRs: two workgroups per CU -- it took 272 otherwise)
 __global__ void __launch_bounds__(64 * WR * WC, BN == 192 ? 2 : 1) gemm_k64_kernel(Args g) {
+#ifdef DTA_K64_TIMELINE
+  const unsigned long long t_entry = k64_rt();
+#endif
   k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW, WR>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
+#ifdef DTA_K64_TIMELINE
+  vm_wait<0>();
+  const unsigned long long t_end = k64_rt();
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  K64_TL(0, t_entry);
+  K64_TL(3, t_end);
+  K64_TL(4, (unsigned long long)hw);
+  K64_TL(5, (unsigned long long)xcc);
+#endif
 }
 
 // Stream-K form (SkArgs): workgroup w (XCD-remapped: consecutive runs share an XCD's L2) walks the units
