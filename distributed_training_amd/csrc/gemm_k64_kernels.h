@@ -121,7 +121,8 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #ifdef DTA_K64_TIMELINE
 // diagnostic build (scripts/k64_timeline.hip): per wave, the device real-time clock (100 MHz, one clock for
 // every CU) at kernel entry (0), after the K loop's prologue (1), after the K loop (2) and after the epilogue's
-// stores have drained (3), plus the wave's HW_ID (4) and XCC_ID (5) -- where a tile's time goes outside the loop
+// stores have drained (3), plus the wave's HW_ID (4), XCC_ID (5) and the time its epilogue stores were all
+// issued (6) -- where a tile's time goes outside the loop (8 slots per wave)
 __device__ __forceinline__ unsigned long long k64_rt() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -131,7 +132,7 @@ __device__ __forceinline__ unsigned long long k64_rt() {
 }
 #define K64_TL(i, v)                                                                         \
   do {                                                                                     \
-    if ((threadIdx.x & 63) == 0) g.stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6 + (i)] = (v); \
+    if ((threadIdx.x & 63) == 0) g.stamps[((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (i)] = (v); \
   } while (0)
 #else
 #define K64_TL(i, v) \
@@ -832,8 +833,10 @@ __global__ void __launch_bounds__(64 * WR * WC, BN == 192 ? 2 : 1) gemm_k64_kern
 #endif
   k64_body<BM, BN, WC, AT, BT, PH, BUF, false, STG, DSW, WR>(g, xcd_remap(blockIdx.x, g.tiles_m * g.tiles_n));
 #ifdef DTA_K64_TIMELINE
+  const unsigned long long t_issued = k64_rt();  // (the epilogue's stores issued, not yet drained)
   vm_wait<0>();
   const unsigned long long t_end = k64_rt();
+  K64_TL(6, t_issued);
   unsigned hw, xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));

@@ -48,7 +48,7 @@ static int run(int M, int N, int K, bool at, bool bt) {
   CK(hipMalloc(&a, (size_t)M * K * 2));
   CK(hipMalloc(&b, (size_t)N * K * 2));
   CK(hipMalloc(&c, (size_t)M * N * 2));
-  CK(hipMalloc(&dta_k64_stamp_buf, (size_t)blocks * NW * 6 * 8));
+  CK(hipMalloc(&dta_k64_stamp_buf, (size_t)blocks * NW * 8 * 8));
   fill<<<1024, 256>>>(a, (int64_t)M * K, 1u, 1.f);
   fill<<<1024, 256>>>(b, (int64_t)N * K, 2u, 0.05f);
   const int64_t lda = at ? M : K, ldb = bt ? N : K;
@@ -71,19 +71,20 @@ static int run(int M, int N, int K, bool at, bool bt) {
     ts.push_back(ms * 1e3f);
   }
   std::sort(ts.begin(), ts.end());
-  std::vector<unsigned long long> h((size_t)blocks * NW * 6);  // the last launch's stamps
+  std::vector<unsigned long long> h((size_t)blocks * NW * 8);  // the last launch's stamps
   CK(hipMemcpy(h.data(), dta_k64_stamp_buf, h.size() * 8, hipMemcpyDeviceToHost));
   // per workgroup: wave 0's entry / loop start / loop end / end (the waves of a workgroup are within a barrier)
-  struct W { double t0, t1, t2, t3; unsigned long long cu; };
+  struct W { double t0, t1, t2, t3, ti; unsigned long long cu; };
   std::vector<W> w(blocks);
   unsigned long long tmin = ~0ull;
-  for (int bl = 0; bl < blocks; ++bl) tmin = std::min(tmin, h[(size_t)bl * NW * 6 + 0]);
+  for (int bl = 0; bl < blocks; ++bl) tmin = std::min(tmin, h[(size_t)bl * NW * 8 + 0]);
   for (int bl = 0; bl < blocks; ++bl) {
-    const unsigned long long* s = &h[(size_t)bl * NW * 6];
+    const unsigned long long* s = &h[(size_t)bl * NW * 8];
     const unsigned long long hw = s[4], xcc = s[5];
     // HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]; XCC_ID [3:0]
     const unsigned long long cu = ((xcc & 0xf) << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf);
-    w[bl] = {(s[0] - tmin) * 0.01, (s[1] - tmin) * 0.01, (s[2] - tmin) * 0.01, (s[3] - tmin) * 0.01, cu};
+    w[bl] = {(s[0] - tmin) * 0.01, (s[1] - tmin) * 0.01, (s[2] - tmin) * 0.01, (s[3] - tmin) * 0.01,
+             (s[6] - tmin) * 0.01, cu};
   }
   double span = 0;
   for (auto& x : w) span = std::max(span, x.t3);
@@ -91,7 +92,7 @@ static int run(int M, int N, int K, bool at, bool bt) {
   std::map<unsigned long long, std::vector<int>> per_cu;
   for (int bl = 0; bl < blocks; ++bl) per_cu[w[bl].cu].push_back(bl);
   const int R = 4;
-  double sum[R][6] = {};
+  double sum[R][7] = {};
   int cnt[R] = {};
   double gap_sum = 0;
   int gap_n = 0;
@@ -106,6 +107,7 @@ static int run(int M, int N, int K, bool at, bool bt) {
       sum[r][2] += x.t2 - x.t1;
       sum[r][3] += x.t3 - x.t2;
       sum[r][4] += x.t3;
+      sum[r][5] += x.ti - x.t2;
       cnt[r]++;
       if (i > 0) {
         gap_sum += x.t0 - w[v[i - 1]].t3;
@@ -120,9 +122,9 @@ static int run(int M, int N, int K, bool at, bool bt) {
   for (int r = 0; r < R; ++r) {
     if (!cnt[r]) continue;
     printf("%s{\"round\": %d, \"workgroups\": %d, \"entry_us\": %.2f, \"prologue_us\": %.2f, \"loop_us\": %.2f, "
-           "\"epilogue_us\": %.2f, \"end_us\": %.2f}",
+           "\"epilogue_us\": %.2f, \"epilogue_issue_us\": %.2f, \"end_us\": %.2f}",
            first ? "" : ", ", r + 1, cnt[r], sum[r][0] / cnt[r], sum[r][1] / cnt[r], sum[r][2] / cnt[r],
-           sum[r][3] / cnt[r], sum[r][4] / cnt[r]);
+           sum[r][3] / cnt[r], sum[r][5] / cnt[r], sum[r][4] / cnt[r]);
     first = false;
   }
   printf("]}\n");
@@ -135,7 +137,9 @@ static int run(int M, int N, int K, bool at, bool bt) {
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  (void)argc;
+  (void)argv;
   if (run(8192, 4096, 4096, false, false)) return 1;   // Llama o-proj forward (512 tiles: two rounds)
   if (run(8192, 4096, 14336, false, false)) return 1;  // down-proj forward (same tiles, 3.5x the K loop)
   if (run(8192, 28672, 4096, false, false)) return 1;  // gate/up forward (3584 tiles: 14 rounds)
