@@ -159,9 +159,9 @@ class GPT2(nn.Module):
         """Logits ``[B, S, V]``; with ``targets``, the mean token cross-entropy
         (LM head and loss fused: the logits are never materialised twice)."""
         B, S = idx.shape
-        pos = torch.arange(S, device=idx.device)
-        # (the token rows' gradient is added straight into the tied head's gradient slice)
-        x = lm.embedding(idx, self.wte.weight) + lm.embedding(pos, self.wpe.weight)
+        # (the token rows' gradient is added straight into the tied head's gradient slice; the
+        # positions 0..S-1 are wpe's first S rows: added as a view, no position ids)
+        x = lm.add_position(lm.embedding(idx, self.wte.weight), self.wpe.weight)
         h = None
         for blk in self.h:
             if self.activation_checkpointing and torch.is_grad_enabled():

@@ -1310,6 +1310,42 @@ def embedding(idx: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return F.embedding(idx, w)
 
 
+class _AddPosition(Function):
+    """``x + w[:S]`` for a learned absolute-position table ``w`` (GPT-2's ``wpe``): the
+    positions 0..S-1 are the table's first S rows, so they are read as a view -- no position
+    ids, no gather and, in the backward, no sort for the sorted-run embedding kernel (the
+    position-id form cost ~50 us per GPT-2 step: arange, gather, a 1024-key radix sort and
+    the run kernel).  The backward sums dy over the batch with one reduction written straight
+    into the table's gradient slice (rows past S zeroed)."""
+
+    @staticmethod
+    def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        ctx.S = x.shape[-2]
+        ctx.wparam = w
+        return x + w[: ctx.S]
+
+    @staticmethod
+    def backward(ctx: Any, dy: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
+        dw = None
+        if ctx.needs_input_grad[1]:
+            w, S = ctx.wparam, ctx.S
+            dw = _grad_dest(w)
+            if dw is None or not dw.is_contiguous():
+                dw = torch.empty_like(w)
+            torch.sum(dy.reshape(-1, S, w.shape[1]), 0, out=dw[:S])
+            if S < w.shape[0]:
+                dw[S:].zero_()
+        return (dy if ctx.needs_input_grad[0] else None), dw
+
+
+def add_position(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x [..., S, C] + w[:S]``: learned absolute positions added without position ids
+    (the GPU path writes the table's gradient in place, ``_AddPosition``)."""
+    if x.is_cuda and w.is_cuda:
+        return _AddPosition.apply(x, w)
+    return x + w[: x.shape[-2]]
+
+
 # ------------------------------------------------------------------ loss
 class _CrossEntropy(Function):
     @staticmethod

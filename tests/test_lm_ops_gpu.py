@@ -780,6 +780,23 @@ def test_embedding_backward_vs_fp32():
     assert w.grad[40:V - 1].abs().max().item() == 0
 
 
+def test_add_position_vs_fp32():
+    """x + w[:S] (learned positions as a view, no ids): forward exact, dx = dy, dw = dy summed over
+    the batch in rows < S and zero past S, against fp32 torch."""
+    torch.manual_seed(14)
+    P, S, C = 96, 80, 256
+    w = (torch.randn(P, C, device=DEV) * 0.02).bfloat16().requires_grad_()
+    x = torch.randn(3, S, C, device=DEV).bfloat16().requires_grad_()
+    y = lm.add_position(x, w)
+    assert torch.equal(y, x.detach() + w.detach()[:S])
+    dy = torch.randn(3, S, C, device=DEV).bfloat16()
+    y.backward(dy)
+    assert torch.equal(x.grad, dy)
+    ref = dy.float().sum(0)
+    assert _rel(w.grad[:S], ref) < 1e-2
+    assert w.grad[S:].abs().max().item() == 0
+
+
 def test_tied_embedding_gradient_accumulated_in_place():
     """GPT-2 under the DDP engine: the token rows are added into the tied head's gradient slice
     (no autograd sum); wte / wpe gradients match the same model without the engine."""
