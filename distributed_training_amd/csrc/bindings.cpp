@@ -26,6 +26,8 @@ hipError_t dta_colsum_batch(int, const float* const*, const int*, const int*, vo
 hipError_t dta_bias_grad(const void*, int64_t, int, float*, int, void*, int, hipStream_t);
 hipError_t dta_gelu_fwd(const void*, void*, int64_t, hipStream_t);
 hipError_t dta_gelu_bwd(const void*, const void*, void*, int64_t, hipStream_t);
+int dta_sort_ids_max();
+hipError_t dta_sort_ids(const int64_t*, int, int64_t, int64_t*, int64_t*, hipStream_t);
 hipError_t dta_embedding_bwd(const int64_t*, const int64_t*, const void*, void*, int, int, int64_t, int64_t,
                              hipStream_t);
 hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
@@ -562,6 +564,19 @@ void embedding_bwd_(torch::Tensor sid, torch::Tensor perm, torch::Tensor dy, tor
                            (int)sid.numel(), (int)dy.size(1), out.stride(0), out.size(0), pick_stream(stream)),
          "embedding_bwd_");
 }
+// stable sort of token ids (values in [0, V); others sort last as V) with their positions, in one workgroup
+// (csrc/sort_ids.hip): (sid, perm) as torch.sort(ids, stable=True) gives them, for embedding_bwd_
+std::vector<torch::Tensor> sort_ids(torch::Tensor ids, int64_t V, int64_t stream) {
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == torch::kLong && ids.dim() == 1 && ids.is_contiguous(),
+              "sort_ids: ids must be a contiguous int64 GPU vector");
+  TORCH_CHECK(ids.numel() >= 1 && ids.numel() <= dta_sort_ids_max(), "sort_ids: 1 .. ", dta_sort_ids_max(), " ids");
+  TORCH_CHECK(V >= 1 && V < ((int64_t)1 << 31), "sort_ids: vocabulary size");
+  auto sid = torch::empty_like(ids), perm = torch::empty_like(ids);
+  hip_ok(dta_sort_ids(ids.data_ptr<int64_t>(), (int)ids.numel(), V, sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
+                      pick_stream(stream)),
+         "sort_ids");
+  return {sid, perm};
+}
 torch::Tensor swiglu_fwd(torch::Tensor ab, int64_t stream) {
   check_bf16_2d(ab, "ab");
   const int64_t F2 = ab.size(-1), N = ab.numel() / F2;
@@ -1083,6 +1098,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("embedding_bwd_", &embedding_bwd_);
+  m.def("sort_ids", &sort_ids, py::arg("ids"), py::arg("V"), py::arg("stream") = -1);
+  m.def("sort_ids_max", &dta_sort_ids_max);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);

@@ -1265,6 +1265,17 @@ def _rows16(t: torch.Tensor) -> bool:
     return t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
 
 
+def _sorted_ids(ids: torch.Tensor, V: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(sorted ids, source positions) as ``torch.sort(ids, stable=True)``: one single-workgroup
+    launch (``csrc/sort_ids.hip``) up to ``sort_ids_max()`` ids -- GPT-2's 8192 token ids took
+    6-8 launches through torch.sort -- else torch.sort.  Ids outside [0, V) come back as V
+    (the run kernel skips them either way)."""
+    if ids.dtype == torch.long and ids.numel() <= native().sort_ids_max():
+        sid, perm = native().sort_ids(ids.contiguous(), V)
+        return sid, perm
+    return torch.sort(ids, stable=True)
+
+
 class _Embedding(Function):
     """``F.embedding`` whose backward is the deterministic sorted-run kernel of
     ``csrc/lm_ops.hip`` (no zero-filled dense gradient + scatter + add).  When the weight's
@@ -1285,7 +1296,7 @@ class _Embedding(Function):
         w = ctx.wparam
         if not ctx.needs_input_grad[1]:
             return None, None
-        sid, perm = torch.sort(idx.reshape(-1), stable=True)
+        sid, perm = _sorted_ids(idx.reshape(-1), w.shape[0])
         dy2 = dy.reshape(-1, w.shape[1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()

@@ -780,6 +780,25 @@ def test_embedding_backward_vs_fp32():
     assert w.grad[40:V - 1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("T,V", [(1, 7), (1000, 40), (8192, 50304), (12289, 50304), (16384, 65535)])
+def test_sort_ids_matches_torch(T, V):
+    """The single-workgroup id sort (csrc/sort_ids.hip) returns torch.sort(stable=True)'s ids and
+    positions bit for bit (many repeats: the order inside each run is the stability check); an id
+    outside [0, V) comes back as V."""
+    from distributed_training_amd.ops import native
+
+    g = torch.Generator(device="cpu").manual_seed(T)
+    ids = torch.randint(0, V, (T,), generator=g).to(DEV)
+    sid, perm = native().sort_ids(ids, V)
+    ref_s, ref_p = torch.sort(ids, stable=True)
+    assert torch.equal(sid, ref_s) and torch.equal(perm, ref_p)
+    if T > 2:
+        ids[1], ids[2] = -3, V + 5
+        sid, perm = native().sort_ids(ids, V)
+        assert torch.equal(sid[-2:], torch.full((2,), V, device=DEV))
+        assert sorted(perm[-2:].tolist()) == [1, 2]
+
+
 def test_add_position_vs_fp32():
     """x + w[:S] (learned positions as a view, no ids): forward exact, dx = dy, dw = dy summed over
     the batch in rows < S and zero past S, against fp32 torch."""
