@@ -33,6 +33,7 @@ hipError_t dta_embedding_bwd(const int64_t*, const int64_t*, const void*, void*,
 hipError_t dta_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
 hipError_t dta_swiglu_bwd(const void*, const void*, void*, int64_t, int, hipStream_t);
 hipError_t dta_rope(void*, const float*, const float*, int, int, int, int, int64_t, int64_t, float, hipStream_t);
+hipError_t dta_ce_mean(const float*, const int64_t*, int64_t, int64_t, float*, float*, hipStream_t);
 hipError_t dta_cross_entropy(const void*, void*, const int64_t*, float*, int64_t, int64_t, float, int64_t,
                              hipStream_t);
 hipError_t dta_attn_bwd(const dta::AttnArgs*, int, bool, hipStream_t);
@@ -626,6 +627,20 @@ torch::Tensor cross_entropy_fwd_bwd(torch::Tensor logits, torch::Tensor dlogits,
   return loss;
 }
 
+// mean of the CE rows over the non-ignored targets: (loss, count) f32 scalars, one launch (csrc/lm_ops.hip)
+std::vector<torch::Tensor> ce_mean(torch::Tensor rows, torch::Tensor target, int64_t ignore_index, int64_t stream) {
+  TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == torch::kFloat32 && rows.dim() == 1 && rows.is_contiguous(),
+              "ce_mean: rows f32 [N]");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous() &&
+                  target.numel() == rows.numel() && rows.numel() >= 1,
+              "ce_mean: target int64 [N]");
+  auto loss = torch::empty({}, rows.options()), count = torch::empty({}, rows.options());
+  hip_ok(dta_ce_mean(rows.data_ptr<float>(), target.data_ptr<int64_t>(), rows.numel(), ignore_index,
+                     loss.data_ptr<float>(), count.data_ptr<float>(), pick_stream(stream)),
+         "ce_mean");
+  return {loss, count};
+}
+
 // ----------------------------- RCCL -----------------------------
 ncclDataType_t nccl_dtype(const torch::Tensor& t) {
   switch (t.scalar_type()) {
@@ -1104,6 +1119,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope_", &rope_);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("ce_mean", &ce_mean, py::arg("rows"), py::arg("target"), py::arg("ignore_index"), py::arg("stream") = -1);
   m.def("bias_grad", &bias_grad, py::arg("dy"), py::arg("out_f32") = false, py::arg("stream") = -1);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("stream") = -1, py::arg("dq") = py::none(),

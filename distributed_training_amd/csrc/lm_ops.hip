@@ -693,9 +693,49 @@ __global__ void __launch_bounds__(128) embedding_bwd_kernel(const int64_t* __res
   }
 }
 
+// ---------------------------------------------------------------- CE mean
+// loss = sum(rows) / max(1, #(target != ignore)) and that divisor, in ONE single-workgroup launch (the
+// torch-op form -- compare, sum, clamp, casts, sum, divide -- was 7-9 launches, ~40 us per GPT-2 step).
+// Fixed reduction order (lane stride, then waves 0..15): the same bits every call.
+__global__ void __launch_bounds__(1024) ce_mean_kernel(const float* __restrict__ rows,
+                                                       const int64_t* __restrict__ target, int64_t N,
+                                                       int64_t ignore_index, float* __restrict__ loss,
+                                                       float* __restrict__ count) {
+  __shared__ float ps[16], pc[16];
+  float s = 0.f, c = 0.f;
+  for (int64_t i = threadIdx.x; i < N; i += 1024) {
+    s += rows[i];
+    c += target[i] != ignore_index ? 1.f : 0.f;
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0) {
+    ps[threadIdx.x >> 6] = s;
+    pc[threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float S = 0.f, C = 0.f;
+    for (int w = 0; w < 16; ++w) {
+      S += ps[w];
+      C += pc[w];
+    }
+    C = fmaxf(C, 1.f);
+    *loss = S / C;
+    *count = C;
+  }
+}
+
 }  // namespace dta
 
 using namespace dta;
+
+hipError_t dta_ce_mean(const float* rows, const int64_t* target, int64_t N, int64_t ignore_index, float* loss,
+                       float* count, hipStream_t st) {
+  if (N < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_mean_kernel, dim3(1), dim3(1024), 0, st, rows, target, N, ignore_index, loss, count);
+  return hipGetLastError();
+}
 
 template <bool RMS>
 static hipError_t norm_fwd_nv(int nv, const bf16* x, const bf16* w, const bf16* b, bf16* y, float* mean, float* rstd,

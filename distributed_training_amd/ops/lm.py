@@ -1358,15 +1358,23 @@ def add_position(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ loss
+def _ce_mean(loss_rows: torch.Tensor, target: torch.Tensor, ignore_index: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mean loss, count) with count = max(1, #(target != ignore_index)): f32 device scalars from ONE
+    launch (``csrc/lm_ops.hip`` ce_mean_kernel) -- no host sync, and none of the 7-9 small torch
+    launches of compare / sum / clamp / cast / sum / divide."""
+    loss, count = native().ce_mean(loss_rows, target.reshape(-1), ignore_index)
+    return loss, count
+
+
 class _CrossEntropy(Function):
     @staticmethod
     def forward(ctx: Any, logits: torch.Tensor, target: torch.Tensor, ignore_index: int) -> torch.Tensor:
         # no host sync: the valid-token count stays on the device
-        count = (target != ignore_index).sum().clamp_min(1).float()
         dlogits = torch.empty_like(logits)
         loss_rows = native().cross_entropy_fwd_bwd(logits, dlogits, target, 1.0, ignore_index, -1)
+        loss, count = _ce_mean(loss_rows, target, ignore_index)
         ctx.save_for_backward(dlogits, count)
-        return loss_rows.sum() / count
+        return loss
 
     @staticmethod
     def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
@@ -1386,12 +1394,12 @@ class _LinearCrossEntropy(Function):
     def forward(ctx: Any, x: torch.Tensor, w: torch.Tensor, target: torch.Tensor, ignore_index: int) -> torch.Tensor:
         x2 = x.reshape(-1, x.shape[-1])
         logits = gemm(x2, w, kind="head_fwd")
-        count = (target != ignore_index).sum().clamp_min(1).float()
         loss_rows = native().cross_entropy_fwd_bwd(logits, logits, target, 1.0, ignore_index, -1)
+        loss, count = _ce_mean(loss_rows, target, ignore_index)
         ctx.save_for_backward(x2, w, logits, count)
         ctx.xshape = x.shape
         ctx.wparam = w  # (its gradient may go straight into a flat gradient slice: _grad_dest)
-        return loss_rows.sum() / count
+        return loss
 
     @staticmethod
     def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:
@@ -1432,7 +1440,6 @@ class _ChunkedLinearCrossEntropy(Function):
         # grad: autograd records this call (needs_input_grad is set from requires_grad even under no_grad --
         # an evaluation forward must neither compute nor write gradients, least of all into an engine's slice)
         need_dx, need_dw = grad and ctx.needs_input_grad[0], grad and ctx.needs_input_grad[1]
-        count = (target != ignore_index).sum().clamp_min(1).float()
         loss_rows = torch.empty(T, dtype=torch.float32, device=x.device)
         buf = torch.empty(min(chunk, T), V, dtype=x.dtype, device=x.device)
         dx = torch.empty_like(x2) if need_dx else None
@@ -1465,12 +1472,13 @@ class _ChunkedLinearCrossEntropy(Function):
                 else:
                     dw.addmm_(lg.t(), xc)
         del buf
+        loss, count = _ce_mean(loss_rows, target, ignore_index)
         ctx.count = count
         ctx.dx, ctx.dw = dx, dw  # (this op's own results, not inputs or outputs: plain attributes)
         ctx.dw_final = dw_final
         ctx.xshape = x.shape
         ctx.wparam = w
-        return loss_rows.sum() / count
+        return loss
 
     @staticmethod
     def backward(ctx: Any, g: torch.Tensor) -> Tuple[Optional[torch.Tensor], ...]:

@@ -780,6 +780,26 @@ def test_embedding_backward_vs_fp32():
     assert w.grad[40:V - 1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("N", [1, 777, 8192, 70000])
+def test_ce_mean_matches_torch(N):
+    """The one-launch CE mean (csrc/lm_ops.hip ce_mean_kernel): sum(rows) / max(1, #valid) and the
+    count, against the torch-op form; every target ignored -> count 1; repeat calls bit-identical."""
+    from distributed_training_amd.ops import native
+
+    torch.manual_seed(N)
+    rows = torch.rand(N, device=DEV) * 10
+    tgt = torch.randint(0, 50, (N,), device=DEV)
+    tgt[::3] = -100
+    loss, count = native().ce_mean(rows, tgt, -100)
+    ref_c = (tgt != -100).sum().clamp_min(1).float()
+    assert count.item() == ref_c.item()
+    assert abs(loss.item() - (rows.double().sum() / ref_c.double()).item()) <= 1e-5 * max(1.0, loss.item())
+    loss2, _ = native().ce_mean(rows, tgt, -100)
+    assert torch.equal(loss, loss2)
+    _, c0 = native().ce_mean(rows, torch.full_like(tgt, -100), -100)
+    assert c0.item() == 1.0
+
+
 @pytest.mark.parametrize("T,V", [(1, 7), (1000, 40), (8192, 50304), (12289, 50304), (16384, 65535)])
 def test_sort_ids_matches_torch(T, V):
     """The single-workgroup id sort (csrc/sort_ids.hip) returns torch.sort(stable=True)'s ids and
