@@ -556,12 +556,17 @@ __host__ __device__ constexpr int ilv_fill_epp(int o) {
   return o < 2 * NA ? 16 / NA : 16 / NC;
 }
 
+// DTA_DKDV64_BM (diagnostic builds, scripts/attn_diag.hip): query rows per slice at D = 64 (32: three
+// waves per SIMD fit the registers and three workgroups per CU the LDS)
+#ifndef DTA_DKDV64_BM
+#define DTA_DKDV64_BM 64
+#endif
 template <int D>
 struct DkdvCfg {
-  static constexpr int kBM = 64;
-  static constexpr int kWavesPerSimd = D == 128 ? 1 : 2;
+  static constexpr int kBM = D == 64 ? DTA_DKDV64_BM : 64;
+  static constexpr int kWavesPerSimd = D == 128 ? 1 : (kBM == 32 ? 3 : 2);
   static constexpr int kPrefetch = DTA_DKDV_PF;  // MFMA ops between a fragment's LDS read and its use
-  static constexpr int kAhead = D == 64 ? 2 : 1;   // slices between a tile's global load and its LDS store
+  static constexpr int kAhead = D == 64 && kBM == 64 ? 2 : 1;  // slices between a tile's global load and its LDS store
 };
 
 // The backward of rotate-half RoPE on one lane's accumulator row (row `pos`, d = dt * 32 + 8 g + 4 hh + j):
