@@ -628,7 +628,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False,
         if alpha != 1.0:
             y.mul_(alpha)
         if scale_dev is not None:
-            y.mul_(scale_dev.to(y.dtype))
+            y.mul_(scale_dev)  # (one pass, the product in fp32: no separate cast of the scale)
         return y if bias is None else y.add_(bias)
 
     impl = 0
