@@ -87,25 +87,10 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef DTA_K64_DMA_IN_MFMA
 #define DTA_K64_DMA_IN_MFMA 0
 #endif
-// DTA_K64_M0 (probe builds): the buffer-DMA pieces own M0 (bglds16_m0: no save / restore around each piece,
-// whose restore waits for the piece to dispatch).
-#ifndef DTA_K64_M0
-#define DTA_K64_M0 0
-#endif
-// DTA_K64_RS (probe builds): the two-phase loop stages its half tiles through registers (buffer_load_dwordx4
-// one K-tile ahead, ds_write_b128 at the point the DMA piece was issued) instead of LDS-DMA.
-#ifndef DTA_K64_RS
-#define DTA_K64_RS 0
-#endif
-// DTA_K64_PRIO (probe builds): 0 = MFMA clusters at priority 1 (default); 1 = no s_setprio; 2 = the
-// two-phase loop's read phases (fragment reads + DMA issue) at priority 2 as well
-#ifndef DTA_K64_PRIO
-#define DTA_K64_PRIO 0
-#endif
-// DTA_K64_BAL (probe builds): the two-phase loop's DMA pieces balanced 4 / 4 over its read phases (B-right of
-// K-tile t + 1 moves from S3 of t - 1 to S1 of t, beside A-bottom) instead of 2 / 6
-#ifndef DTA_K64_BAL
-#define DTA_K64_BAL 0
+// DTA_K64_NOTAIL: the two-phase loop's last K-tiles issue no DMA for K-tiles past the end (they were DMA'd
+// from the last K-tile, never read, and drained before the epilogue); their waits become vmcnt(LA) / vmcnt(0)
+#ifndef DTA_K64_NOTAIL
+#define DTA_K64_NOTAIL 0
 #endif
 
 template <int N, int I = 0, typename F>
@@ -331,10 +316,6 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     }
   }
   const unsigned lds0 = lds_addr(lds);
-  auto dma16 = [&](__amdgpu_buffer_rsrc_t rs, unsigned vo, unsigned so, unsigned dst) __attribute__((always_inline)) {
-    if constexpr (DTA_K64_M0 != 0) bglds16_m0(rs, vo, so, dst);
-    else bglds16(rs, vo, so, dst);
-  };
   // LDS layout ILV: [A-top p0 | A-top p1 | A-bottom p0 | A-bottom p1 | B-left p0 | B-left p1 | B-right p0
   // | B-right p1] (p = K-tile parity): with the two-phase loop unrolled by two K-tiles the parity is a
   // compile-time constant and every fragment read is a loop-invariant lane base + an immediate offset
@@ -354,7 +335,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     if constexpr (BUF) {
       const unsigned so = (unsigned)(ks * stepA * 2), d0 = lds0 + aoff(h, kt & 1);
 #pragma unroll
-      for (int j = 0; j < LA; ++j) dma16(rsA, voA[h][j], so, d0 + (j * NW + wave) * 1024);
+      for (int j = 0; j < LA; ++j) bglds16(rsA, voA[h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < LA; ++j) glds16(srcA[h][j] + ks * stepA, dst + (j * NW + wave) * 1024);
@@ -367,7 +348,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     if constexpr (BUF) {
       const unsigned so = (unsigned)(ks * stepB * 2), d0 = lds0 + boff(h, kt & 1);
 #pragma unroll
-      for (int j = 0; j < LBG; ++j) dma16(rsB, voB[BJ ? 0 : h][j], so, d0 + (j * NW + wave) * 1024);
+      for (int j = 0; j < LBG; ++j) bglds16(rsB, voB[BJ ? 0 : h][j], so, d0 + (j * NW + wave) * 1024);
     } else {
 #pragma unroll
       for (int j = 0; j < LBG; ++j) glds16(srcB[BJ ? 0 : h][j] + ks * stepB, dst + (j * NW + wave) * 1024);
@@ -405,7 +386,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     for (int j = 0; j < 2 * MTH; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const bf16x8 (&af)[MTH][2], const bf16x8 (&bf)[NTH][2], int mh, int nh) {
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (DTA_K64_PRIO != 1) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -415,7 +396,7 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
           acc[nh * NTH + ii][mh * MTH + jj] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ii][kk], af[jj][kk], acc[nh * NTH + ii][mh * MTH + jj], 0,
                                                       0, 0);
-    if constexpr (DTA_K64_PRIO != 1) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
   // CS (tile column 0 of a weight-gradient problem): db[m] = sum_k A(m, k) from MFMAs against an
@@ -497,44 +478,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   // restages it.  (Round 3's first form waited vmcnt after the MFMA cluster, one barrier too late for
   // the leading group: wrong tiles on busy chips -- rel. error 0.17 on the 256x128 tile at 8192 x 4096 x
   // 4096, tests/test_gemm_k64_gpu.py.)  Each wait leaves 2LA + 2LB pieces in flight.
-  // RS: register-staged half tiles (DTA_K64_RS probe builds).  rb holds A-bottom of K-tile t + 1 (stored in
-  // S1 of t, then reloaded with t + 2), rt A-top and both B halves of K-tile t + 2 (stored in S3 of t, then
-  // reloaded with t + 3): every load has a whole K-tile (two MFMA clusters) to land, and each store sits where
-  // the DMA piece was issued, so the restaging rules below hold unchanged (a store is even retired, lgkmcnt,
-  // before its wave's next barrier).  The compiler counts these loads itself (no inline-asm DMA in the loop).
-  constexpr bool RS = DTA_K64_RS != 0 && BUF && DTA_K64_DMA_IN_MFMA == 0;
-  u32x4 rb[RS ? LA : 1], rt[RS ? LA + LB2 : 1];
-  auto ld_a = [&](int h, int kt, int j) __attribute__((always_inline)) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rsA, voA[h][j], (unsigned)((kofs + min(kt, nk - 1)) * stepA * 2), 0);
-  };
-  auto ld_b = [&](int p, int kt) __attribute__((always_inline)) {  // B piece p of LB2 (half p / LBG, piece p % LBG)
-    return __builtin_amdgcn_raw_buffer_load_b128(rsB, voB[BJ ? 0 : p / LBG][p % LBG],
-                                                 (unsigned)((kofs + min(kt, nk - 1)) * stepB * 2), 0);
-  };
-  auto st16 = [&](int off, const u32x4& v) __attribute__((always_inline)) {
-    *reinterpret_cast<u32x4*>(lds + off + 16 * lane) = v;
-  };
   dma_a(0, 0);
   dma_b(0, 0);
   dma_b(1, 0);
   dma_a(1, 0);
   dma_a(0, 1);
   dma_b(0, 1);
-  constexpr bool BAL = DTA_K64_BAL != 0 && !BJ && !RS && DTA_K64_DMA_IN_MFMA == 0;
-  if constexpr (!BAL) dma_b(1, 1);
-  if constexpr (BAL) {
-    vm_wait<2 * LA + LB>();  // K-tile 0 but its bottom half
-  } else if constexpr (RS) {
-    vm_wait<0>();
-#pragma unroll
-    for (int j = 0; j < LA; ++j) rb[j] = ld_a(1, 1, j);
-#pragma unroll
-    for (int j = 0; j < LA; ++j) rt[j] = ld_a(0, 2, j);
-#pragma unroll
-    for (int p = 0; p < LB2; ++p) rt[LA + p] = ld_b(p, 2);
-  } else {
-    vm_wait<2 * LA + LB2>();
-  }
+  dma_b(1, 1);
+  vm_wait<2 * LA + LB2>();
   bar();
   if constexpr (STAG) {
     if (lag) bar();
@@ -552,14 +503,15 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   // fewer in flight (S1: the previous S3's top / left / right; S3: the S1 bottom), three barrier
   // intervals after issue as before
   constexpr bool DIM = DTA_K64_DMA_IN_MFMA != 0;
+  constexpr bool NT = DTA_K64_NOTAIL != 0 && !DIM;
   auto piece_a = [&](int h, int kt, int j) {
     const int ks = kofs + min(kt, nk - 1);
-    if constexpr (BUF) dma16(rsA, voA[h][j], (unsigned)(ks * stepA * 2), lds0 + aoff(h, kt & 1) + (j * NW + wave) * 1024);
+    if constexpr (BUF) bglds16(rsA, voA[h][j], (unsigned)(ks * stepA * 2), lds0 + aoff(h, kt & 1) + (j * NW + wave) * 1024);
     else glds16(srcA[h][j] + ks * stepA, lds + aoff(h, kt & 1) + (j * NW + wave) * 1024);
   };
   auto piece_b = [&](int h, int kt, int j) {
     const int ks = kofs + min(kt, nk - 1);
-    if constexpr (BUF) dma16(rsB, voB[BJ ? 0 : h][j], (unsigned)(ks * stepB * 2), lds0 + boff(h, kt & 1) + (j * NW + wave) * 1024);
+    if constexpr (BUF) bglds16(rsB, voB[BJ ? 0 : h][j], (unsigned)(ks * stepB * 2), lds0 + boff(h, kt & 1) + (j * NW + wave) * 1024);
     else glds16(srcB[BJ ? 0 : h][j] + ks * stepB, lds + boff(h, kt & 1) + (j * NW + wave) * 1024);
   };
   // the 2 x (2 NTH MTH) MFMAs of mma(af, bx, mh, nhx) then mma(af, by, mh, nhy), with piece p of NP issued
@@ -589,25 +541,18 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   // P = -1: runtime parity (every tile but the buffer-DMA 256 x 256 one)
   auto ktile = [&](const int kt, auto P) {
     const int kt2 = decltype(P)::value < 0 ? kt : ((kt & ~1) | decltype(P)::value);
-    if constexpr (DTA_K64_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     read_a(af, kt2, 0);
     read_b(b0, kt2, 0);
     read_b(b1, kt2, 1);
-    if constexpr (RS) {
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < LA; ++j) st16(aoff(1, (kt2 + 1) & 1) + (j * NW + wave) * 1024, rb[j]);
-#pragma unroll
-      for (int j = 0; j < LA; ++j) rb[j] = ld_a(1, kt2 + 2, j);
-      __builtin_amdgcn_sched_barrier(0);
-    } else if constexpr (!DIM) {
-      dma_a(1, kt2 + 1);
-      if constexpr (BAL) dma_b(1, kt2 + 1);
+    // NT: K-tile t + 1 does not exist -- nothing to stage; bottom (t) is then the youngest piece in flight
+    const bool tail1 = NT && kt2 + 1 >= nk;
+    if constexpr (!DIM) {
+      if (!tail1) dma_a(1, kt2 + 1);
     }
     K64_STAMP(0);
     lgkm0();
-    if constexpr (BAL) vm_wait<2 * LA + 2 * LB>();  // bottom (t)
-    else if constexpr (!RS) vm_wait<DIM ? LA + LB2 : 2 * LA + LB2>();  // bottom (t)
+    if (tail1) vm_wait<0>();
+    else vm_wait<DIM ? LA + LB2 : 2 * LA + LB2>();  // bottom (t)
     K64_STAMP(1);
     bar();
     K64_STAMP(2);
@@ -622,28 +567,22 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     K64_STAMP(3);
     bar();
     K64_STAMP(4);
-    if constexpr (DTA_K64_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     read_a(af, kt2, 1);
-    if constexpr (RS) {
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < LA; ++j) st16(aoff(0, kt2 & 1) + (j * NW + wave) * 1024, rt[j]);
-#pragma unroll
-      for (int p = 0; p < LB2; ++p) st16(boff(BJ ? 0 : p / LBG, kt2 & 1) + ((p % LBG) * NW + wave) * 1024, rt[LA + p]);
-#pragma unroll
-      for (int j = 0; j < LA; ++j) rt[j] = ld_a(0, kt2 + 3, j);
-#pragma unroll
-      for (int p = 0; p < LB2; ++p) rt[LA + p] = ld_b(p, kt2 + 3);
-      __builtin_amdgcn_sched_barrier(0);
-    } else if constexpr (!DIM) {
-      dma_a(0, kt2 + 2);
-      dma_b(0, kt2 + 2);
-      if constexpr (!BAL) dma_b(1, kt2 + 2);
+    // NT: no K-tile t + 2 to stage; the wait then leaves only bottom (t+1) of this K-tile's S1 in flight
+    // (none past the last K-tile)
+    const bool tail2 = NT && kt2 + 2 >= nk;
+    if constexpr (!DIM) {
+      if (!tail2) {
+        dma_a(0, kt2 + 2);
+        dma_b(0, kt2 + 2);
+        dma_b(1, kt2 + 2);
+      }
     }
     K64_STAMP(5);
     lgkm0();
-    if constexpr (BAL) vm_wait<LA + LB>();  // top, left (t+1) and right (t+1), issued in this K-tile's S1
-    else if constexpr (!RS) vm_wait<DIM ? LA : 2 * LA + LB2>();  // top, left, right (t+1)
+    if (!tail2) vm_wait<DIM ? LA : 2 * LA + LB2>();  // top, left, right (t+1)
+    else if (kt2 + 1 < nk) vm_wait<DIM ? 0 : LA>();
+    else vm_wait<0>();
     K64_STAMP(6);
     bar();
     K64_STAMP(7);

@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
     if (run(tag, 1024, 768, 1536, l[0], l[1], true)) return 1;
   for (auto& l : lays)
     if (run(tag, 1024, 512, 64, l[0], l[1], true)) return 1;
-  const int shapes[2][3] = {{8192, 28672, 4096}, {8192, 4096, 4096}};
+  const int shapes[4][3] = {{8192, 28672, 4096}, {8192, 4096, 4096}, {8192, 3072, 768}, {8192, 2304, 768}};
   for (auto& s : shapes)
     for (auto& l : lays)
       if (run(tag, s[0], s[1], s[2], l[0], l[1], false)) return 1;
