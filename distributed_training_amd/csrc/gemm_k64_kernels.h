@@ -87,11 +87,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #ifndef DTA_K64_DMA_IN_MFMA
 #define DTA_K64_DMA_IN_MFMA 0
 #endif
-// DTA_K64_NOTAIL: the two-phase loop's last K-tiles issue no DMA for K-tiles past the end (they were DMA'd
-// from the last K-tile, never read, and drained before the epilogue); their waits become vmcnt(LA) / vmcnt(0)
-#ifndef DTA_K64_NOTAIL
-#define DTA_K64_NOTAIL 0
-#endif
 
 template <int N, int I = 0, typename F>
 __device__ __forceinline__ void k64_static_for(F&& f) {
@@ -503,7 +498,6 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
   // fewer in flight (S1: the previous S3's top / left / right; S3: the S1 bottom), three barrier
   // intervals after issue as before
   constexpr bool DIM = DTA_K64_DMA_IN_MFMA != 0;
-  constexpr bool NT = DTA_K64_NOTAIL != 0 && !DIM;
   auto piece_a = [&](int h, int kt, int j) {
     const int ks = kofs + min(kt, nk - 1);
     if constexpr (BUF) bglds16(rsA, voA[h][j], (unsigned)(ks * stepA * 2), lds0 + aoff(h, kt & 1) + (j * NW + wave) * 1024);
@@ -544,15 +538,10 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     read_a(af, kt2, 0);
     read_b(b0, kt2, 0);
     read_b(b1, kt2, 1);
-    // NT: K-tile t + 1 does not exist -- nothing to stage; bottom (t) is then the youngest piece in flight
-    const bool tail1 = NT && kt2 + 1 >= nk;
-    if constexpr (!DIM) {
-      if (!tail1) dma_a(1, kt2 + 1);
-    }
+    if constexpr (!DIM) dma_a(1, kt2 + 1);
     K64_STAMP(0);
     lgkm0();
-    if (tail1) vm_wait<0>();
-    else vm_wait<DIM ? LA + LB2 : 2 * LA + LB2>();  // bottom (t)
+    vm_wait<DIM ? LA + LB2 : 2 * LA + LB2>();  // bottom (t)
     K64_STAMP(1);
     bar();
     K64_STAMP(2);
@@ -568,21 +557,14 @@ __device__ __forceinline__ void k64_body(const Args& g, const int t, const int k
     bar();
     K64_STAMP(4);
     read_a(af, kt2, 1);
-    // NT: no K-tile t + 2 to stage; the wait then leaves only bottom (t+1) of this K-tile's S1 in flight
-    // (none past the last K-tile)
-    const bool tail2 = NT && kt2 + 2 >= nk;
     if constexpr (!DIM) {
-      if (!tail2) {
-        dma_a(0, kt2 + 2);
-        dma_b(0, kt2 + 2);
-        dma_b(1, kt2 + 2);
-      }
+      dma_a(0, kt2 + 2);
+      dma_b(0, kt2 + 2);
+      dma_b(1, kt2 + 2);
     }
     K64_STAMP(5);
     lgkm0();
-    if (!tail2) vm_wait<DIM ? LA : 2 * LA + LB2>();  // top, left, right (t+1)
-    else if (kt2 + 1 < nk) vm_wait<DIM ? 0 : LA>();
-    else vm_wait<0>();
+    vm_wait<DIM ? LA : 2 * LA + LB2>();  // top, left, right (t+1)
     K64_STAMP(6);
     bar();
     K64_STAMP(7);
